@@ -1,0 +1,116 @@
+"""ctypes binding of libemrifd.so (the C ABI declared in include/emrifd.h).
+
+This is the only way the package reaches its compute path. There is deliberately no CPU
+fallback: if the HIP library is missing or no GPU is visible, calls raise.
+"""
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libemrifd.so")
+
+EFD_OK = 0
+EFD_ERR_ARG = -1
+EFD_ERR_HIP = -2
+EFD_ERR_WORKSPACE = -3
+EFD_CAUSTIC_SPA = 0
+EFD_CAUSTIC_UNIFORM = 1
+EFD_LOGLIKE_SCRATCH = 1024
+
+# every symbol include/emrifd.h declares (tests check the library exports all of them)
+EXPORTED_SYMBOLS = (
+    "efd_version",
+    "efd_last_error",
+    "efd_spline_build",
+    "efd_modesum_workspace_bytes",
+    "efd_modesum",
+    "efd_modesum_status",
+    "efd_modesum_contributions",
+    "efd_polarizations",
+    "efd_loglike",
+)
+
+
+class ModesumArgs(ctypes.Structure):
+    """Mirror of `efd_modesum_args` (include/emrifd.h)."""
+
+    _fields_ = [
+        ("t", ctypes.c_void_p),
+        ("phi_phi", ctypes.c_void_p),
+        ("phi_r", ctypes.c_void_p),
+        ("f_phi", ctypes.c_void_p),
+        ("f_r", ctypes.c_void_p),
+        ("nt", ctypes.c_int32),
+        ("amp", ctypes.c_void_p),
+        ("m", ctypes.c_void_p),
+        ("n", ctypes.c_void_p),
+        ("ylm_p", ctypes.c_void_p),
+        ("ylm_m", ctypes.c_void_p),
+        ("K", ctypes.c_int32),
+        ("freq", ctypes.c_void_p),
+        ("nf", ctypes.c_int64),
+        ("grid_symmetric", ctypes.c_int32),
+        ("scale_re", ctypes.c_double),
+        ("scale_im", ctypes.c_double),
+        ("caustic", ctypes.c_int32),
+        ("accumulate", ctypes.c_int32),
+        ("out", ctypes.c_void_p),
+    ]
+
+
+class EFDError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load libemrifd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EFDError(
+            f"HIP library {p} not found: build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(p)
+    vp, i32, i64, dbl, sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
+                             ctypes.c_size_t)
+    lib.efd_version.restype = ctypes.c_int
+    lib.efd_version.argtypes = []
+    lib.efd_last_error.restype = ctypes.c_int
+    lib.efd_last_error.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.efd_spline_build.restype = ctypes.c_int
+    lib.efd_spline_build.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
+    lib.efd_modesum_workspace_bytes.restype = sz
+    lib.efd_modesum_workspace_bytes.argtypes = [i32, i32, i64, i64]
+    lib.efd_modesum.restype = ctypes.c_int
+    lib.efd_modesum.argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
+    lib.efd_modesum_status.restype = ctypes.c_int
+    lib.efd_modesum_status.argtypes = [vp, ctypes.POINTER(i64), vp]
+    lib.efd_modesum_contributions.restype = ctypes.c_int
+    lib.efd_modesum_contributions.argtypes = [vp, ctypes.POINTER(i64), vp]
+    lib.efd_polarizations.restype = ctypes.c_int
+    lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
+    lib.efd_loglike.restype = ctypes.c_int
+    lib.efd_loglike.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
+    _ = dbl
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error(lib=None):
+    lib = lib or load()
+    buf = ctypes.create_string_buffer(512)
+    lib.efd_last_error(buf, 512)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc, what, lib=None):
+    if rc != EFD_OK:
+        raise EFDError(f"{what} failed ({rc}): {last_error(lib)}")
+    return rc

@@ -1,0 +1,1139 @@
+// emrifd.hip -- MI355X (gfx950, CDNA4) FD EMRI mode-sum: kernels + C ABI (include/emrifd.h).
+//
+// Hot path (BASELINE.json:north_star): for every
+// selected harmonic k = (l, m, n) of the sparse inspiral, the stationary-phase spectrum
+//   S(f) = - scale * sum_k [ Y+_k z_k(g) at f = -g ,  Y-_k conj(z_k(g)) at f = +g ]
+//   z_k(g) = A_k(t) Q(F', F'') exp(i (2 pi g t - Phi_k(t))),  t = t_k(g) (inverse spline)
+// restated from the reference notebook FD_waveform (Tutorial_FD_construction_single_mode.ipynb
+// :552-623): Phi_k = m Phi_phi + n Phi_r (:558), F_k = m f_phi + n f_r (:564), t(f) from the
+// inverse spline CubicSpline(F, t) (:566), supports (:569-572), F' and F'' spline derivatives
+// (:579-584), amplitude spline (:587-594), K_{1/3} factor (:599-613), phases (:615-616).
+// The oracle (oracle/fd_oracle.py) states the same maths in numpy; tests pin them together.
+//
+// Pipeline (all on one stream, no host sync, no allocation):
+//   K1 k_traj_splines     1 wave: not-a-knot splines of Phi_phi, Phi_r, f_phi, f_r and of the
+//                         knot derivatives f_phi'(t_i), f_r'(t_i) (for F'' as in notebook :583)
+//   K2 k_spline_shared    1 lane per amplitude interpolant (Re/Im A_k): 2K lanes
+//   K3 k_inverse_splines  1 lane per harmonic: F knots, monotonic runs, inverse spline per run
+//   K4 k_items            1 thread per (harmonic, knot interval): gathers every cubic the SPA
+//                         needs for that interval into one 256-B record + its bin (lane) ranges
+//   K5 k_segments         1 thread per (harmonic, run, branch): lane range, per-tile counts
+//   K6 k_scan             exclusive scan of per-tile counts
+//   K7 k_fill             per-tile lists of (segment, first interval) entries
+//   K8 k_modesum          OUTPUT-STATIONARY: one 256-lane workgroup per tile of frequency bins;
+//                         each lane owns one bin (and its mirror -f when the grid is symmetric:
+//                         the +m branch and its -m partner share t(g), the amplitude/phase
+//                         splines and sin/cos, so one evaluation feeds two bins); the tile's
+//                         harmonic list is sorted in LDS (deterministic summation order),
+//                         interval records are read with scalar loads (wave-uniform), and
+//                         results are written once -- no atomics on the spectrum.
+// The SPA evaluation is FP64 VALU work (phases reach ~1e7 rad); MFMA is not applicable.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/emrifd.h"
+
+#define EFD_VERSION 100  // 0.1.0
+
+namespace {
+
+constexpr int TILE = 256;           // frequency bins (lanes) per workgroup in k_modesum
+constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
+constexpr int MAX_NT = 2048;        // knots (FEW max_init_len is 1000)
+constexpr int LDS_SORT_CAP = 4096;  // tile-list entries sorted in LDS
+constexpr double PI = 3.141592653589793238462643383279502884;
+constexpr double TWO_PI = 6.283185307179586476925286766559005768;
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(EFD_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ----------------------------------------------------------------------------------------
+// Data layouts in HBM
+// ----------------------------------------------------------------------------------------
+
+// One record per (harmonic h, forward knot interval j): everything the SPA needs on the
+// bins whose t(g) falls in [t_j, t_{j+1}). 256 B, read with scalar (SMEM) loads.
+struct __attribute__((aligned(16))) Item {
+    double gx;        // left end of the inverse-spline interval (ascending F)
+    double ic[4];     // t(g) = ((ic0 u + ic1) u + ic2) u + ic3, u = g - gx
+    double tj, tj1;   // forward interval
+    double ar[4];     // Re A(t), w = t - tj (c0 highest power, scipy PPoly order)
+    double ai[4];     // Im A(t)
+    double ph[4];     // Phi_k(t) = m Phi_phi + n Phi_r
+    double fd[3];     // F'(t)
+    double fdd[3];    // F''(t): derivative of the spline of F'(t_i) (notebook :583)
+    double yp[2];     // -scale * Y+        (parent branch, f = -g)
+    double ym[2];     // -scale * Y-        (partner branch, f = +g)
+    int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
+    int32_t flags;    // bit0: interval part of a run; bit1: has partner (m != 0)
+    int32_t h;
+};
+static_assert(sizeof(Item) == 256, "Item must be 256 B");
+
+// One record per (harmonic, monotonic run, sub-branch s).
+struct __attribute__((aligned(16))) Seg {
+    int32_t h, ja, jb;   // run covers forward intervals [ja, jb)
+    int32_t s;           // sub-branch: s = 0 -> g = -f_k, s = 1 -> g = +f_k
+    int32_t dir;         // lane order walks intervals with j += dir
+    int32_t klo, khi;    // lane range of the whole segment
+    int32_t partner;     // 1 if the harmonic has a -m partner
+};
+static_assert(sizeof(Seg) == 32, "Seg must be 32 B");
+
+struct Header {
+    int64_t needed;       // incidences required by the last call
+    int64_t capacity;     // incidences the workspace holds
+    int64_t contributions;
+    int64_t nsegs;
+    int64_t pad[4];
+};
+
+struct Layout {
+    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, segs, counts, offsets,
+        cursor, entries, total;
+    int64_t ntiles, nlanes, capacity;
+};
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+Layout make_layout(int32_t nt, int32_t K, int64_t nf, int64_t capacity, int paired) {
+    Layout L{};
+    const int64_t ni = nt - 1;
+    L.nlanes = paired ? (nf + 1) / 2 : nf;
+    L.ntiles = (L.nlanes + TILE - 1) / TILE;
+    L.capacity = capacity;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
+    L.header = take(sizeof(Header));
+    L.coefA = take(sizeof(double) * ni * 4 * 2 * K);
+    L.coefT = take(sizeof(double) * ni * 4 * 8);
+    L.kslope = take(sizeof(double) * nt * 2);
+    L.tscratch = take(sizeof(double) * nt * 16);
+    L.invcp = take(sizeof(double) * nt * K);
+    L.invdp = take(sizeof(double) * nt * K);
+    L.runs = take(sizeof(int32_t) * 4 * MAXRUNS * K);
+    L.items = take(sizeof(Item) * ni * K);
+    L.segs = take(sizeof(Seg) * 2 * MAXRUNS * K);
+    L.counts = take(sizeof(int32_t) * (L.ntiles + 1));
+    L.offsets = take(sizeof(int32_t) * (L.ntiles + 1));
+    L.cursor = take(sizeof(int32_t) * (L.ntiles + 1));
+    L.entries = take(sizeof(uint64_t) * capacity);
+    L.total = off;
+    return L;
+}
+
+// ----------------------------------------------------------------------------------------
+// Not-a-knot cubic spline solve (scipy.interpolate.CubicSpline semantics)
+// ----------------------------------------------------------------------------------------
+// Slopes s_i solve the tridiagonal system of scipy/_cubic.py (rows 0 and n-1 encode the
+// not-a-knot end conditions); coefficients follow scipy's PPoly construction:
+//   tt = (s_i + s_{i+1} - 2 slope_i)/dx_i; c0 = tt/dx_i; c1 = (slope_i - s_i)/dx_i - tt;
+//   c2 = s_i; c3 = y_i.
+// X(i), Y(i) load knot i; CP/DP are per-lane scratch accessors; OUT(i, c, v) stores.
+template <class FX, class FY, class FCP, class FDP, class FOUT>
+__device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
+    if (n < 2) return;
+    if (n == 2) {
+        const double dx = X(1) - X(0);
+        const double slope = (Y(1) - Y(0)) / dx;
+        OUT(0, 0, 0.0); OUT(0, 1, 0.0); OUT(0, 2, slope); OUT(0, 3, Y(0));
+        return;
+    }
+    if (n == 3) {  // parabola through the three points (scipy special case)
+        const double dx0 = X(1) - X(0), dx1 = X(2) - X(1);
+        const double y0 = Y(0), y1 = Y(1), y2 = Y(2);
+        const double sl0 = (y1 - y0) / dx0, sl1 = (y2 - y1) / dx1;
+        const double s1 = (dx0 * sl1 + dx1 * sl0) / (dx0 + dx1);
+        const double s0 = 2.0 * sl0 - s1, s2 = 2.0 * sl1 - s1;
+        double tt = (s0 + s1 - 2.0 * sl0) / dx0;
+        OUT(0, 0, tt / dx0); OUT(0, 1, (sl0 - s0) / dx0 - tt); OUT(0, 2, s0); OUT(0, 3, y0);
+        tt = (s1 + s2 - 2.0 * sl1) / dx1;
+        OUT(1, 0, tt / dx1); OUT(1, 1, (sl1 - s1) / dx1 - tt); OUT(1, 2, s1); OUT(1, 3, y1);
+        return;
+    }
+    // forward sweep (Thomas); row 0
+    double x0 = X(0), x1 = X(1), x2 = X(2);
+    double y0 = Y(0), y1 = Y(1), y2 = Y(2);
+    double dxm = x1 - x0, dxi = x2 - x1;          // dx_{i-1}, dx_i at i = 1
+    double slm = (y1 - y0) / dxm, sli = (y2 - y1) / dxi;
+    {
+        const double d = x2 - x0;
+        const double b0 = dxi, c0 = d;
+        const double r0 = ((dxm + 2.0 * d) * dxi * slm + dxm * dxm * sli) / d;
+        CP(0) = c0 / b0;
+        DP(0) = r0 / b0;
+    }
+    double cpm = CP(0), dpm = DP(0);
+    double xi = x2, yi = y2;
+    for (int i = 1; i <= n - 2; ++i) {
+        // row i: a = dx_i, b = 2(dx_{i-1} + dx_i), c = dx_{i-1}, r = 3(dx_i sl_{i-1} + dx_{i-1} sl_i)
+        const double a = dxi, b = 2.0 * (dxm + dxi), c = dxm;
+        const double r = 3.0 * (dxi * slm + dxm * sli);
+        const double mm = b - a * cpm;
+        cpm = c / mm;
+        dpm = (r - a * dpm) / mm;
+        CP(i) = cpm;
+        DP(i) = dpm;
+        if (i + 2 <= n - 1) {
+            const double xn = X(i + 2), yn = Y(i + 2);
+            dxm = dxi; slm = sli;
+            dxi = xn - xi; sli = (yn - yi) / dxi;
+            xi = xn; yi = yn;
+        }
+    }
+    // last row (scipy: A[1,-1] = dx[-2], A[-1,-2] = x[-1] - x[-3]): a = x_{n-1} - x_{n-3},
+    // b = dx_{n-3}; here dxm = dx_{n-3}, dxi = dx_{n-2}, slm = sl_{n-3}, sli = sl_{n-2}
+    double s_next;
+    {
+        const double d = dxm + dxi;  // x_{n-1} - x_{n-3}
+        const double a = X(n - 1) - X(n - 3);
+        const double b = dxm;
+        const double r = (dxi * dxi * slm + (2.0 * d + dxi) * dxm * sli) / d;
+        const double mm = b - a * cpm;
+        s_next = (r - a * dpm) / mm;
+    }
+    // back substitution, emitting interval coefficients from the right
+    double xr = X(n - 1), yr = Y(n - 1);
+    for (int i = n - 2; i >= 0; --i) {
+        const double s_i = DP(i) - CP(i) * s_next;
+        const double xl = X(i), yl = Y(i);
+        const double dx = xr - xl;
+        const double sl = (yr - yl) / dx;
+        const double tt = (s_i + s_next - 2.0 * sl) / dx;
+        OUT(i, 0, tt / dx);
+        OUT(i, 1, (sl - s_i) / dx - tt);
+        OUT(i, 2, s_i);
+        OUT(i, 3, yl);
+        s_next = s_i;
+        xr = xl; yr = yl;
+    }
+}
+
+// derivative of a cubic piece at w (scipy evaluates c2 + 2 c1 w + 3 c0 w^2 by power sum)
+__device__ __forceinline__ double dcubic(const double* c, double w) {
+    return (c[2] + (2.0 * c[1]) * w) + (3.0 * c[0]) * (w * w);
+}
+
+// ----------------------------------------------------------------------------------------
+// K1: trajectory splines (one wave; lanes 0..3 the knot data, then lanes 4..5 the slopes)
+// coefT layout: [interval][coef c][q], q: 0 Phi_phi, 1 Phi_r, 2 f_phi, 3 f_r, 4 f_phi', 5 f_r'
+// ----------------------------------------------------------------------------------------
+__global__ void k_traj_splines(const double* __restrict__ t, const double* __restrict__ phi_phi,
+                               const double* __restrict__ phi_r, const double* __restrict__ f_phi,
+                               const double* __restrict__ f_r, int nt, double* __restrict__ coefT,
+                               double* __restrict__ kslope, double* __restrict__ scratch) {
+    const int q = threadIdx.x;
+    double* cp = scratch + (size_t)q * nt;
+    double* dp = scratch + (size_t)(8 + q) * nt;
+    auto X = [&](int i) { return t[i]; };
+    auto CP = [&](int i) -> double& { return cp[i]; };
+    auto DP = [&](int i) -> double& { return dp[i]; };
+    if (q < 4) {
+        const double* y = q == 0 ? phi_phi : (q == 1 ? phi_r : (q == 2 ? f_phi : f_r));
+        auto Y = [&](int i) { return y[i]; };
+        auto OUT = [&](int i, int c, double v) { coefT[((size_t)i * 4 + c) * 8 + q] = v; };
+        spline_not_a_knot(nt, X, Y, CP, DP, OUT);
+    }
+    __syncthreads();
+    // knot values of f_phi'(t) and f_r'(t), evaluated like scipy's derivative PPoly at the knots
+    if (q < 2) {
+        const int qq = 2 + q;
+        for (int i = 0; i < nt; ++i) {
+            double v;
+            if (i < nt - 1) {
+                v = coefT[((size_t)i * 4 + 2) * 8 + qq];
+            } else {
+                double c[4];
+                for (int cc = 0; cc < 4; ++cc) c[cc] = coefT[((size_t)(nt - 2) * 4 + cc) * 8 + qq];
+                v = dcubic(c, t[nt - 1] - t[nt - 2]);
+            }
+            kslope[(size_t)q * nt + i] = v;
+        }
+    }
+    __syncthreads();
+    if (q >= 4 && q < 6) {
+        const double* y = kslope + (size_t)(q - 4) * nt;
+        auto Y = [&](int i) { return y[i]; };
+        auto OUT = [&](int i, int c, double v) { coefT[((size_t)i * 4 + c) * 8 + q] = v; };
+        spline_not_a_knot(nt, X, Y, CP, DP, OUT);
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// K2: shared-knot splines of the amplitudes, one lane per interpolant (Re/Im of each harmonic).
+// y is knot-major [n][ninterp] (FEW's teuk_modes[N_t][K] complex layout), coef [n-1][4][ninterp].
+// ----------------------------------------------------------------------------------------
+__global__ void k_spline_shared(const double* __restrict__ x, int n, const double* __restrict__ y,
+                                int ninterp, double* coef, int64_t scratch_stride) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= ninterp) return;
+    // Thomas scratch CP(i), DP(i) (rows i <= n-2) live in the c0 / c1 slots of interval i of
+    // the output itself: the back substitution reads CP(i), DP(i) before it writes interval i,
+    // and the forward sweep never reads an interval the back substitution has written.
+    double* cpbuf = coef;
+    double* dpbuf = coef + ninterp;
+    auto X = [&](int i) { return x[i]; };
+    auto Y = [&](int i) { return y[(size_t)i * ninterp + q]; };
+    auto CP = [&](int i) -> double& { return cpbuf[(size_t)i * scratch_stride + q]; };
+    auto DP = [&](int i) -> double& { return dpbuf[(size_t)i * scratch_stride + q]; };
+    auto OUT = [&](int i, int c, double v) { coef[((size_t)i * 4 + c) * ninterp + q] = v; };
+    spline_not_a_knot(n, X, Y, CP, DP, OUT);
+}
+
+// ----------------------------------------------------------------------------------------
+// K3: inverse splines t(F) per monotonic run, one lane per harmonic
+// runs[h][r] = (ja, jb, sign, 0): forward intervals [ja, jb), F increasing (+1)/decreasing (-1)
+// Item.gx / Item.ic are filled for the intervals of each run.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ double knotF(const double* f_phi, const double* f_r, int m, int n,
+                                        int i) {
+    // numpy's m * f_phi + n * f_r, rounded the same way (no FMA contraction)
+    return __dadd_rn(__dmul_rn((double)m, f_phi[i]), __dmul_rn((double)n, f_r[i]));
+}
+
+__global__ void k_inverse_splines(const double* __restrict__ t, const double* __restrict__ f_phi,
+                                  const double* __restrict__ f_r, const int32_t* __restrict__ marr,
+                                  const int32_t* __restrict__ narr, int nt, int K,
+                                  int32_t* __restrict__ runs, Item* __restrict__ items,
+                                  double* __restrict__ cpbuf, double* __restrict__ dpbuf,
+                                  int32_t* __restrict__ err) {
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= K) return;
+    const int m = marr[h], n = narr[h];
+    const int ni = nt - 1;
+    Item* it = items + (size_t)h * ni;
+    int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
+    for (int r = 0; r < MAXRUNS; ++r) { rr[4 * r] = 0; rr[4 * r + 1] = 0; rr[4 * r + 2] = 0; }
+    int nrun = 0;
+    int j = 0;
+    double Fprev = knotF(f_phi, f_r, m, n, 0);
+    // scan the interval signs and emit maximal strictly monotonic runs
+    int cur_sign = 0, ja = 0;
+    for (j = 0; j <= ni; ++j) {
+        int sg = 0;
+        double Fn = 0.0;
+        if (j < ni) {
+            Fn = knotF(f_phi, f_r, m, n, j + 1);
+            sg = (Fn > Fprev) ? 1 : ((Fn < Fprev) ? -1 : 0);
+        }
+        if (sg != cur_sign || j == ni) {
+            if (cur_sign != 0) {  // close run [ja, j)
+                if (nrun < MAXRUNS) {
+                    rr[4 * nrun] = ja; rr[4 * nrun + 1] = j; rr[4 * nrun + 2] = cur_sign;
+                    ++nrun;
+                } else {
+                    atomicOr(err, 1);
+                }
+            }
+            cur_sign = sg;
+            ja = j;
+        }
+        Fprev = Fn;
+    }
+    // inverse spline per run: x = F ascending, y = t
+    for (int r = 0; r < nrun; ++r) {
+        const int a = rr[4 * r], b = rr[4 * r + 1], sg = rr[4 * r + 2];
+        const int npts = b - a + 1;
+        // ascending index q -> knot index
+        auto KI = [&](int qq) { return sg > 0 ? a + qq : b - qq; };
+        auto X = [&](int qq) { return knotF(f_phi, f_r, m, n, KI(qq)); };
+        auto Y = [&](int qq) { return t[KI(qq)]; };
+        auto CP = [&](int qq) -> double& { return cpbuf[(size_t)(a + qq) * K + h]; };
+        auto DP = [&](int qq) -> double& { return dpbuf[(size_t)(a + qq) * K + h]; };
+        // ascending interval qq covers knots KI(qq), KI(qq+1) -> forward interval
+        auto OUT = [&](int qq, int c, double v) {
+            const int jf = sg > 0 ? a + qq : b - 1 - qq;
+            it[jf].ic[c] = v;
+            if (c == 3) it[jf].gx = X(qq);
+        };
+        spline_not_a_knot(npts, X, Y, CP, DP, OUT);
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// K4: interval records. Lane ranges per sub-branch s over the "lane" index k of the output:
+//   s = 0: g = -freq[k];  s = 1: g = +freq[k].
+// The inverse interval (ascending) covers g in [x_lo, x_hi), open at the run's first knot
+// (notebook supports are open: :569-570; scipy picks the interval x_r <= g < x_{r+1}).
+// Paired (symmetric) grids restrict lanes to the non-positive half: s = 0 to [0, nl),
+// s = 1 to [0, nl1) (nl1 excludes the f = 0 bin so it is counted once).
+// ----------------------------------------------------------------------------------------
+__device__ int64_t lower_bound(const double* f, int64_t nf, double v) {  // first f >= v
+    int64_t lo = 0, hi = nf;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (f[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ int64_t upper_bound(const double* f, int64_t nf, double v) {  // first f > v
+    int64_t lo = 0, hi = nf;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (f[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_items(const double* __restrict__ t, const double* __restrict__ f_phi,
+                        const double* __restrict__ f_r, const int32_t* __restrict__ marr,
+                        const int32_t* __restrict__ narr, const double* __restrict__ ylm_p,
+                        const double* __restrict__ ylm_m, int nt, int K,
+                        const double* __restrict__ coefA, const double* __restrict__ coefT,
+                        const int32_t* __restrict__ runs, const double* __restrict__ freq,
+                        int64_t nf, int paired, int64_t nl, int64_t nl1, double sc_re,
+                        double sc_im, Item* __restrict__ items) {
+    const int ni = nt - 1;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (int64_t)ni * K) return;
+    const int h = (int)(gid % K);
+    const int j = (int)(gid / K);
+    Item& it = items[(size_t)h * ni + j];
+    const int m = marr[h], n = narr[h];
+    const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
+    int run = -1;
+    for (int r = 0; r < MAXRUNS; ++r) {
+        if (rr[4 * r + 2] != 0 && j >= rr[4 * r] && j < rr[4 * r + 1]) { run = r; break; }
+    }
+    const int partner = (m != 0) ? 1 : 0;
+    it.h = h;
+    if (run < 0) {  // flat interval (F_{j+1} == F_j): no support; place empty ranges at 0
+        it.flags = 0;
+        it.klo[0] = it.khi[0] = it.klo[1] = it.khi[1] = 0;
+        return;
+    }
+    const int a = rr[4 * run], sg = rr[4 * run + 2];
+    it.flags = 1 | (partner << 1);
+    it.tj = t[j];
+    it.tj1 = t[j + 1];
+    const double dm = (double)m, dn = (double)n;
+    for (int c = 0; c < 4; ++c) {
+        it.ar[c] = coefA[((size_t)j * 4 + c) * 2 * K + 2 * h];
+        it.ai[c] = coefA[((size_t)j * 4 + c) * 2 * K + 2 * h + 1];
+        const double* ct = coefT + ((size_t)j * 4 + c) * 8;
+        it.ph[c] = dm * ct[0] + dn * ct[1];
+    }
+    // F' = derivative of (m f_phi + n f_r) piece; F'' = derivative of (m f_phi' + n f_r') piece
+    {
+        const double* ct = coefT + (size_t)j * 32;
+        const double F0 = dm * ct[0 * 8 + 2] + dn * ct[0 * 8 + 3];
+        const double F1 = dm * ct[1 * 8 + 2] + dn * ct[1 * 8 + 3];
+        const double F2 = dm * ct[2 * 8 + 2] + dn * ct[2 * 8 + 3];
+        it.fd[0] = 3.0 * F0; it.fd[1] = 2.0 * F1; it.fd[2] = F2;
+        const double G0 = dm * ct[0 * 8 + 4] + dn * ct[0 * 8 + 5];
+        const double G1 = dm * ct[1 * 8 + 4] + dn * ct[1 * 8 + 5];
+        const double G2 = dm * ct[2 * 8 + 4] + dn * ct[2 * 8 + 5];
+        it.fdd[0] = 3.0 * G0; it.fdd[1] = 2.0 * G1; it.fdd[2] = G2;
+    }
+    // S = -h_nb(-f) * scale: fold the minus sign and the complex scale into Y
+    {
+        const double yr = ylm_p[2 * h], yi = ylm_p[2 * h + 1];
+        it.yp[0] = -(sc_re * yr - sc_im * yi);
+        it.yp[1] = -(sc_re * yi + sc_im * yr);
+        const double zr = partner ? ylm_m[2 * h] : 0.0, zi = partner ? ylm_m[2 * h + 1] : 0.0;
+        it.ym[0] = -(sc_re * zr - sc_im * zi);
+        it.ym[1] = -(sc_re * zi + sc_im * zr);
+    }
+    // g-interval of this record: [x_lo, x_hi), lower end open at the run's first knot
+    const double Fj = knotF(f_phi, f_r, m, n, j), Fj1 = knotF(f_phi, f_r, m, n, j + 1);
+    const double xlo = sg > 0 ? Fj : Fj1;
+    const double xhi = sg > 0 ? Fj1 : Fj;
+    const bool strict_lo = sg > 0 ? (j == a) : (j + 1 == rr[4 * run + 1]);
+    // s = 0: g = -f  ->  f in (-xhi, -xlo]  (or (-xhi, -xlo) if strict)
+    int64_t lo0 = upper_bound(freq, nf, -xhi);
+    int64_t hi0 = strict_lo ? lower_bound(freq, nf, -xlo) : upper_bound(freq, nf, -xlo);
+    // s = 1: g = +f  ->  f in [xlo, xhi)  (or (xlo, xhi))
+    int64_t lo1 = strict_lo ? upper_bound(freq, nf, xlo) : lower_bound(freq, nf, xlo);
+    int64_t hi1 = lower_bound(freq, nf, xhi);
+    const int64_t lim0 = paired ? nl : nf;
+    const int64_t lim1 = paired ? nl1 : (partner ? nf : 0);
+    auto clampr = [](int64_t& lo, int64_t& hi, int64_t lim) {
+        if (lo > lim) lo = lim;
+        if (hi > lim) hi = lim;
+        if (hi < lo) hi = lo;
+    };
+    clampr(lo0, hi0, lim0);
+    clampr(lo1, hi1, lim1);
+    it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
+    it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
+}
+
+// ----------------------------------------------------------------------------------------
+// K5: segments (harmonic, run, s): lane range, per-tile counts, contributions C
+// ----------------------------------------------------------------------------------------
+__global__ void k_segments(const int32_t* __restrict__ runs, const Item* __restrict__ items,
+                           int nt, int K, int paired, Seg* __restrict__ segs,
+                           int32_t* __restrict__ counts, Header* __restrict__ hdr) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= K * MAXRUNS * 2) return;
+    const int h = gid / (MAXRUNS * 2);
+    const int r = (gid / 2) % MAXRUNS;
+    const int s = gid & 1;
+    const int ni = nt - 1;
+    Seg sg{};
+    sg.h = h;
+    sg.s = s;
+    const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS + 4 * r;
+    const Item* it = items + (size_t)h * ni;
+    int64_t contrib = 0;
+    if (rr[2] != 0) {
+        sg.ja = rr[0];
+        sg.jb = rr[1];
+        // lane order: s = 0 walks g downward, s = 1 upward; F rises with j when rr[2] > 0
+        sg.dir = (s == 0) ? -rr[2] : rr[2];
+        sg.partner = (it[sg.ja].flags >> 1) & 1;
+        int32_t lo = INT32_MAX, hi = INT32_MIN;
+        for (int j = sg.ja; j < sg.jb; ++j) {
+            const int32_t a = it[j].klo[s], b = it[j].khi[s];
+            if (b > a) {
+                lo = min(lo, a);
+                hi = max(hi, b);
+                const int mult = paired ? (1 + sg.partner) : 1;
+                contrib += (int64_t)(b - a) * mult;
+            }
+        }
+        if (hi > lo) { sg.klo = lo; sg.khi = hi; } else { sg.klo = sg.khi = 0; }
+    }
+    segs[gid] = sg;
+    if (sg.khi > sg.klo) {
+        for (int tt = sg.klo / TILE; tt <= (sg.khi - 1) / TILE; ++tt) atomicAdd(&counts[tt], 1);
+        atomicAdd((unsigned long long*)&hdr->contributions, (unsigned long long)contrib);
+    }
+}
+
+// K6: exclusive scan of counts[ntiles] into offsets[ntiles + 1] (single workgroup)
+__global__ void k_scan(const int32_t* __restrict__ counts, int64_t ntiles,
+                       int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
+                       Header* __restrict__ hdr) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    const int64_t chunk = (ntiles + blockDim.x - 1) / blockDim.x;
+    const int64_t b0 = tid * chunk, b1 = min(ntiles, b0 + chunk);
+    int64_t s = 0;
+    for (int64_t i = b0; i < b1; ++i) s += counts[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+        int64_t v = (tid >= off) ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = part[tid] - s;
+    for (int64_t i = b0; i < b1; ++i) {
+        offsets[i] = (int32_t)min(run, (int64_t)INT32_MAX);
+        cursor[i] = 0;
+        run += counts[i];
+    }
+    if (tid == blockDim.x - 1) {
+        offsets[ntiles] = (int32_t)min(part[tid], (int64_t)INT32_MAX);
+        hdr->needed = part[tid];
+    }
+}
+
+// K7: per-tile entries (segment id << 32 | first interval j whose lanes reach into the tile)
+__global__ void k_fill(const Seg* __restrict__ segs, const Item* __restrict__ items, int nt,
+                       int K, const int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
+                       uint64_t* __restrict__ entries, const Header* __restrict__ hdr) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= K * MAXRUNS * 2) return;
+    const Seg sg = segs[gid];
+    if (sg.khi <= sg.klo) return;
+    if (hdr->needed > hdr->capacity) return;
+    const int ni = nt - 1;
+    const Item* it = items + (size_t)sg.h * ni;
+    int j = sg.dir > 0 ? sg.ja : sg.jb - 1;
+    for (int tt = sg.klo / TILE; tt <= (sg.khi - 1) / TILE; ++tt) {
+        const int32_t tile_lo = tt * TILE;
+        // advance past intervals whose lanes end before this tile
+        while (true) {
+            const int jn = j + sg.dir;
+            if (it[j].khi[sg.s] > tile_lo || jn < sg.ja || jn >= sg.jb) break;
+            j = jn;
+        }
+        const int32_t pos = offsets[tt] + atomicAdd(&cursor[tt], 1);
+        entries[pos] = ((uint64_t)(uint32_t)gid << 32) | (uint32_t)j;
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// SPA arithmetic
+// ----------------------------------------------------------------------------------------
+
+// sin/cos of a phase up to |x| ~ 1e9 rad: two-term FMA Cody-Waite reduction by pi/2 and
+// fdlibm's kernel polynomials on [-pi/4, pi/4].
+__device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
+    constexpr double INV_PIO2 = 6.36619772367581382433e-01;
+    constexpr double PIO2_1 = 1.57079632679489655800e+00;   // first 53 bits of pi/2
+    constexpr double PIO2_2 = 6.12323399573676603587e-17;   // pi/2 - PIO2_1
+    constexpr double PIO2_3 = -1.4973849048591698e-33;      // pi/2 - PIO2_1 - PIO2_2
+    const double q = rint(x * INV_PIO2);
+    double r = fma(-q, PIO2_1, x);
+    r = fma(-q, PIO2_2, r);
+    r = fma(-q, PIO2_3, r);
+    const int64_t iq = (int64_t)q;
+    const double z = r * r;
+    // fdlibm __kernel_sin / __kernel_cos coefficients
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10,
+                       -2.50507602534068634195e-08), 2.75573137070700676789e-06),
+                       -1.98412698298579493134e-04), 8.33333333332248946124e-03),
+                       -1.66666666666666324348e-01);
+    const double sr = fma(r * z, ps, r);
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11,
+                       2.08757232129817482790e-09), -2.75573143513906633035e-07),
+                       2.48015872894767294178e-05), -1.38888888888741095749e-03),
+                       4.16666666666666019037e-02);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * z * pc);
+    const int quad = (int)(iq & 3);
+    const double ss = (quad & 1) ? cr : sr;
+    const double cc = (quad & 1) ? sr : cr;
+    s = (quad & 2) ? -ss : ss;
+    c = ((quad + 1) & 2) ? -cc : cc;
+}
+
+// K~(y) = K_{1/3}(z) e^{z} for z = -i y (y real, nonzero): asymptotic series for |y| >= 17,
+// ascending series (K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3})) below.
+__device__ __noinline__ void kv13_scaled(double y, double& kr, double& ki) {
+    const double ay = fabs(y);
+    const double sgn = y > 0 ? 1.0 : -1.0;
+    if (ay >= 17.0) {
+        // sqrt(pi/(2z)) sum_k a_k z^{-k}, a_k = a_{k-1} (4 nu^2 - (2k-1)^2)/(8k), z^{-1} = i/y
+        constexpr double mu = 4.0 / 9.0;
+        double sr = 1.0, si = 0.0, term = 1.0;
+        const double iy = 1.0 / y;
+        for (int k = 1; k < 60; ++k) {
+            const double tk = term * (mu - (2.0 * k - 1.0) * (2.0 * k - 1.0)) / (8.0 * k) * iy;
+            if (fabs(tk) >= fabs(term) && k > 1) break;
+            term = tk;
+            switch (k & 3) {  // i^k
+                case 0: sr += term; break;
+                case 1: si += term; break;
+                case 2: sr -= term; break;
+                default: si -= term; break;
+            }
+            if (fabs(term) < 1e-17 * fabs(sr)) break;
+        }
+        // sqrt(pi/(2z)) = sqrt(pi/(2|y|)) e^{i sgn pi/4}
+        const double amp = sqrt(PI / (2.0 * ay));
+        const double c4 = 0.70710678118654752440 * amp, s4 = sgn * c4;
+        kr = c4 * sr - s4 * si;
+        ki = c4 * si + s4 * sr;
+        return;
+    }
+    // ascending series: I_{+-nu}(z) = (z/2)^{+-nu} sum_k (z^2/4)^k / (k! Gamma(k +- nu + 1)),
+    // z^2/4 = -y^2/4; (z/2)^{nu} = (|y|/2)^{1/3} e^{-i sgn pi/6}
+    constexpr double nu = 1.0 / 3.0;
+    constexpr double G_P = 0.89297951156924921122;  // Gamma(4/3)
+    constexpr double G_M = 1.35411793942640041695;  // Gamma(2/3)
+    const double q = -0.25 * y * y;
+    double tp = 1.0 / G_P, tm = 1.0 / G_M, sp = tp, sm = tm;
+    for (int k = 1; k < 200; ++k) {
+        tp *= q / (k * (k + nu));
+        tm *= q / (k * (k - nu));
+        sp += tp;
+        sm += tm;
+        if (fabs(tp) < 1e-18 * fabs(sp) && fabs(tm) < 1e-18 * fabs(sm)) break;
+    }
+    const double hz = 0.5 * ay;
+    const double zp = cbrt(hz);           // (|y|/2)^{1/3}
+    const double zm = 1.0 / zp;
+    constexpr double c6 = 0.86602540378443864676, s6 = 0.5;  // cos, sin(pi/6)
+    // I_nu = zp e^{-i sgn pi/6} sp ; I_{-nu} = zm e^{+i sgn pi/6} sm
+    const double ipr = zp * c6 * sp, ipi = -sgn * zp * s6 * sp;
+    const double imr = zm * c6 * sm, imi = sgn * zm * s6 * sm;
+    constexpr double pref = PI / (2.0 * 0.86602540378443864676);  // pi / (2 sin(pi/3))
+    const double Kr = pref * (imr - ipr), Ki = pref * (imi - ipi);
+    // times e^{z} = e^{-i y}
+    double sy, cy;
+    sincos(y, &sy, &cy);
+    kr = Kr * cy + Ki * sy;
+    ki = Ki * cy - Kr * sy;
+}
+
+// Q factor: mirror-convention term is A Y Q e^{i(2 pi g t - Phi)}.
+//   SPA:      Q = e^{i sgn(F') 3 pi/4} / sqrt|F'|
+//   uniform:  Q = i F'/|F''| K~(y) 2/sqrt(3),  y = 2 pi F'^3 / (3 F''^2)   (notebook :599-608)
+// Returns |Q| as (qa) and folds arg(Q) into the phase where it is a constant (SPA).
+template <int CAUSTIC>
+__device__ __forceinline__ void qfactor(double fd, double fdd, double& qr, double& qi) {
+    if (CAUSTIC == EFD_CAUSTIC_SPA || fdd == 0.0) {
+        const double a = rsqrt(fabs(fd));
+        constexpr double c34 = -0.70710678118654752440;  // cos(3pi/4)
+        constexpr double s34 = 0.70710678118654752440;   // sin(3pi/4)
+        qr = a * c34;
+        qi = (fd > 0 ? a : -a) * s34;
+        if (fd == 0.0) { qr = 0.0; qi = 0.0; }
+        return;
+    }
+    if (fd == 0.0) { qr = 0.0; qi = 0.0; return; }
+    const double y = TWO_PI * fd * fd * fd / (3.0 * fdd * fdd);
+    double kr, ki;
+    kv13_scaled(y, kr, ki);
+    const double f = 1.15470053837925152902 * fd / fabs(fdd);  // 2/sqrt(3) F'/|F''|
+    // i * f * (kr + i ki)
+    qr = -f * ki;
+    qi = f * kr;
+}
+
+// Generic (slow-path) evaluation of the harmonic's forward splines at t when t(g) overshoots
+// the record's interval: search the knot and gather the cubic pieces directly.
+struct FwdEval {
+    double ar, ai, ph, fd, fdd;
+};
+__device__ __noinline__ FwdEval forward_generic(double tt, const double* __restrict__ t, int nt,
+                                                int h, int K, int m, int n,
+                                                const double* __restrict__ coefA,
+                                                const double* __restrict__ coefT) {
+    // scipy: interval i with t_i <= tt < t_{i+1}, clamped to [0, nt-2] (extrapolation)
+    int lo = 0, hi = nt - 1;
+    if (tt >= t[nt - 1]) lo = nt - 2;
+    else if (tt <= t[0]) lo = 0;
+    else {
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t[mid] <= tt) lo = mid; else hi = mid;
+        }
+    }
+    const int j = lo;
+    const double w = tt - t[j];
+    auto cub = [&](double c0, double c1, double c2, double c3) {
+        return fma(fma(fma(c0, w, c1), w, c2), w, c3);
+    };
+    const double* ca = coefA + (size_t)j * 4 * 2 * K + 2 * h;
+    const double* ct = coefT + (size_t)j * 32;
+    const double dm = (double)m, dn = (double)n;
+    FwdEval e;
+    e.ar = cub(ca[0], ca[2 * K], ca[4 * K], ca[6 * K]);
+    e.ai = cub(ca[1], ca[2 * K + 1], ca[4 * K + 1], ca[6 * K + 1]);
+    e.ph = cub(dm * ct[0] + dn * ct[1], dm * ct[8] + dn * ct[9], dm * ct[16] + dn * ct[17],
+               dm * ct[24] + dn * ct[25]);
+    const double F0 = dm * ct[2] + dn * ct[3], F1 = dm * ct[10] + dn * ct[11],
+                 F2 = dm * ct[18] + dn * ct[19];
+    e.fd = fma(fma(3.0 * F0, w, 2.0 * F1), w, F2);
+    const double G0 = dm * ct[4] + dn * ct[5], G1 = dm * ct[12] + dn * ct[13],
+                 G2 = dm * ct[20] + dn * ct[21];
+    e.fdd = fma(fma(3.0 * G0, w, 2.0 * G1), w, G2);
+    return e;
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ----------------------------------------------------------------------------------------
+// K8: the mode sum. One workgroup (256 lanes = 4 waves) per tile of TILE lanes.
+// ----------------------------------------------------------------------------------------
+template <bool PAIRED, int CAUSTIC>
+__global__ __launch_bounds__(TILE) void k_modesum(
+    const Item* __restrict__ items, const Seg* __restrict__ segs,
+    const int32_t* __restrict__ offsets, const uint64_t* __restrict__ entries,
+    const double* __restrict__ freq, int64_t nf, int64_t nlanes, int64_t ntiles, int nt, int K,
+    const int32_t* __restrict__ marr, const int32_t* __restrict__ narr,
+    const double* __restrict__ t, const double* __restrict__ coefA,
+    const double* __restrict__ coefT, const Header* __restrict__ hdr, int accumulate,
+    double* __restrict__ out) {
+    __shared__ uint64_t keys[LDS_SORT_CAP];
+    // XCD-aware tile order: consecutive blocks land on different XCDs (round-robin dispatch),
+    // so give each XCD a contiguous run of tiles -- neighbouring tiles share interval records
+    // and harmonic lists, which then hit in that XCD's L2.
+    // grid is padded to a multiple of 8, so this is a bijection on [0, gridDim.x)
+    const int64_t per = gridDim.x >> 3;
+    const int64_t b = blockIdx.x;
+    const int64_t tile = (b & 7) * per + (b >> 3);
+    if (tile >= ntiles) return;
+    const int tid = threadIdx.x;
+    const int64_t k = tile * TILE + tid;
+    const bool lane_ok = k < nlanes;
+    const bool valid_call = hdr->needed <= hdr->capacity;
+
+    const int32_t off = offsets[tile];
+    const int32_t cnt = valid_call ? offsets[tile + 1] - off : 0;
+    const bool sorted = cnt <= LDS_SORT_CAP;
+    if (sorted) {
+        int p2 = 1;
+        while (p2 < cnt) p2 <<= 1;
+        for (int i = tid; i < p2; i += TILE) keys[i] = (i < cnt) ? entries[off + i] : ~0ull;
+        __syncthreads();
+        // bitonic sort by (segment id, interval) -> deterministic summation order
+        for (int size = 2; size <= p2; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = tid; i < p2; i += TILE) {
+                    const int pr = i ^ stride;
+                    if (pr > i) {
+                        const uint64_t a = keys[i], bb = keys[pr];
+                        const bool up = (i & size) == 0;
+                        if ((a > bb) == up) { keys[i] = bb; keys[pr] = a; }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+
+    const double fk = lane_ok ? freq[k] : 0.0;
+    double own_r = 0.0, own_i = 0.0, mir_r = 0.0, mir_i = 0.0;
+    const int wave = tid >> 6;
+    const int32_t w_lo = (int32_t)(tile * TILE + wave * 64);
+    const int32_t w_hi = w_lo + 64;
+    const int ni = nt - 1;
+
+    for (int e = 0; e < cnt; ++e) {
+        const uint64_t key = sorted ? keys[e] : entries[off + e];
+        const uint32_t sid = rfl((uint32_t)(key >> 32));
+        int j = (int)rfl((uint32_t)key);
+        const Seg sg = segs[sid];
+        const int s = sg.s;
+        const Item* hit = items + (size_t)sg.h * ni;
+        while (true) {
+            const Item* it = hit + j;
+            const int32_t klo = it->klo[s], khi = it->khi[s];
+            if (klo >= w_hi) break;
+            if (khi > w_lo && khi > klo) {
+                if (k >= klo && k < khi) {
+                    // g = -f (s = 0) or +f (s = 1), exact negation
+                    const double g = s ? fk : -fk;
+                    const double u = g - it->gx;
+                    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u,
+                                          it->ic[3]);
+                    double ar, ai, ph, fd, fdd;
+                    if (tt >= it->tj && tt < it->tj1) {
+                        const double w = tt - it->tj;
+                        ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
+                        ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
+                        ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+                        fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+                        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM)
+                                  ? fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2])
+                                  : 0.0;
+                    } else {
+                        const FwdEval fe = forward_generic(tt, t, nt, sg.h, K, marr[sg.h],
+                                                           narr[sg.h], coefA, coefT);
+                        ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd;
+                        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM) ? fe.fdd : 0.0;
+                    }
+                    double qr, qi;
+                    qfactor<CAUSTIC>(fd, fdd, qr, qi);
+                    // psi = 2 pi g t - Phi
+                    const double psi = fma(TWO_PI * g, tt, -ph);
+                    double sn, cs;
+                    sincos_big(psi, sn, cs);
+                    // zc = A Q e^{i psi}
+                    const double aqr = ar * qr - ai * qi;
+                    const double aqi = ar * qi + ai * qr;
+                    const double zr = aqr * cs - aqi * sn;
+                    const double zi = aqr * sn + aqi * cs;
+                    const double ypr = it->yp[0], ypi = it->yp[1];
+                    const double ymr = it->ym[0], ymi = it->ym[1];
+                    if (s == 0) {
+                        own_r += ypr * zr - ypi * zi;   // parent at f = -g (own bin)
+                        own_i += ypr * zi + ypi * zr;
+                        if (PAIRED && sg.partner) {     // partner at f = +g (mirror bin)
+                            mir_r += ymr * zr + ymi * zi;
+                            mir_i += ymi * zr - ymr * zi;
+                        }
+                    } else {
+                        if (sg.partner) {               // partner at f = +g (own bin)
+                            own_r += ymr * zr + ymi * zi;
+                            own_i += ymi * zr - ymr * zi;
+                        }
+                        if (PAIRED) {                   // parent at f = -g (mirror bin)
+                            mir_r += ypr * zr - ypi * zi;
+                            mir_i += ypr * zi + ypi * zr;
+                        }
+                    }
+                }
+            }
+            const int jn = j + sg.dir;
+            if (jn < sg.ja || jn >= sg.jb) break;
+            j = jn;
+        }
+    }
+
+    if (!lane_ok || !valid_call) return;
+    double2* o = reinterpret_cast<double2*>(out);
+    if (PAIRED) {
+        const int64_t km = nf - 1 - k;
+        if (km == k) {
+            own_r += mir_r;
+            own_i += mir_i;
+        } else {
+            double2 vm = make_double2(mir_r, mir_i);
+            if (accumulate) { const double2 p = o[km]; vm.x += p.x; vm.y += p.y; }
+            o[km] = vm;
+        }
+    }
+    double2 v = make_double2(own_r, own_i);
+    if (accumulate) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
+    o[k] = v;
+}
+
+// h+ / hx split with FEW's array flip
+__global__ void k_polarizations(const double2* __restrict__ S, int64_t nf, int64_t k0,
+                                double2* __restrict__ hp, double2* __restrict__ hc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = k0 + i;
+    if (k >= nf) return;
+    const double2 a = S[k], b = S[nf - 1 - k];
+    // h+ = (a + conj b)/2 ; hx = i (a - conj b)/2
+    hp[i] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+    hc[i] = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+}
+
+// fused log-likelihood partials: one workgroup per chunk, then a second pass
+__global__ void k_loglike_partial(const double2* __restrict__ h, const double2* __restrict__ d,
+                                  const double* __restrict__ w, int64_t total,
+                                  double* __restrict__ part) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double2 dv = d[i];
+        const double ww = w[i];
+        double rr = dv.x, ri = dv.y;
+        if (h) {
+            const double2 hv = h[i];
+            rr -= hv.x * ww;
+            ri -= hv.y * ww;
+        }
+        acc = fma(rr, rr, fma(ri, ri, acc));
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void k_loglike_final(const double* __restrict__ part, int np, double* __restrict__ out) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) acc += part[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = -0.5 * 4.0 * red[0];
+}
+
+}  // namespace
+
+// ========================================================================================
+// C ABI
+// ========================================================================================
+extern "C" {
+
+int efd_version(void) { return EFD_VERSION; }
+
+int efd_last_error(char* buf, int len) {
+    if (!buf || len <= 0) return EFD_ERR_ARG;
+    std::snprintf(buf, (size_t)len, "%s", g_err.c_str());
+    return EFD_OK;
+}
+
+int efd_spline_build(const double* x, int n, const double* y, int ninterp, double* coef,
+                     void* stream) {
+    if (!x || !y || !coef || n < 2 || ninterp <= 0 || n > MAX_NT)
+        return fail(EFD_ERR_ARG, "efd_spline_build: bad arguments");
+    const int threads = 64;
+    const int blocks = (ninterp + threads - 1) / threads;
+    hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, x, n,
+                       y, ninterp, coef, (int64_t)4 * ninterp);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
+size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf, int64_t incidences) {
+    if (nt < 2 || K <= 0 || nf <= 0 || incidences < 0) return 0;
+    return make_layout(nt, K, nf, incidences, 0).total;  // unpaired has the most tiles
+}
+
+int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!a || !workspace) return fail(EFD_ERR_ARG, "efd_modesum: NULL argument");
+    if (!a->t || !a->phi_phi || !a->phi_r || !a->f_phi || !a->f_r || !a->amp || !a->m ||
+        !a->n || !a->ylm_p || !a->ylm_m || !a->freq || !a->out)
+        return fail(EFD_ERR_ARG, "efd_modesum: NULL array");
+    if (a->nt < 2 || a->nt > MAX_NT) return fail(EFD_ERR_ARG, "efd_modesum: nt out of range");
+    if (a->K <= 0) return fail(EFD_ERR_ARG, "efd_modesum: K must be positive");
+    if (a->nf <= 0 || a->nf >= (int64_t)INT32_MAX)
+        return fail(EFD_ERR_ARG, "efd_modesum: nf out of range");
+    if (a->caustic != EFD_CAUSTIC_SPA && a->caustic != EFD_CAUSTIC_UNIFORM)
+        return fail(EFD_ERR_ARG, "efd_modesum: unknown caustic mode");
+    const int paired = a->grid_symmetric ? 1 : 0;
+    // capacity from the bytes we were given
+    Layout L0 = make_layout(a->nt, a->K, a->nf, 0, paired);
+    if (workspace_bytes < L0.total) return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small");
+    const int64_t cap = (int64_t)((workspace_bytes - L0.total) / sizeof(uint64_t));
+    Layout L = make_layout(a->nt, a->K, a->nf, cap, paired);
+    while (L.total > workspace_bytes && L.capacity > 0) {
+        L = make_layout(a->nt, a->K, a->nf, L.capacity - 64, paired);
+    }
+    if (L.total > workspace_bytes) return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small");
+
+    hipStream_t st = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    Header* hdr = (Header*)(ws + L.header);
+    double* coefA = (double*)(ws + L.coefA);
+    double* coefT = (double*)(ws + L.coefT);
+    double* kslope = (double*)(ws + L.kslope);
+    double* invcp = (double*)(ws + L.invcp);
+    double* invdp = (double*)(ws + L.invdp);
+    int32_t* runs = (int32_t*)(ws + L.runs);
+    Item* items = (Item*)(ws + L.items);
+    Seg* segs = (Seg*)(ws + L.segs);
+    int32_t* counts = (int32_t*)(ws + L.counts);
+    int32_t* offsets = (int32_t*)(ws + L.offsets);
+    int32_t* cursor = (int32_t*)(ws + L.cursor);
+    uint64_t* entries = (uint64_t*)(ws + L.entries);
+
+    const int nt = a->nt, K = a->K;
+    const int64_t nf = a->nf;
+    const int64_t nl = L.nlanes;
+    const int64_t nl1 = paired ? ((nf % 2) ? nl - 1 : nl) : nf;
+
+    Header h0{};
+    h0.capacity = L.capacity;
+    HIP_TRY(hipMemcpyAsync(hdr, &h0, sizeof(Header), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int32_t) * (L.ntiles + 1), st));
+
+    // K1: trajectory splines
+    hipLaunchKernelGGL(k_traj_splines, dim3(1), dim3(64), 0, st, a->t, a->phi_phi, a->phi_r,
+                       a->f_phi, a->f_r, nt, coefT, kslope, (double*)(ws + L.tscratch));
+    HIP_TRY(hipGetLastError());
+    // K2: amplitude splines (2K interpolants, Thomas scratch in place)
+    {
+        const int ninterp = 2 * K;
+        const int threads = 64;
+        const int blocks = (ninterp + threads - 1) / threads;
+        hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), 0, st, a->t, nt, a->amp,
+                           ninterp, coefA, (int64_t)4 * ninterp);
+        HIP_TRY(hipGetLastError());
+    }
+    // K3: inverse splines (writes Item.gx/ic, runs)
+    {
+        const int threads = 64;
+        const int blocks = (K + threads - 1) / threads;
+        hipLaunchKernelGGL(k_inverse_splines, dim3(blocks), dim3(threads), 0, st, a->t, a->f_phi,
+                           a->f_r, a->m, a->n, nt, K, runs, items, invcp, invdp,
+                           (int32_t*)&hdr->pad[0]);
+        HIP_TRY(hipGetLastError());
+    }
+    // K4: interval records
+    {
+        const int64_t total = (int64_t)(nt - 1) * K;
+        const int threads = 256;
+        const int64_t blocks = (total + threads - 1) / threads;
+        hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(threads), 0, st, a->t, a->f_phi,
+                           a->f_r, a->m, a->n, a->ylm_p, a->ylm_m, nt, K, coefA, coefT, runs,
+                           a->freq, nf, paired, nl, nl1, a->scale_re, a->scale_im, items);
+        HIP_TRY(hipGetLastError());
+    }
+    // K5..K7: segments, scan, fill
+    {
+        const int nseg = K * MAXRUNS * 2;
+        const int threads = 256;
+        const int blocks = (nseg + threads - 1) / threads;
+        hipLaunchKernelGGL(k_segments, dim3(blocks), dim3(threads), 0, st, runs, items, nt, K,
+                           paired, segs, counts, hdr);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, L.ntiles, offsets, cursor,
+                           hdr);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(threads), 0, st, segs, items, nt, K,
+                           offsets, cursor, entries, hdr);
+        HIP_TRY(hipGetLastError());
+    }
+    // K8: mode sum
+    {
+        const dim3 grid((unsigned)((L.ntiles + 7) / 8 * 8)), block(TILE);
+        const int acc = a->accumulate ? 1 : 0;
+#define EFD_LAUNCH(P, C)                                                                      \
+    hipLaunchKernelGGL((k_modesum<P, C>), grid, block, 0, st, items, segs, offsets, entries,   \
+                       a->freq, nf, nl, L.ntiles, nt, K, a->m, a->n, a->t, coefA, coefT, hdr, \
+                       acc, a->out)
+        if (paired) {
+            if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
+            else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
+        } else {
+            if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(false, EFD_CAUSTIC_UNIFORM);
+            else EFD_LAUNCH(false, EFD_CAUSTIC_SPA);
+        }
+#undef EFD_LAUNCH
+        HIP_TRY(hipGetLastError());
+    }
+    return EFD_OK;
+}
+
+int efd_modesum_status(const void* workspace, int64_t* needed, void* stream) {
+    if (!workspace) return fail(EFD_ERR_ARG, "efd_modesum_status: NULL workspace");
+    Header h{};
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
+    if (needed) *needed = h.needed;
+    if (h.pad[0] != 0) return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
+    if (h.needed > h.capacity)
+        return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small for the tile lists");
+    return EFD_OK;
+}
+
+int efd_modesum_contributions(const void* workspace, int64_t* contributions, void* stream) {
+    if (!workspace || !contributions) return fail(EFD_ERR_ARG, "NULL argument");
+    Header h{};
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
+    *contributions = h.contributions;
+    return EFD_OK;
+}
+
+int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, double* hc,
+                      void* stream) {
+    if (!S || !hp || !hc || nf <= 0 || k0 < 0 || k0 > nf)
+        return fail(EFD_ERR_ARG, "efd_polarizations: bad arguments");
+    const int64_t cnt = nf - k0;
+    if (cnt == 0) return EFD_OK;
+    const int threads = 256;
+    const int64_t blocks = (cnt + threads - 1) / threads;
+    hipLaunchKernelGGL(k_polarizations, dim3((unsigned)blocks), dim3(threads), 0,
+                       (hipStream_t)stream, (const double2*)S, nf, k0, (double2*)hp, (double2*)hc);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
+int efd_loglike(const double* h, const double* d, const double* w, int32_t nchan, int64_t nbin,
+                double* out, double* scratch, void* stream) {
+    if (!d || !w || !out || !scratch || nchan <= 0 || nbin <= 0)
+        return fail(EFD_ERR_ARG, "efd_loglike: bad arguments");
+    const int64_t total = (int64_t)nchan * nbin;
+    const int threads = 256;
+    const int np = (int)std::min<int64_t>(EFD_LOGLIKE_SCRATCH, (total + threads - 1) / threads);
+    hipStream_t st = (hipStream_t)stream;
+    // fixed partition + fixed reduction tree: bitwise reproducible
+    hipLaunchKernelGGL(k_loglike_partial, dim3(np), dim3(threads), 0, st, (const double2*)h,
+                       (const double2*)d, w, total, scratch);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_loglike_final, dim3(1), dim3(256), 0, st, scratch, np, out);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
+}  // extern "C"

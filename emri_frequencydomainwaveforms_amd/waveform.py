@@ -1,0 +1,171 @@
+"""FEW-compatible waveform classes for the FD path.
+
+Call surfaces kept from the reference (so its drivers only change the import line):
+  GenerateEMRIWaveform("FastSchwarzschildEccentricFlux",
+                       sum_kwargs=dict(pad_output=True, output_type="fd", odd_len=True),
+                       use_gpu=..., return_list=...)          check_mode_by_mode.py:69-83
+  few_gen(M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0,
+          T=, dt=, eps=, [f_arr=, mask_positive=, mode_selection=, include_minus_m=])
+                                                              emri_pe.py:140-155, 212, 242
+  few_gen.waveform_generator.create_waveform.frequency        check_mode_by_mode.py:250
+
+Upstream of the hot path (trajectory, amplitudes, Ylm, mode selection) runs on the host with
+the stand-ins of trajectory.py / amplitude.py (NOT FEW physics).
+The FD summation itself runs in libemrifd.so on the GPU.
+`use_gpu` selects the return type (torch tensors on the GPU, or numpy copies); the compute
+always runs on the GPU -- there is no CPU fallback.
+
+Frame handling [FEW-ext, FEW 1.x GenerateEMRIWaveform as recalled]: the source-frame viewing
+angles are theta = arccos(-R.S), phi = -pi/2 from the sky (qS, phiS) and spin (qK, phiK)
+directions; frame="detector" (default) rotates (h+, hx) by the polarisation angle psi, which on
+the complex spectrum S = h+ - i hx is the constant factor exp(-2 i psi) -- folded into the
+kernel's complex scale, so it costs nothing.
+"""
+
+import numpy as np
+
+from .amplitude import ModeSelector, RomanAmplitude
+from .constants import Gpc, MRSUN_SI
+from .summation import FDInterpolatedModeSum, require_gpu
+from .trajectory import EMRIInspiral
+from .ylm import GetYlms
+
+
+def get_viewing_angles(qS, phiS, qK, phiK):
+    R = np.array([np.sin(qS) * np.cos(phiS), np.sin(qS) * np.sin(phiS), np.cos(qS)])
+    S = np.array([np.sin(qK) * np.cos(phiK), np.sin(qK) * np.sin(phiK), np.cos(qK)])
+    theta = float(np.arccos(np.clip(-np.dot(R, S), -1.0, 1.0)))
+    return theta, -np.pi / 2.0
+
+
+def polarization_angle(qS, phiS, qK, phiK):
+    up = np.cos(qS) * np.sin(qK) * np.cos(phiS - phiK) - np.cos(qK) * np.sin(qS)
+    dw = np.sin(qK) * np.sin(phiS - phiK)
+    return float(-np.arctan2(up, dw)) if dw != 0.0 else 0.5 * np.pi
+
+
+class FastSchwarzschildEccentricFlux:
+    """FD Schwarzschild-eccentric waveform (stand-in upstream, MI355X mode sum)."""
+
+    descriptor = "eccentric"
+
+    def __init__(self, inspiral_kwargs=None, amplitude_kwargs=None, sum_kwargs=None,
+                 Ylm_kwargs=None, use_gpu=False, caustic="uniform", **kwargs):
+        sum_kwargs = dict(sum_kwargs or {})
+        if sum_kwargs.get("output_type", "td") != "fd":
+            raise NotImplementedError(
+                "only the frequency-domain summation (sum_kwargs output_type='fd') is built; the "
+                "time-domain InterpolatedModeSum is out of scope for this hot path (SURVEY.md "
+                "section 8f row 3)")
+        sum_kwargs.setdefault("caustic", caustic)
+        self.use_gpu = use_gpu
+        self.inspiral_generator = EMRIInspiral(func="SchwarzEccFlux", **(inspiral_kwargs or {}))
+        self.amplitude_generator = RomanAmplitude(**(amplitude_kwargs or {}))
+        self.ylm_gen = GetYlms(assume_positive_m=True, **(Ylm_kwargs or {}))
+        self.mode_selector = ModeSelector(self.amplitude_generator.m0mask)
+        self.create_waveform = FDInterpolatedModeSum(use_gpu=use_gpu, **sum_kwargs)
+        self.last_modes = None
+
+    # -- host-side upstream ------------------------------------------------------------------
+    def prepare(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, T=1.0,
+                eps=1e-5, mode_selection=None, include_minus_m=True):
+        """Trajectory, amplitudes, Ylm and mode selection (host; stand-in physics)."""
+        amp = self.amplitude_generator
+        t, p, e, x, Phi_phi, Phi_theta, Phi_r = self.inspiral_generator(
+            M, mu, 0.0, p0, e0, 1.0, Phi_phi0=Phi_phi0, Phi_r0=Phi_r0, T=T)
+        if mode_selection is not None:
+            idx = []
+            for lmn in mode_selection:
+                l, m, n = (int(v) for v in lmn)
+                if m < 0:
+                    l, m, n = l, -m, -n  # FEW folds -m requests onto +m with the partner branch
+                idx.append(amp.lmn_indices[(l, m, n)])
+            keep = np.unique(np.asarray(idx, dtype=np.int64))
+            teuk = amp(p, e)[:, keep]
+            ylms = self.ylm_gen(amp.l_arr[keep], amp.m_arr[keep], theta, phi)
+        else:
+            teuk_all = amp(p, e)
+            ylms_all = self.ylm_gen(amp.l_arr, amp.m_arr, theta, phi)
+            keep = self.mode_selector(teuk_all, ylms_all, None, eps=eps)
+            teuk = teuk_all[:, keep]
+            K = amp.num_teuk_modes
+            ylms = np.concatenate([ylms_all[:K][keep], ylms_all[K:][keep]])
+        K = len(keep)
+        if not include_minus_m:
+            ylms = ylms.copy()
+            ylms[K:] = 0.0
+        self.last_modes = (amp.l_arr[keep], amp.m_arr[keep], amp.n_arr[keep])
+        return dict(t=t, p=p, e=e, Phi_phi=Phi_phi, Phi_r=Phi_r, teuk=teuk, ylms=ylms,
+                    m=amp.m_arr[keep], n=amp.n_arr[keep])
+
+    def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
+                 T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
+                 extra_scale=1.0 + 0.0j, **kwargs):
+        """Complex FD spectrum S = h+ - i hx (torch, on the GPU), distance-scaled."""
+        require_gpu()
+        d = self.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
+                         mode_selection, include_minus_m)
+        K = len(d["m"])
+        scale = complex(extra_scale) * (mu * MRSUN_SI / (dist * Gpc))
+        return self.create_waveform.spectrum(d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:],
+                                             d["Phi_phi"], d["Phi_r"], d["m"], d["n"], M, d["p"],
+                                             d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale)
+
+    def __call__(self, M, mu, p0, e0, theta, phi, dist=1.0, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
+                 T=1.0, eps=1e-5, show_progress=False, batch_size=-1, mode_selection=None,
+                 include_minus_m=True, f_arr=None, mask_positive=False, **kwargs):
+        """FEW FD output: stacked [h+, hx] (2, N) in the source frame."""
+        torch = require_gpu()
+        S = self.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, dt, T, eps,
+                          mode_selection, include_minus_m, f_arr)
+        hp, hc = self.create_waveform.polarizations(S, mask_positive)
+        out = torch.stack([hp, hc])
+        return out if self.use_gpu else out.cpu().numpy()
+
+
+_WAVEFORMS = {"FastSchwarzschildEccentricFlux": FastSchwarzschildEccentricFlux}
+
+
+class GenerateEMRIWaveform:
+    """Generic EMRI generator with FEW's 14-parameter call (frame handling + list output)."""
+
+    def __init__(self, waveform_class, *args, frame="detector", return_list=False, **kwargs):
+        if isinstance(waveform_class, str):
+            if waveform_class not in _WAVEFORMS:
+                raise ValueError(f"unknown waveform {waveform_class!r}; available: "
+                                 f"{sorted(_WAVEFORMS)}")
+            waveform_class = _WAVEFORMS[waveform_class]
+        if frame not in ("detector", "source"):
+            raise ValueError("frame must be 'detector' or 'source'")
+        self.waveform_generator = waveform_class(*args, **kwargs)
+        self.frame = frame
+        self.return_list = return_list
+
+    @property
+    def use_gpu(self):
+        return self.waveform_generator.use_gpu
+
+    def __call__(self, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
+                 Phi_r0, *add_args, mask_positive=False, **kwargs):
+        # a, x0, Phi_theta0 are ignored for Schwarzschild (emri_pe.py:598, 602)
+        theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
+        rot = 1.0 + 0.0j
+        if self.frame == "detector":
+            rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
+        gen = self.waveform_generator
+        S = gen.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, extra_scale=rot,
+                         **kwargs)
+        cw = gen.create_waveform
+        if self.return_list:
+            hp, hc = cw.polarizations(S, mask_positive)
+            out = [hp, hc]
+        else:
+            if mask_positive:
+                torch = require_gpu()
+                k0 = int(torch.searchsorted(cw._freq_dev, torch.zeros(
+                    1, dtype=torch.float64, device=S.device)).item())
+                S = S[k0:]
+            out = S
+        if self.use_gpu:
+            return out
+        return [o.cpu().numpy() for o in out] if isinstance(out, list) else out.cpu().numpy()

@@ -1,0 +1,134 @@
+/*
+ * emrifd.h -- C ABI of the MI355X-native FD EMRI mode-sum library (libemrifd.so).
+ *
+ * Drop-in boundary for the hot path named in BASELINE.json:north_star. In the reference, the
+ * FD summation is reached through FastEMRIWaveforms' Python call surface
+ *   GenerateEMRIWaveform("FastSchwarzschildEccentricFlux",
+ *                        sum_kwargs=dict(pad_output=True, output_type="fd", odd_len=True))
+ * (check_mode_by_mode.py:69-83, emri_pe.py:86-105) whose native seam (FEW's Cython wrapper of
+ * its FD kernels) is external and absent offline [FEW-ext]. The entry points below are what
+ * that seam needs, per SURVEY.md section 8(b):
+ *   - efd_spline_build   <- FEW CubicSplineInterpolant build over the sparse trajectory
+ *                          (analogue: Tutorial_FD_construction_single_mode.ipynb:558, :594)
+ *   - efd_modesum        <- FDInterpolatedModeSum.sum: spline -> SPA per harmonic -> sum over
+ *                          harmonics into the two-sided spectrum (notebook :552-623,
+ *                          summed over modes; called per waveform at check_mode_by_mode.py:226)
+ *   - efd_polarizations  <- the h+/hx split of the 'fd' output (contract
+ *                          check_mode_by_mode.py:247: S = h+ - i hx) and mask_positive
+ *                          (emri_pe.py:241)
+ *   - efd_loglike        <- Likelihood.get_ll's reduction -1/2 * 4 * sum |d - h w|^2
+ *                          (LISAanalysistools/lisatools/sampling/likelihood.py:257-274)
+ *
+ * Conventions: all arrays are caller-owned DEVICE pointers (HIP, gfx950) unless stated;
+ * complex numbers are interleaved (re, im) float64 pairs; every call is asynchronous on the
+ * given hipStream_t (NULL = default stream) and never allocates device memory; return value 0
+ * on success, negative on error (efd_last_error gives the message). Calls on different
+ * streams/devices are independent (no global mutable state except the per-thread error string).
+ */
+#ifndef EMRIFD_H
+#define EMRIFD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EFD_OK 0
+#define EFD_ERR_ARG (-1)        /* invalid argument (shape, NULL pointer, unsorted grid...)  */
+#define EFD_ERR_HIP (-2)        /* HIP runtime error                                          */
+#define EFD_ERR_WORKSPACE (-3)  /* workspace too small: call again with the size reported   */
+
+#define EFD_CAUSTIC_SPA 0       /* plain stationary phase: Q = e^{i sgn(F') 3pi/4} / sqrt|F'| */
+#define EFD_CAUSTIC_UNIFORM 1   /* notebook K_{1/3} uniform form (notebook :599-613)          */
+
+/* Library version (major*10000 + minor*100 + patch). */
+int efd_version(void);
+
+/* Copies the last error message of the calling thread into buf (NUL-terminated). */
+int efd_last_error(char* buf, int len);
+
+/*
+ * Batched not-a-knot cubic splines on shared knots x[n] (n >= 2, strictly increasing):
+ * y is knot-major [n][ninterp]; coef is written as [n-1][4][ninterp] in scipy PPoly order
+ * (c0 highest power): y(x) = ((c0 w + c1) w + c2) w + c3, w = x - x[i].
+ * Matches scipy.interpolate.CubicSpline(x, y, bc_type='not-a-knot') including its n = 2
+ * (line) and n = 3 (parabola) special cases. One lane per interpolant.
+ */
+int efd_spline_build(const double* x, int n, const double* y, int ninterp, double* coef,
+                     void* stream);
+
+/* Input of one FD mode sum (one waveform). */
+typedef struct efd_modesum_args {
+    /* sparse trajectory knots, length nt (device) */
+    const double* t;          /* [nt] seconds, strictly increasing                           */
+    const double* phi_phi;    /* [nt] azimuthal phase                                        */
+    const double* phi_r;      /* [nt] radial phase                                           */
+    const double* f_phi;      /* [nt] Omega_phi / (2 pi M MTSUN_SI) [Hz]                     */
+    const double* f_r;        /* [nt] Omega_r / (2 pi M MTSUN_SI) [Hz]                       */
+    int32_t nt;
+    /* harmonics (device) */
+    const double* amp;        /* complex [nt][K]: Teukolsky amplitude A_k(t_i) (FEW layout)  */
+    const int32_t* m;         /* [K] m >= 0; m > 0 adds the -m partner branch                */
+    const int32_t* n;         /* [K]                                                          */
+    const double* ylm_p;      /* complex [K]: Y_lm                                            */
+    const double* ylm_m;      /* complex [K]: (-1)^l Y_{l,-m} (ignored for m = 0)             */
+    int32_t K;
+    /* frequency grid (device), ascending */
+    const double* freq;       /* [nf]                                                         */
+    int64_t nf;
+    int32_t grid_symmetric;   /* 1 iff freq[nf-1-k] == -freq[k] for all k (mirror pairing)    */
+    /* scaling: S *= scale (complex), e.g. mu MRSUN_SI/(dist Gpc) * e^{-2 i psi_pol}           */
+    double scale_re, scale_im;
+    int32_t caustic;          /* EFD_CAUSTIC_*                                                */
+    int32_t accumulate;       /* 1: out += S, 0: out = S                                      */
+    double* out;              /* complex [nf] (device): FEW 'fd' spectrum S = h+ - i hx       */
+} efd_modesum_args;
+
+/* Bytes of workspace efd_modesum needs for (nt, K, nf) with room for `incidences`
+ * (tile, harmonic-segment) pairs. */
+size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf, int64_t incidences);
+
+/*
+ * Full FD mode sum: spline build -> per-harmonic t(f) inverse splines -> interval records ->
+ * per-tile harmonic lists -> SPA evaluation and output-stationary accumulation.
+ * Asynchronous. The number of incidences the call needed is written into the workspace; read
+ * it with efd_modesum_status after the stream completes. If it exceeded the capacity the
+ * output is NOT valid (status returns EFD_ERR_WORKSPACE): grow the workspace and call again.
+ */
+int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Synchronises `stream`, then reports the incidences the last efd_modesum on this workspace
+ * needed (*needed) and returns EFD_OK or EFD_ERR_WORKSPACE. */
+int efd_modesum_status(const void* workspace, int64_t* needed, void* stream);
+
+/* Contributions C (harmonic branch x bin pairs) evaluated by the last efd_modesum on this
+ * workspace (for the roofline); synchronises `stream`. */
+int efd_modesum_contributions(const void* workspace, int64_t* contributions, void* stream);
+
+/*
+ * h+ = (S(f) + conj(S_flip))/2, hx = i (S(f) - conj(S_flip))/2 with S_flip the array reversed
+ * (FEW list output). Writes bins [k0, nf) of each (k0 = first bin to keep, e.g. the f >= 0
+ * bin for mask_positive) into hp, hc (complex [nf - k0]).
+ */
+int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, double* hc,
+                      void* stream);
+
+/*
+ * Fused Gaussian log-likelihood over nchan channels of nbin bins each:
+ *   out = -1/2 * 4 * sum_c sum_k | d[c][k] - h[c][k] * w[c][k] |^2
+ * (likelihood.py:257-274 with noise factor w = sqrt(df/S) built at likelihood.py:213-220).
+ * h, d complex [nchan][nbin]; w real [nchan][nbin]; out is one device double; scratch holds
+ * EFD_LOGLIKE_SCRATCH device doubles. h = NULL gives the data-only term -2 sum |d|^2.
+ * Bitwise reproducible (fixed partition and reduction order).
+ */
+#define EFD_LOGLIKE_SCRATCH 1024
+int efd_loglike(const double* h, const double* d, const double* w, int32_t nchan, int64_t nbin,
+                double* out, double* scratch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EMRIFD_H */
