@@ -1,0 +1,233 @@
+"""Benchmark: FD EMRI waveforms/s on MI355X (BASELINE.json metric, config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): M = 1e6, mu = 10, e0 = 0.35,
+p0 solved so the inspiral lasts 0.99 * Tobs (README's p0 = 12 is overwritten like
+emri_pe.py:623-635), Tobs = 2 yr, dt = 10 s (N_f = 6,311,631 two-sided bins), eps = 1e-5
+(~3000 harmonics), K_{1/3} uniform SPA (the reference notebook's form). Inputs (sparse
+trajectory, amplitudes, Ylm; host stand-ins, NOT FEW physics) are resident in HBM before timing.
+One step = one full FD waveform on the device: spline build -> inverse splines -> interval
+records -> tile lists -> mode sum -> h+/hx over f >= 0 (the Likelihood path, emri_pe.py:241).
+
+Multi-GPU: one process per GPU; each rank generates its own waveforms (the walker batch of
+emri_pe.py shards with no data-path exchange: weak scaling); value = all ranks' waveforms / the
+max over ranks of the timed region.
+
+roofline: the mode-sum kernel (k_modesum) timed with HIP events recorded on its own stream
+around that kernel only; achieved = B_alg / t with B_alg = 32 C + 32 n_interp N_t + 16 N_f
+(32 B per SPA contribution of the reference's scatter formulation),
+peak 8.0 TB/s (MI355X_MICROARCH.md). traffic: HBM bytes per launch from the committed rocprofv3
+PMC pass (profiles/), or null.
+
+cpu_baseline: the oracle's C restatement (oracle/fd_oracle_c.c, OpenMP, kind "port") timed on a
+bounded sample of the same workload (a subset of its harmonics) on this host, extrapolated to
+waveforms/s through the contribution count; rank 0 at N = 1 only.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "FD waveforms/sec (2 yr, dt=10 s, ~3000 modes) at 1/2/4/8 GPUs; mode-sum HBM GB/s"
+HBM_PEAK_GBS = 8000.0
+
+
+def build_workload(T=2.0, dt=10.0, eps=1e-5, M=1e6, mu=10.0, e0=0.35, theta=np.pi / 3,
+                   phi=-np.pi / 2, dist=1.0):
+    from emri_frequencydomainwaveforms_amd.amplitude import ModeSelector, SyntheticTeukolskyAmplitude
+    from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI, MTSUN_SI
+    from emri_frequencydomainwaveforms_amd.frequencies import get_fundamental_frequencies
+    from emri_frequencydomainwaveforms_amd.summation import fd_grid
+    from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
+    from emri_frequencydomainwaveforms_amd.ylm import GetYlms
+
+    traj = EMRIInspiral()
+    p0 = get_p_at_t(traj, 0.99 * T, [M, mu, 0.0, e0, 1.0])
+    t, p, e, x, pp, pt, pr = traj(M, mu, 0.0, p0, e0, 1.0, T=T)
+    amp = SyntheticTeukolskyAmplitude()
+    A = amp(p, e)
+    ylms = GetYlms(assume_positive_m=True)(amp.l_arr, amp.m_arr, theta, phi)
+    keep = ModeSelector(amp.m0mask)(A, ylms, None, eps=eps)
+    Kall = amp.num_teuk_modes
+    op, _, orr = get_fundamental_frequencies(0.0, p, e, 0.0)
+    return dict(t=t, amp=np.ascontiguousarray(A[:, keep]), phi_phi=pp, phi_r=pr,
+                f_phi=op / (2 * np.pi * M * MTSUN_SI), f_r=orr / (2 * np.pi * M * MTSUN_SI),
+                m=amp.m_arr[keep].astype(np.int32), n=amp.n_arr[keep].astype(np.int32),
+                ylm_p=ylms[:Kall][keep], ylm_m=ylms[Kall:][keep],
+                prefactor=mu * MRSUN_SI / (dist * Gpc), freq=fd_grid(T, dt),
+                params=dict(M=M, mu=mu, p0=float(p0), e0=e0, T=T, dt=dt, eps=eps))
+
+
+def cpu_baseline(w, seconds=15.0):
+    """Time the C oracle on a growing subset of harmonics until ~`seconds` of CPU work."""
+    from oracle import fd_oracle, fd_oracle_c
+    lib = fd_oracle_c.load()
+    if lib is None:
+        return None
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    C_total = fd_oracle.contributions(w["t"], w["f_phi"], w["f_r"], w["m"], w["n"], w["freq"])
+    order = np.argsort(-np.abs(w["amp"]).max(axis=0))   # strongest harmonics first (typical mix)
+    k = 8
+    while True:
+        sel = order[:k]
+        C_s = fd_oracle.contributions(w["t"], w["f_phi"], w["f_r"], w["m"][sel], w["n"][sel],
+                                      w["freq"])
+        t0 = time.perf_counter()
+        fd_oracle_c.modesum(w["t"], w["amp"][:, sel].T, w["phi_phi"], w["phi_r"], w["f_phi"],
+                            w["f_r"], w["m"][sel], w["n"][sel], w["ylm_p"][sel], w["ylm_m"][sel],
+                            w["freq"], w["prefactor"], caustic="uniform", nthreads=threads)
+        dt = time.perf_counter() - t0
+        if dt > seconds / 3 or k >= len(order):
+            break
+        k = min(len(order), int(k * max(2.0, seconds / 3 / max(dt, 1e-3))))
+    rate = C_s / dt                                    # contributions per second
+    return {"value": rate / C_total, "unit": "waveforms/s", "cores": threads, "kind": "port",
+            "sample": f"{k} of {len(order)} harmonics of config 2 ({C_s} of {C_total} SPA "
+                      f"contributions) in {dt:.1f} s on {threads} threads, extrapolated by "
+                      f"contribution count"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--caustic", default="uniform", choices=["uniform", "spa"])
+    ap.add_argument("--T", type=float, default=2.0)
+    ap.add_argument("--eps", type=float, default=1e-5)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine
+
+    w = build_workload(T=args.T, eps=args.eps)
+    inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
+                                 w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"], device=dev)
+    freq = torch.as_tensor(w["freq"], device=dev)
+    nf = int(freq.numel())
+    k0 = int(np.searchsorted(w["freq"], 0.0))
+    S = torch.empty(nf, dtype=torch.complex128, device=dev)
+    hp = torch.empty(nf - k0, dtype=torch.complex128, device=dev)
+    hc = torch.empty_like(hp)
+    eng = ModeSumEngine(caustic=args.caustic)
+    eng.run(inp, freq, out=S, grid_symmetric=True, scale=w["prefactor"])  # sizes the workspace
+    lib = eng.lib
+    stream = torch.cuda.current_stream(dev)
+    st = stream.cuda_stream
+    fS = torch.view_as_real(S)
+    fhp, fhc = torch.view_as_real(hp), torch.view_as_real(hc)
+
+    evs = []
+    for _ in range(args.steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        b.record(stream)
+        evs.append((a, b))
+    torch.cuda.synchronize()
+
+    def step(ev=None):
+        pe = (ev[0].cuda_event, ev[1].cuda_event) if ev is not None else (None, None)
+        eng.launch(inp, freq, fS, True, w["prefactor"], stream=st, prof_events=pe)
+        _lib.check(lib.efd_polarizations(fS.data_ptr(), nf, k0, fhp.data_ptr(), fhc.data_ptr(),
+                                         st), "efd_polarizations", lib)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    ok, needed = eng.status()
+    if not ok:
+        raise RuntimeError("tile-list workspace overflowed during the timed region")
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    C = eng.contributions()
+
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(tt[0]), float(tt[1])
+
+    if rank == 0:
+        K = int(len(w["m"]))
+        nt = int(len(w["t"]))
+        n_interp = 2 * K + 4
+        b_alg = 32.0 * C + 32.0 * n_interp * nt + 16.0 * nf
+        achieved = b_alg / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(prof):
+            try:
+                pj = json.load(open(prof))
+                if pj.get("workload") == "config2" and pj.get("caustic") == args.caustic:
+                    traffic = pj.get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(w, seconds=args.cpu_seconds)
+            except Exception as exc:  # the baseline must not kill the GPU measurement
+                cpu = {"value": None, "error": repr(exc)}
+        value = world * args.steps / elapsed
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "waveforms/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (stand-in trajectory/amplitudes; FEW data absent offline)",
+            "config": {"workload": "config2: M=1e6 mu=10 e0=0.35 Tobs=2yr dt=10s eps=1e-5 "
+                                   f"caustic={args.caustic}",
+                       "harmonics": K, "N_t": nt, "N_f": nf, "contributions": C,
+                       "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_modesum", "kernel_ms": kern_ms,
+                         "contributions_per_s": C / (kern_ms * 1e-3)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libemrifd.so")
+LIB_PATH = os.environ.get("EFD_LIB") or os.path.join(_HERE, "libemrifd.so")
 
 EFD_OK = 0
 EFD_ERR_ARG = -1
@@ -56,6 +56,8 @@ class ModesumArgs(ctypes.Structure):
         ("caustic", ctypes.c_int32),
         ("accumulate", ctypes.c_int32),
         ("out", ctypes.c_void_p),
+        ("prof_begin", ctypes.c_void_p),
+        ("prof_end", ctypes.c_void_p),
     ]
 
 
@@ -72,6 +74,10 @@ def load(path=None):
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    try:  # load torch's HIP runtime first so libemrifd.so binds to the same libamdhip64.so.7
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise EFDError(
             f"HIP library {p} not found: build it with `python -c 'import __graft_entry__ as g; "

@@ -43,7 +43,13 @@
 
 namespace {
 
-constexpr int TILE = 256;           // frequency bins (lanes) per workgroup in k_modesum
+constexpr int TILE = 256;           // threads per workgroup in k_modesum
+#ifndef EFD_BPL
+#define EFD_BPL 4
+#endif
+constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum
+constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
+constexpr int XCD_GROUP = 4;        // consecutive tiles per XCD in the k_modesum dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 2048;        // knots (FEW max_init_len is 1000)
 constexpr int LDS_SORT_CAP = 4096;  // tile-list entries sorted in LDS
@@ -117,7 +123,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int64_t capacity, int pair
     Layout L{};
     const int64_t ni = nt - 1;
     L.nlanes = paired ? (nf + 1) / 2 : nf;
-    L.ntiles = (L.nlanes + TILE - 1) / TILE;
+    L.ntiles = (L.nlanes + TILE_LANES - 1) / TILE_LANES;
     L.capacity = capacity;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
@@ -513,7 +519,8 @@ __global__ void k_segments(const int32_t* __restrict__ runs, const Item* __restr
     }
     segs[gid] = sg;
     if (sg.khi > sg.klo) {
-        for (int tt = sg.klo / TILE; tt <= (sg.khi - 1) / TILE; ++tt) atomicAdd(&counts[tt], 1);
+        for (int tt = sg.klo / TILE_LANES; tt <= (sg.khi - 1) / TILE_LANES; ++tt)
+            atomicAdd(&counts[tt], 1);
         atomicAdd((unsigned long long*)&hdr->contributions, (unsigned long long)contrib);
     }
 }
@@ -560,8 +567,8 @@ __global__ void k_fill(const Seg* __restrict__ segs, const Item* __restrict__ it
     const int ni = nt - 1;
     const Item* it = items + (size_t)sg.h * ni;
     int j = sg.dir > 0 ? sg.ja : sg.jb - 1;
-    for (int tt = sg.klo / TILE; tt <= (sg.khi - 1) / TILE; ++tt) {
-        const int32_t tile_lo = tt * TILE;
+    for (int tt = sg.klo / TILE_LANES; tt <= (sg.khi - 1) / TILE_LANES; ++tt) {
+        const int32_t tile_lo = tt * TILE_LANES;
         // advance past intervals whose lanes end before this tile
         while (true) {
             const int jn = j + sg.dir;
@@ -610,37 +617,53 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
     c = ((quad + 1) & 2) ? -cc : cc;
 }
 
-// K~(y) = K_{1/3}(z) e^{z} for z = -i y (y real, nonzero): asymptotic series for |y| >= 17,
-// ascending series (K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3})) below.
-__device__ __noinline__ void kv13_scaled(double y, double& kr, double& ki) {
+// Q factor. The mirror-convention term of one branch is A Y Q e^{i(2 pi g t - Phi)} with
+//   SPA:      Q_spa = e^{i sgn(F') 3 pi/4} / sqrt|F'|
+//   uniform:  Q = i F'/|F''| K_{1/3}(z) e^{z} 2/sqrt(3),  z = -i y,  y = 2 pi F'^3 / (3 F''^2)
+//             (notebook :599-608). Since i F'/|F''| sqrt(pi/(2z)) 2/sqrt(3) == Q_spa exactly,
+//             Q = Q_spa * sum_k a_k (i w)^k,  w = 1/y, a_k the Hankel asymptotic coefficients
+//             of K_{1/3}: a_k = a_{k-1} (4/9 - (2k-1)^2) / (8k).
+// The kernel folds arg(Q_spa) into the phase and multiplies A by the series (R + i I).
+// Series split: R = sum_j b_j u^j, I = w sum_j c_j u^j, u = w^2, b_j = (-1)^j a_{2j},
+// c_j = (-1)^j a_{2j+1}. With 6 terms the truncation is < 1e-17 for |y| >= 555 (fast path);
+// smaller |y| (hours before plunge, turning points) takes kfactor_slow.
+__constant__ double KB[20] = {
+    1.0, -0.037133487654320986, 0.05764919041266972, -0.2915913992307505, 3.079453030173167,
+    -55.62278536591708, 1533.1694320127956, -59892.51356587907, 3148257.4178668265,
+    -214288036.96368033, 18335766937.890568, -1926471158970.4465, 243826826879716.03,
+    -3.659030701264313e+16, 6.424049357901938e+18, -1.3045132993176097e+21,
+    3.0338710865943386e+23, -8.011464687609593e+25, 2.3839516727271057e+28,
+    -7.940171107576632e+30};
+__constant__ double KC[20] = {
+    -0.06944444444444445, 0.03799305912780064, -0.11609906402551541, 0.8776669695100169,
+    -12.341573332345238, 278.46508077760257, -9207.206599726414, 419524.87511655106,
+    -25198919.871602368, 1929375549.182493, -183418303528.83255, 21196999388647.65,
+    -2926599219297925.0, 4.7576810203630675e+17, -8.995207427058378e+19,
+    1.9570621786581614e+22, -4.854832179436167e+24, 1.3621079545263217e+27,
+    -4.2915604492858035e+29, 1.5087738952527293e+32};
+
+// (R + i I) for |y| < 555: asymptotic with up to 40 terms down to |y| = 18.4, below that the
+// ascending series K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3}) divided by Q_spa.
+__device__ __noinline__ void kfactor_slow(double fd, double fdd, double& R, double& I) {
+    const double y = TWO_PI * fd * fd * fd / (3.0 * fdd * fdd);
     const double ay = fabs(y);
-    const double sgn = y > 0 ? 1.0 : -1.0;
-    if (ay >= 17.0) {
-        // sqrt(pi/(2z)) sum_k a_k z^{-k}, a_k = a_{k-1} (4 nu^2 - (2k-1)^2)/(8k), z^{-1} = i/y
-        constexpr double mu = 4.0 / 9.0;
-        double sr = 1.0, si = 0.0, term = 1.0;
-        const double iy = 1.0 / y;
-        for (int k = 1; k < 60; ++k) {
-            const double tk = term * (mu - (2.0 * k - 1.0) * (2.0 * k - 1.0)) / (8.0 * k) * iy;
-            if (fabs(tk) >= fabs(term) && k > 1) break;
-            term = tk;
-            switch (k & 3) {  // i^k
-                case 0: sr += term; break;
-                case 1: si += term; break;
-                case 2: sr -= term; break;
-                default: si -= term; break;
-            }
-            if (fabs(term) < 1e-17 * fabs(sr)) break;
+    if (ay >= 18.4) {
+        const double w = 1.0 / y, u = w * w;
+        int J = 20;  // 40 terms
+        if (ay >= 153.0) J = 4; else if (ay >= 75.0) J = 5; else if (ay >= 48.0) J = 6;
+        else if (ay >= 29.4) J = 8; else if (ay >= 23.1) J = 10; else if (ay >= 20.3) J = 12;
+        else if (ay >= 19.0) J = 14; else J = 20;
+        double r = 0.0, im = 0.0;
+        for (int jj = J - 1; jj >= 0; --jj) {
+            r = fma(r, u, KB[jj]);
+            im = fma(im, u, KC[jj]);
         }
-        // sqrt(pi/(2z)) = sqrt(pi/(2|y|)) e^{i sgn pi/4}
-        const double amp = sqrt(PI / (2.0 * ay));
-        const double c4 = 0.70710678118654752440 * amp, s4 = sgn * c4;
-        kr = c4 * sr - s4 * si;
-        ki = c4 * si + s4 * sr;
+        R = r;
+        I = w * im;
         return;
     }
-    // ascending series: I_{+-nu}(z) = (z/2)^{+-nu} sum_k (z^2/4)^k / (k! Gamma(k +- nu + 1)),
-    // z^2/4 = -y^2/4; (z/2)^{nu} = (|y|/2)^{1/3} e^{-i sgn pi/6}
+    // ascending series for K_{1/3}(z), z = -i y; K~ = K e^{z}
+    const double sgn = y > 0 ? 1.0 : -1.0;
     constexpr double nu = 1.0 / 3.0;
     constexpr double G_P = 0.89297951156924921122;  // Gamma(4/3)
     constexpr double G_M = 1.35411793942640041695;  // Gamma(2/3)
@@ -653,45 +676,26 @@ __device__ __noinline__ void kv13_scaled(double y, double& kr, double& ki) {
         sm += tm;
         if (fabs(tp) < 1e-18 * fabs(sp) && fabs(tm) < 1e-18 * fabs(sm)) break;
     }
-    const double hz = 0.5 * ay;
-    const double zp = cbrt(hz);           // (|y|/2)^{1/3}
+    const double zp = cbrt(0.5 * ay);     // (|y|/2)^{1/3}
     const double zm = 1.0 / zp;
     constexpr double c6 = 0.86602540378443864676, s6 = 0.5;  // cos, sin(pi/6)
-    // I_nu = zp e^{-i sgn pi/6} sp ; I_{-nu} = zm e^{+i sgn pi/6} sm
     const double ipr = zp * c6 * sp, ipi = -sgn * zp * s6 * sp;
     const double imr = zm * c6 * sm, imi = sgn * zm * s6 * sm;
-    constexpr double pref = PI / (2.0 * 0.86602540378443864676);  // pi / (2 sin(pi/3))
+    constexpr double pref = PI / (2.0 * 0.86602540378443864676);
     const double Kr = pref * (imr - ipr), Ki = pref * (imi - ipi);
-    // times e^{z} = e^{-i y}
     double sy, cy;
     sincos(y, &sy, &cy);
-    kr = Kr * cy + Ki * sy;
-    ki = Ki * cy - Kr * sy;
-}
-
-// Q factor: mirror-convention term is A Y Q e^{i(2 pi g t - Phi)}.
-//   SPA:      Q = e^{i sgn(F') 3 pi/4} / sqrt|F'|
-//   uniform:  Q = i F'/|F''| K~(y) 2/sqrt(3),  y = 2 pi F'^3 / (3 F''^2)   (notebook :599-608)
-// Returns |Q| as (qa) and folds arg(Q) into the phase where it is a constant (SPA).
-template <int CAUSTIC>
-__device__ __forceinline__ void qfactor(double fd, double fdd, double& qr, double& qi) {
-    if (CAUSTIC == EFD_CAUSTIC_SPA || fdd == 0.0) {
-        const double a = rsqrt(fabs(fd));
-        constexpr double c34 = -0.70710678118654752440;  // cos(3pi/4)
-        constexpr double s34 = 0.70710678118654752440;   // sin(3pi/4)
-        qr = a * c34;
-        qi = (fd > 0 ? a : -a) * s34;
-        if (fd == 0.0) { qr = 0.0; qi = 0.0; }
-        return;
-    }
-    if (fd == 0.0) { qr = 0.0; qi = 0.0; return; }
-    const double y = TWO_PI * fd * fd * fd / (3.0 * fdd * fdd);
-    double kr, ki;
-    kv13_scaled(y, kr, ki);
-    const double f = 1.15470053837925152902 * fd / fabs(fdd);  // 2/sqrt(3) F'/|F''|
-    // i * f * (kr + i ki)
-    qr = -f * ki;
-    qi = f * kr;
+    const double kr = Kr * cy + Ki * sy;   // K e^{-i y}
+    const double ki = Ki * cy - Kr * sy;
+    // Q = i f K~, f = (2/sqrt3) F'/|F''|; (R + iI) = Q / Q_spa = Q conj(Q_spa) |F'|
+    const double f = 1.15470053837925152902 * fd / fabs(fdd);
+    const double qr = -f * ki, qi = f * kr;
+    const double a = 1.0 / sqrt(fabs(fd));
+    constexpr double c34 = -0.70710678118654752440;
+    const double sr = a * c34, si = (fd > 0 ? a : -a) * 0.70710678118654752440;
+    const double afd = fabs(fd);
+    R = (qr * sr + qi * si) * afd;
+    I = (qi * sr - qr * si) * afd;
 }
 
 // Generic (slow-path) evaluation of the harmonic's forward splines at t when t(g) overshoots
@@ -737,10 +741,62 @@ __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restr
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// One SPA evaluation of interval record `it` at g: returns zc = A Q e^{i(2 pi g t - Phi)}
+// (the mirror-convention term before Y and scale), see the Q-factor notes above.
+template <int CAUSTIC>
+__device__ __forceinline__ void spa_eval(const Item* __restrict__ it, double g,
+                                         const double* __restrict__ t, int nt, int h, int K,
+                                         int m, int n, const double* __restrict__ coefA,
+                                         const double* __restrict__ coefT, double& zr,
+                                         double& zi) {
+    const double u = g - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    double ar, ai, ph, fd, fdd;
+    if (tt >= it->tj && tt < it->tj1) {
+        const double w = tt - it->tj;
+        ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
+        ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
+        ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+        fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM) ? fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2])
+                                               : 0.0;
+    } else {  // t(g) overshot the record's knot interval: evaluate like scipy (rare)
+        const FwdEval fe = forward_generic(tt, t, nt, h, K, m, n, coefA, coefT);
+        ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd;
+        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM) ? fe.fdd : 0.0;
+    }
+    // SPA amplitude and phase: Q_spa = e^{i sgn 3pi/4} / sqrt|F'|
+    const double amp = fd != 0.0 ? rsqrt(fabs(fd)) : 0.0;
+    const double psi = fma(TWO_PI * g, tt, -ph) + (fd > 0.0 ? 0.75 * PI : -0.75 * PI);
+    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
+        // A *= sum_k a_k (i w)^k, w = 1/y = 3 F''^2 / (2 pi F'^3)
+        const double a2 = amp * amp;
+        const double a6 = a2 * a2 * a2;   // 1/|F'|^3
+        const double w = (fd > 0.0 ? 1.0 : -1.0) * (3.0 / TWO_PI) * fdd * fdd * a6;
+        double R, I;
+        if (fabs(w) * 555.0 <= 1.0) {
+            const double uu = w * w;
+            R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
+            I = w * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
+        } else {
+            kfactor_slow(fd, fdd, R, I);
+        }
+        const double nr = ar * R - ai * I;
+        ai = ar * I + ai * R;
+        ar = nr;
+    }
+    double sn, cs;
+    sincos_big(psi, sn, cs);
+    zr = amp * (ar * cs - ai * sn);
+    zi = amp * (ar * sn + ai * cs);
+}
+
 // ----------------------------------------------------------------------------------------
-// K8: the mode sum. One workgroup (256 lanes = 4 waves) per tile of TILE lanes.
+// K8: the mode sum. One workgroup (4 waves) per tile of TILE * BPL lanes; wave w owns the
+// contiguous chunk [tile_base + w*64*BPL, +64*BPL) and lane l its bins chunk + 64 i + l
+// (i < BPL): one interval record (scalar loads) feeds BPL evaluations per lane.
 // ----------------------------------------------------------------------------------------
-template <bool PAIRED, int CAUSTIC>
+template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) void k_modesum(
     const Item* __restrict__ items, const Seg* __restrict__ segs,
     const int32_t* __restrict__ offsets, const uint64_t* __restrict__ entries,
@@ -750,17 +806,19 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     const double* __restrict__ coefT, const Header* __restrict__ hdr, int accumulate,
     double* __restrict__ out) {
     __shared__ uint64_t keys[LDS_SORT_CAP];
-    // XCD-aware tile order: consecutive blocks land on different XCDs (round-robin dispatch),
-    // so give each XCD a contiguous run of tiles -- neighbouring tiles share interval records
-    // and harmonic lists, which then hit in that XCD's L2.
-    // grid is padded to a multiple of 8, so this is a bijection on [0, gridDim.x)
-    const int64_t per = gridDim.x >> 3;
+    // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
+    // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
+    // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
+    // of dense (low |f|) and empty (near Nyquist) tiles. The lane order runs from -Nyquist to
+    // f = 0, so walking it backwards dispatches the dense band first and the cheap high-|f|
+    // tiles last (short tail). The grid is padded to a multiple of 8 * XCD_GROUP.
     const int64_t b = blockIdx.x;
-    const int64_t tile = (b & 7) * per + (b >> 3);
+    const int64_t r = b >> 3, grp = r / XCD_GROUP;
+    const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
+    const int64_t tile = (int64_t)gridDim.x - 1 - lin;
     if (tile >= ntiles) return;
     const int tid = threadIdx.x;
-    const int64_t k = tile * TILE + tid;
-    const bool lane_ok = k < nlanes;
+    const int lane = tid & 63;
     const bool valid_call = hdr->needed <= hdr->capacity;
 
     const int32_t off = offsets[tile];
@@ -787,11 +845,17 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         }
     }
 
-    const double fk = lane_ok ? freq[k] : 0.0;
-    double own_r = 0.0, own_i = 0.0, mir_r = 0.0, mir_i = 0.0;
-    const int wave = tid >> 6;
-    const int32_t w_lo = (int32_t)(tile * TILE + wave * 64);
-    const int32_t w_hi = w_lo + 64;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
+    const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
+    const int32_t w_hi = w_lo + 64 * BPL;
+    double fk[BPL];
+    double own_r[BPL], own_i[BPL], mir_r[BPL], mir_i[BPL];
+#pragma unroll
+    for (int i = 0; i < BPL; ++i) {
+        const int32_t k = w_lo + 64 * i + lane;
+        fk[i] = k < nlanes ? freq[k] : 0.0;
+        own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
+    }
     const int ni = nt - 1;
 
     for (int e = 0; e < cnt; ++e) {
@@ -799,63 +863,41 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         const uint32_t sid = rfl((uint32_t)(key >> 32));
         int j = (int)rfl((uint32_t)key);
         const Seg sg = segs[sid];
+        if (sg.khi <= w_lo || sg.klo >= w_hi) continue;   // segment misses this wave's chunk
         const int s = sg.s;
-        const Item* hit = items + (size_t)sg.h * ni;
+        const int h = sg.h;
+        const Item* hit = items + (size_t)h * ni;
         while (true) {
             const Item* it = hit + j;
             const int32_t klo = it->klo[s], khi = it->khi[s];
             if (klo >= w_hi) break;
             if (khi > w_lo && khi > klo) {
-                if (k >= klo && k < khi) {
-                    // g = -f (s = 0) or +f (s = 1), exact negation
-                    const double g = s ? fk : -fk;
-                    const double u = g - it->gx;
-                    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u,
-                                          it->ic[3]);
-                    double ar, ai, ph, fd, fdd;
-                    if (tt >= it->tj && tt < it->tj1) {
-                        const double w = tt - it->tj;
-                        ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
-                        ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
-                        ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
-                        fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-                        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM)
-                                  ? fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2])
-                                  : 0.0;
-                    } else {
-                        const FwdEval fe = forward_generic(tt, t, nt, sg.h, K, marr[sg.h],
-                                                           narr[sg.h], coefA, coefT);
-                        ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd;
-                        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM) ? fe.fdd : 0.0;
-                    }
-                    double qr, qi;
-                    qfactor<CAUSTIC>(fd, fdd, qr, qi);
-                    // psi = 2 pi g t - Phi
-                    const double psi = fma(TWO_PI * g, tt, -ph);
-                    double sn, cs;
-                    sincos_big(psi, sn, cs);
-                    // zc = A Q e^{i psi}
-                    const double aqr = ar * qr - ai * qi;
-                    const double aqi = ar * qi + ai * qr;
-                    const double zr = aqr * cs - aqi * sn;
-                    const double zi = aqr * sn + aqi * cs;
-                    const double ypr = it->yp[0], ypi = it->yp[1];
-                    const double ymr = it->ym[0], ymi = it->ym[1];
+                const double ypr = it->yp[0], ypi = it->yp[1];
+                const double ymr = it->ym[0], ymi = it->ym[1];
+#pragma unroll
+                for (int i = 0; i < BPL; ++i) {
+                    const int32_t sub = w_lo + 64 * i;
+                    if (khi <= sub || klo >= sub + 64) continue;      // uniform
+                    const int32_t k = sub + lane;
+                    if (k < klo || k >= khi) continue;                // per lane
+                    const double g = s ? fk[i] : -fk[i];               // exact negation
+                    double zr, zi;
+                    spa_eval<CAUSTIC>(it, g, t, nt, h, K, marr[h], narr[h], coefA, coefT, zr, zi);
                     if (s == 0) {
-                        own_r += ypr * zr - ypi * zi;   // parent at f = -g (own bin)
-                        own_i += ypr * zi + ypi * zr;
-                        if (PAIRED && sg.partner) {     // partner at f = +g (mirror bin)
-                            mir_r += ymr * zr + ymi * zi;
-                            mir_i += ymi * zr - ymr * zi;
+                        own_r[i] += ypr * zr - ypi * zi;   // parent at f = -g (own bin)
+                        own_i[i] += ypr * zi + ypi * zr;
+                        if (PAIRED && sg.partner) {        // partner at f = +g (mirror bin)
+                            mir_r[i] += ymr * zr + ymi * zi;
+                            mir_i[i] += ymi * zr - ymr * zi;
                         }
                     } else {
-                        if (sg.partner) {               // partner at f = +g (own bin)
-                            own_r += ymr * zr + ymi * zi;
-                            own_i += ymi * zr - ymr * zi;
+                        if (sg.partner) {                  // partner at f = +g (own bin)
+                            own_r[i] += ymr * zr + ymi * zi;
+                            own_i[i] += ymi * zr - ymr * zi;
                         }
-                        if (PAIRED) {                   // parent at f = -g (mirror bin)
-                            mir_r += ypr * zr - ypi * zi;
-                            mir_i += ypr * zi + ypi * zr;
+                        if (PAIRED) {                      // parent at f = -g (mirror bin)
+                            mir_r[i] += ypr * zr - ypi * zi;
+                            mir_i[i] += ypr * zi + ypi * zr;
                         }
                     }
                 }
@@ -866,22 +908,28 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         }
     }
 
-    if (!lane_ok || !valid_call) return;
+    if (!valid_call) return;
     double2* o = reinterpret_cast<double2*>(out);
-    if (PAIRED) {
-        const int64_t km = nf - 1 - k;
-        if (km == k) {
-            own_r += mir_r;
-            own_i += mir_i;
-        } else {
-            double2 vm = make_double2(mir_r, mir_i);
-            if (accumulate) { const double2 p = o[km]; vm.x += p.x; vm.y += p.y; }
-            o[km] = vm;
+#pragma unroll
+    for (int i = 0; i < BPL; ++i) {
+        const int64_t k = w_lo + 64 * i + lane;
+        if (k >= nlanes) continue;
+        double orr = own_r[i], oi = own_i[i];
+        if (PAIRED) {
+            const int64_t km = nf - 1 - k;
+            if (km == k) {
+                orr += mir_r[i];
+                oi += mir_i[i];
+            } else {
+                double2 vm = make_double2(mir_r[i], mir_i[i]);
+                if (accumulate) { const double2 p = o[km]; vm.x += p.x; vm.y += p.y; }
+                o[km] = vm;
+            }
         }
+        double2 v = make_double2(orr, oi);
+        if (accumulate) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
+        o[k] = v;
     }
-    double2 v = make_double2(own_r, own_i);
-    if (accumulate) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
-    o[k] = v;
 }
 
 // h+ / hx split with FEW's array flip
@@ -1065,10 +1113,12 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     }
     // K8: mode sum
     {
-        const dim3 grid((unsigned)((L.ntiles + 7) / 8 * 8)), block(TILE);
+        const int64_t gq = 8 * XCD_GROUP;
+        const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
         const int acc = a->accumulate ? 1 : 0;
+        if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
-    hipLaunchKernelGGL((k_modesum<P, C>), grid, block, 0, st, items, segs, offsets, entries,   \
+    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, segs, offsets, entries,   \
                        a->freq, nf, nl, L.ntiles, nt, K, a->m, a->n, a->t, coefA, coefT, hdr, \
                        acc, a->out)
         if (paired) {
@@ -1080,6 +1130,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         }
 #undef EFD_LAUNCH
         HIP_TRY(hipGetLastError());
+        if (a->prof_end) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_end, st));
     }
     return EFD_OK;
 }

@@ -109,7 +109,7 @@ class ModeSumEngine:
         return self._ws
 
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
-               stream=None):
+               stream=None, prof_events=(None, None)):
         """Asynchronous launch; returns the workspace (check with `status`)."""
         torch = _torch()
         nf = int(freq.numel())
@@ -122,7 +122,7 @@ class ModeSumEngine:
             freq=freq.data_ptr(), nf=nf, grid_symmetric=1 if grid_symmetric else 0,
             scale_re=float(np.real(scale)), scale_im=float(np.imag(scale)),
             caustic=CAUSTIC_MODES[self.caustic], accumulate=1 if accumulate else 0,
-            out=out.data_ptr())
+            out=out.data_ptr(), prof_begin=prof_events[0], prof_end=prof_events[1])
         st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
         _lib.check(self.lib.efd_modesum(a, ws.data_ptr(), ws.numel(), st), "efd_modesum", self.lib)
         return ws

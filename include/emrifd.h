@@ -84,6 +84,10 @@ typedef struct efd_modesum_args {
     int32_t caustic;          /* EFD_CAUSTIC_*                                                */
     int32_t accumulate;       /* 1: out += S, 0: out = S                                      */
     double* out;              /* complex [nf] (device): FEW 'fd' spectrum S = h+ - i hx       */
+    /* optional hipEvent_t pair recorded on `stream` around the mode-sum kernel alone (K8), for
+     * roofline timing; NULL = not recorded */
+    void* prof_begin;
+    void* prof_end;
 } efd_modesum_args;
 
 /* Bytes of workspace efd_modesum needs for (nt, K, nf) with room for `incidences`

@@ -1,0 +1,70 @@
+"""C ABI: libemrifd.so loads, exports every function include/emrifd.h declares, and the ctypes
+mirror of efd_modesum_args has the C layout. No compute calls (runs without a GPU)."""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from emri_frequencydomainwaveforms_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "emrifd.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(efd_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_and_python_list_agree():
+    assert declared_functions() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        from emri_frequencydomainwaveforms_amd import _build
+        _build.build()
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.efd_version() == 100
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    for name in declared_functions():
+        assert re.search(rf"\bT {name}$", nm, flags=re.M), name
+
+
+def test_workspace_query_is_host_only():
+    lib = _lib.load()
+    assert lib.efd_modesum_workspace_bytes(100, 3000, 6311631, 1 << 20) > 0
+    assert lib.efd_modesum_workspace_bytes(1, 3000, 100, 0) == 0
+
+
+def test_struct_layout_matches_c(tmp_path):
+    fields = [f for f, _ in _lib.ModesumArgs._fields_]
+    prog = ["#include <stdio.h>", "#include <stddef.h>", '#include "emrifd.h"', "int main(void){",
+            'printf("%zu\\n", sizeof(efd_modesum_args));']
+    prog += [f'printf("%zu\\n", offsetof(efd_modesum_args, {f}));' for f in fields]
+    prog += ["return 0;}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(prog))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert out[0] == ctypes.sizeof(_lib.ModesumArgs)
+    for f, off in zip(fields, out[1:]):
+        assert getattr(_lib.ModesumArgs, f).offset == off, f
+
+
+def test_no_cpu_fallback_without_gpu():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from emri_frequencydomainwaveforms_amd.summation import require_gpu
+    with pytest.raises(_lib.EFDError):
+        require_gpu()
