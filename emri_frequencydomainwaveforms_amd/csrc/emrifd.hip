@@ -17,16 +17,16 @@
 //   K3 k_inverse_splines  1 lane per harmonic: F knots, monotonic runs, inverse spline per run
 //   K4 k_items            1 thread per (harmonic, knot interval): gathers every cubic the SPA
 //                         needs for that interval into one 256-B record + its bin (lane) ranges
-//   K5 k_segments         1 thread per (harmonic, run, branch): lane range, per-tile counts
+//   K5 k_count            1 thread per (record, sub-branch): per-tile incidence counts, C
 //   K6 k_scan             exclusive scan of per-tile counts
-//   K7 k_fill             per-tile lists of (segment, first interval) entries
-//   K8 k_modesum          OUTPUT-STATIONARY: one 256-lane workgroup per tile of frequency bins;
-//                         each lane owns one bin (and its mirror -f when the grid is symmetric:
-//                         the +m branch and its -m partner share t(g), the amplitude/phase
-//                         splines and sin/cos, so one evaluation feeds two bins); the tile's
-//                         harmonic list is sorted in LDS (deterministic summation order),
-//                         interval records are read with scalar loads (wave-uniform), and
-//                         results are written once -- no atomics on the spectrum.
+//   K7 k_fill             per-tile lists of record keys
+//   K8 k_modesum          OUTPUT-STATIONARY: one 4-wave workgroup per tile of 256*BPL bins;
+//                         each lane owns BPL bins (and their mirrors -f when the grid is
+//                         symmetric: the +m branch and its -m partner share t(g), the
+//                         amplitude/phase splines and sin/cos, so one evaluation feeds two
+//                         bins); the tile's record list is sorted in LDS (deterministic
+//                         summation order), records are streamed through a double-buffered LDS
+//                         stage, and results are written once -- no atomics on the spectrum.
 // The SPA evaluation is FP64 VALU work (phases reach ~1e7 rad); MFMA is not applicable.
 
 #include <hip/hip_runtime.h>
@@ -36,6 +36,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "../../include/emrifd.h"
 
@@ -45,7 +46,7 @@ namespace {
 
 constexpr int TILE = 256;           // threads per workgroup in k_modesum
 #ifndef EFD_BPL
-#define EFD_BPL 4
+#define EFD_BPL 2
 #endif
 constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
@@ -53,6 +54,7 @@ constexpr int XCD_GROUP = 4;        // consecutive tiles per XCD in the k_modesu
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 2048;        // knots (FEW max_init_len is 1000)
 constexpr int LDS_SORT_CAP = 4096;  // tile-list entries sorted in LDS
+constexpr int NC = 32;              // interval records per LDS stage in k_modesum
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 
@@ -75,7 +77,7 @@ int fail(int code, const std::string& msg) {
 // ----------------------------------------------------------------------------------------
 
 // One record per (harmonic h, forward knot interval j): everything the SPA needs on the
-// bins whose t(g) falls in [t_j, t_{j+1}). 256 B, read with scalar (SMEM) loads.
+// bins whose t(g) falls in [t_j, t_{j+1}). 256 B, staged through LDS by k_modesum.
 struct __attribute__((aligned(16))) Item {
     double gx;        // left end of the inverse-spline interval (ascending F)
     double ic[4];     // t(g) = ((ic0 u + ic1) u + ic2) u + ic3, u = g - gx
@@ -93,26 +95,16 @@ struct __attribute__((aligned(16))) Item {
 };
 static_assert(sizeof(Item) == 256, "Item must be 256 B");
 
-// One record per (harmonic, monotonic run, sub-branch s).
-struct __attribute__((aligned(16))) Seg {
-    int32_t h, ja, jb;   // run covers forward intervals [ja, jb)
-    int32_t s;           // sub-branch: s = 0 -> g = -f_k, s = 1 -> g = +f_k
-    int32_t dir;         // lane order walks intervals with j += dir
-    int32_t klo, khi;    // lane range of the whole segment
-    int32_t partner;     // 1 if the harmonic has a -m partner
-};
-static_assert(sizeof(Seg) == 32, "Seg must be 32 B");
-
 struct Header {
     int64_t needed;       // incidences required by the last call
     int64_t capacity;     // incidences the workspace holds
     int64_t contributions;
-    int64_t nsegs;
+    int64_t pad0;
     int64_t pad[4];
 };
 
 struct Layout {
-    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, segs, counts, offsets,
+    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, counts, offsets,
         cursor, entries, total;
     int64_t ntiles, nlanes, capacity;
 };
@@ -136,11 +128,10 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int64_t capacity, int pair
     L.invdp = take(sizeof(double) * nt * K);
     L.runs = take(sizeof(int32_t) * 4 * MAXRUNS * K);
     L.items = take(sizeof(Item) * ni * K);
-    L.segs = take(sizeof(Seg) * 2 * MAXRUNS * K);
     L.counts = take(sizeof(int32_t) * (L.ntiles + 1));
     L.offsets = take(sizeof(int32_t) * (L.ntiles + 1));
     L.cursor = take(sizeof(int32_t) * (L.ntiles + 1));
-    L.entries = take(sizeof(uint64_t) * capacity);
+    L.entries = take(sizeof(uint32_t) * capacity);
     L.total = off;
     return L;
 }
@@ -482,46 +473,31 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
 }
 
 // ----------------------------------------------------------------------------------------
-// K5: segments (harmonic, run, s): lane range, per-tile counts, contributions C
+// K5: per-tile counts of (interval record, sub-branch) incidences, and the contribution count C
+// (block-reduced: one 64-bit atomic per workgroup)
 // ----------------------------------------------------------------------------------------
-__global__ void k_segments(const int32_t* __restrict__ runs, const Item* __restrict__ items,
-                           int nt, int K, int paired, Seg* __restrict__ segs,
-                           int32_t* __restrict__ counts, Header* __restrict__ hdr) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= K * MAXRUNS * 2) return;
-    const int h = gid / (MAXRUNS * 2);
-    const int r = (gid / 2) % MAXRUNS;
-    const int s = gid & 1;
-    const int ni = nt - 1;
-    Seg sg{};
-    sg.h = h;
-    sg.s = s;
-    const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS + 4 * r;
-    const Item* it = items + (size_t)h * ni;
-    int64_t contrib = 0;
-    if (rr[2] != 0) {
-        sg.ja = rr[0];
-        sg.jb = rr[1];
-        // lane order: s = 0 walks g downward, s = 1 upward; F rises with j when rr[2] > 0
-        sg.dir = (s == 0) ? -rr[2] : rr[2];
-        sg.partner = (it[sg.ja].flags >> 1) & 1;
-        int32_t lo = INT32_MAX, hi = INT32_MIN;
-        for (int j = sg.ja; j < sg.jb; ++j) {
-            const int32_t a = it[j].klo[s], b = it[j].khi[s];
-            if (b > a) {
-                lo = min(lo, a);
-                hi = max(hi, b);
-                const int mult = paired ? (1 + sg.partner) : 1;
-                contrib += (int64_t)(b - a) * mult;
-            }
+__global__ void k_count(const Item* __restrict__ items, int64_t nitems, int paired,
+                        int32_t* __restrict__ counts, Header* __restrict__ hdr) {
+    __shared__ unsigned long long red[4];
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long contrib = 0;
+    if (gid < 2 * nitems) {
+        const Item& it = items[gid >> 1];
+        const int s = (int)(gid & 1);
+        const int32_t lo = it.klo[s], hi = it.khi[s];
+        if (hi > lo) {
+            const int partner = (it.flags >> 1) & 1;
+            contrib = (unsigned long long)(hi - lo) * (paired ? 1 + partner : 1);
+            for (int tt = lo / TILE_LANES; tt <= (hi - 1) / TILE_LANES; ++tt)
+                atomicAdd(&counts[tt], 1);
         }
-        if (hi > lo) { sg.klo = lo; sg.khi = hi; } else { sg.klo = sg.khi = 0; }
     }
-    segs[gid] = sg;
-    if (sg.khi > sg.klo) {
-        for (int tt = sg.klo / TILE_LANES; tt <= (sg.khi - 1) / TILE_LANES; ++tt)
-            atomicAdd(&counts[tt], 1);
-        atomicAdd((unsigned long long*)&hdr->contributions, (unsigned long long)contrib);
+    for (int o = 32; o > 0; o >>= 1) contrib += __shfl_xor(contrib, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = contrib;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long v = red[0] + red[1] + red[2] + red[3];
+        if (v) atomicAdd((unsigned long long*)&hdr->contributions, v);
     }
 }
 
@@ -555,28 +531,20 @@ __global__ void k_scan(const int32_t* __restrict__ counts, int64_t ntiles,
     }
 }
 
-// K7: per-tile entries (segment id << 32 | first interval j whose lanes reach into the tile)
-__global__ void k_fill(const Seg* __restrict__ segs, const Item* __restrict__ items, int nt,
-                       int K, const int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
-                       uint64_t* __restrict__ entries, const Header* __restrict__ hdr) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= K * MAXRUNS * 2) return;
-    const Seg sg = segs[gid];
-    if (sg.khi <= sg.klo) return;
+// K7: per-tile entry lists: key = (interval record index << 1) | s
+__global__ void k_fill(const Item* __restrict__ items, int64_t nitems,
+                       const int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
+                       uint32_t* __restrict__ entries, const Header* __restrict__ hdr) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= 2 * nitems) return;
     if (hdr->needed > hdr->capacity) return;
-    const int ni = nt - 1;
-    const Item* it = items + (size_t)sg.h * ni;
-    int j = sg.dir > 0 ? sg.ja : sg.jb - 1;
-    for (int tt = sg.klo / TILE_LANES; tt <= (sg.khi - 1) / TILE_LANES; ++tt) {
-        const int32_t tile_lo = tt * TILE_LANES;
-        // advance past intervals whose lanes end before this tile
-        while (true) {
-            const int jn = j + sg.dir;
-            if (it[j].khi[sg.s] > tile_lo || jn < sg.ja || jn >= sg.jb) break;
-            j = jn;
-        }
+    const Item& it = items[gid >> 1];
+    const int s = (int)(gid & 1);
+    const int32_t lo = it.klo[s], hi = it.khi[s];
+    if (hi <= lo) return;
+    for (int tt = lo / TILE_LANES; tt <= (hi - 1) / TILE_LANES; ++tt) {
         const int32_t pos = offsets[tt] + atomicAdd(&cursor[tt], 1);
-        entries[pos] = ((uint64_t)(uint32_t)gid << 32) | (uint32_t)j;
+        entries[pos] = (uint32_t)gid;
     }
 }
 
@@ -741,12 +709,49 @@ __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restr
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// One SPA evaluation of interval record `it` at g: returns zc = A Q e^{i(2 pi g t - Phi)}
-// (the mirror-convention term before Y and scale), see the Q-factor notes above.
+// Branch-free SPA evaluation of interval record `it` at g on the fast path: returns
+// zc = A Q e^{i(2 pi g t - Phi)} (the mirror-convention term before Y and scale; see the
+// Q-factor notes above) and ok = false when this lane needs the general path (t(g) overshot the
+// record's knot interval, or |y| < 555 in the uniform mode) -- then zc is 0.
 template <int CAUSTIC>
-__device__ __forceinline__ void spa_eval(const Item* __restrict__ it, double g,
-                                         const double* __restrict__ t, int nt, int h, int K,
-                                         int m, int n, const double* __restrict__ coefA,
+__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, double& zr,
+                                         double& zi, bool& ok) {
+    const double u = g - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    const double w = tt - it->tj;
+    bool good = (tt >= it->tj) && (tt < it->tj1);
+    double ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
+    double ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
+    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+    const double amp = fd != 0.0 ? rsqrt(fabs(fd)) : 0.0;
+    const double psi = fma(TWO_PI * g, tt, -ph) + (fd > 0.0 ? 0.75 * PI : -0.75 * PI);
+    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
+        const double fdd = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        const double a2 = amp * amp;
+        const double a6 = a2 * a2 * a2;   // 1/|F'|^3
+        const double ww = (fd > 0.0 ? 1.0 : -1.0) * (3.0 / TWO_PI) * fdd * fdd * a6;
+        good = good && (fabs(ww) * 555.0 <= 1.0);
+        const double uu = ww * ww;
+        const double R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
+        const double I = ww * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
+        const double nr = ar * R - ai * I;
+        ai = ar * I + ai * R;
+        ar = nr;
+    }
+    double sn, cs;
+    sincos_big(psi, sn, cs);
+    const double a = good ? amp : 0.0;
+    zr = a * (ar * cs - ai * sn);
+    zi = a * (ar * sn + ai * cs);
+    ok = good;
+}
+
+// General (cold) path: scipy interval selection for t(g) and the full K_{1/3} evaluation.
+template <int CAUSTIC>
+__device__ __noinline__ void spa_general(const Item* __restrict__ it, double g,
+                                         const double* __restrict__ t, int nt, int h, int K, int m,
+                                         int n, const double* __restrict__ coefA,
                                          const double* __restrict__ coefT, double& zr,
                                          double& zi) {
     const double u = g - it->gx;
@@ -758,26 +763,22 @@ __device__ __forceinline__ void spa_eval(const Item* __restrict__ it, double g,
         ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM) ? fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2])
-                                               : 0.0;
-    } else {  // t(g) overshot the record's knot interval: evaluate like scipy (rare)
+        fdd = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+    } else {  // t(g) overshot the record's knot interval: evaluate like scipy
         const FwdEval fe = forward_generic(tt, t, nt, h, K, m, n, coefA, coefT);
-        ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd;
-        fdd = (CAUSTIC == EFD_CAUSTIC_UNIFORM) ? fe.fdd : 0.0;
+        ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd; fdd = fe.fdd;
     }
-    // SPA amplitude and phase: Q_spa = e^{i sgn 3pi/4} / sqrt|F'|
     const double amp = fd != 0.0 ? rsqrt(fabs(fd)) : 0.0;
     const double psi = fma(TWO_PI * g, tt, -ph) + (fd > 0.0 ? 0.75 * PI : -0.75 * PI);
-    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
-        // A *= sum_k a_k (i w)^k, w = 1/y = 3 F''^2 / (2 pi F'^3)
+    if (CAUSTIC == EFD_CAUSTIC_UNIFORM && fd != 0.0 && fdd != 0.0) {
         const double a2 = amp * amp;
-        const double a6 = a2 * a2 * a2;   // 1/|F'|^3
-        const double w = (fd > 0.0 ? 1.0 : -1.0) * (3.0 / TWO_PI) * fdd * fdd * a6;
+        const double a6 = a2 * a2 * a2;
+        const double ww = (fd > 0.0 ? 1.0 : -1.0) * (3.0 / TWO_PI) * fdd * fdd * a6;
         double R, I;
-        if (fabs(w) * 555.0 <= 1.0) {
-            const double uu = w * w;
+        if (fabs(ww) * 555.0 <= 1.0) {
+            const double uu = ww * ww;
             R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
-            I = w * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
+            I = ww * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
         } else {
             kfactor_slow(fd, fdd, R, I);
         }
@@ -792,20 +793,25 @@ __device__ __forceinline__ void spa_eval(const Item* __restrict__ it, double g,
 }
 
 // ----------------------------------------------------------------------------------------
-// K8: the mode sum. One workgroup (4 waves) per tile of TILE * BPL lanes; wave w owns the
-// contiguous chunk [tile_base + w*64*BPL, +64*BPL) and lane l its bins chunk + 64 i + l
-// (i < BPL): one interval record (scalar loads) feeds BPL evaluations per lane.
+// K8: the mode sum. One workgroup (4 waves) per tile of TILE * BPL frequency bins ("lanes");
+// wave w owns the contiguous chunk [tile_base + w*64*BPL, +64*BPL) and lane l its bins
+// chunk + 64 i + l (i < BPL). The tile's list of interval records is sorted in LDS (fixed
+// summation order -> bitwise reproducible), then streamed through a double-buffered LDS stage:
+// the whole workgroup gathers the next NC records with coalesced 16-B loads while the waves
+// evaluate the current NC from LDS (broadcast reads; no dependent global latency in the loop).
+// Each record feeds BPL independent, branch-free evaluations per lane; lanes needing the
+// general path are masked and redone in a cold block.
 // ----------------------------------------------------------------------------------------
 template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) void k_modesum(
-    const Item* __restrict__ items, const Seg* __restrict__ segs,
-    const int32_t* __restrict__ offsets, const uint64_t* __restrict__ entries,
-    const double* __restrict__ freq, int64_t nf, int64_t nlanes, int64_t ntiles, int nt, int K,
-    const int32_t* __restrict__ marr, const int32_t* __restrict__ narr,
-    const double* __restrict__ t, const double* __restrict__ coefA,
-    const double* __restrict__ coefT, const Header* __restrict__ hdr, int accumulate,
-    double* __restrict__ out) {
-    __shared__ uint64_t keys[LDS_SORT_CAP];
+    const Item* __restrict__ items, const int32_t* __restrict__ offsets,
+    const uint32_t* __restrict__ entries, const double* __restrict__ freq, int64_t nf,
+    int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ marr,
+    const int32_t* __restrict__ narr, const double* __restrict__ t,
+    const double* __restrict__ coefA, const double* __restrict__ coefT,
+    const Header* __restrict__ hdr, int accumulate, double* __restrict__ out) {
+    __shared__ uint32_t keys[LDS_SORT_CAP];
+    __shared__ Item stage[2][NC];
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
     // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
@@ -827,15 +833,14 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     if (sorted) {
         int p2 = 1;
         while (p2 < cnt) p2 <<= 1;
-        for (int i = tid; i < p2; i += TILE) keys[i] = (i < cnt) ? entries[off + i] : ~0ull;
+        for (int i = tid; i < p2; i += TILE) keys[i] = (i < cnt) ? entries[off + i] : 0xffffffffu;
         __syncthreads();
-        // bitonic sort by (segment id, interval) -> deterministic summation order
-        for (int size = 2; size <= p2; size <<= 1) {
+        for (int size = 2; size <= p2; size <<= 1) {   // bitonic sort
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
                 for (int i = tid; i < p2; i += TILE) {
                     const int pr = i ^ stride;
                     if (pr > i) {
-                        const uint64_t a = keys[i], bb = keys[pr];
+                        const uint32_t a = keys[i], bb = keys[pr];
                         const bool up = (i & size) == 0;
                         if ((a > bb) == up) { keys[i] = bb; keys[pr] = a; }
                     }
@@ -844,6 +849,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
             }
         }
     }
+    auto key_at = [&](int e) -> uint32_t { return sorted ? keys[e] : entries[off + e]; };
 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
@@ -856,56 +862,97 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         fk[i] = k < nlanes ? freq[k] : 0.0;
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
-    const int ni = nt - 1;
 
-    for (int e = 0; e < cnt; ++e) {
-        const uint64_t key = sorted ? keys[e] : entries[off + e];
-        const uint32_t sid = rfl((uint32_t)(key >> 32));
-        int j = (int)rfl((uint32_t)key);
-        const Seg sg = segs[sid];
-        if (sg.khi <= w_lo || sg.klo >= w_hi) continue;   // segment misses this wave's chunk
-        const int s = sg.s;
-        const int h = sg.h;
-        const Item* hit = items + (size_t)h * ni;
-        while (true) {
-            const Item* it = hit + j;
-            const int32_t klo = it->klo[s], khi = it->khi[s];
-            if (klo >= w_hi) break;
-            if (khi > w_lo && khi > klo) {
-                const double ypr = it->yp[0], ypi = it->yp[1];
-                const double ymr = it->ym[0], ymi = it->ym[1];
+    // staging: a record is 16 pieces of 16 B; NC records = 16 NC pieces, PPT per thread
+    constexpr int PPT = 16 * NC / TILE;
+    uint4 pre[PPT];
+    auto fetch = [&](int c) {
+#pragma unroll
+        for (int p = 0; p < PPT; ++p) {
+            const int piece = tid + p * TILE;
+            const int e = c * NC + (piece >> 4);
+            if (e < cnt) {
+                const uint32_t key = key_at(e);
+                pre[p] = reinterpret_cast<const uint4*>(items + (key >> 1))[piece & 15];
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PPT; ++p) {
+            const int piece = tid + p * TILE;
+            reinterpret_cast<uint4*>(&stage[buf][piece >> 4])[piece & 15] = pre[p];
+        }
+    };
+    const int nchunk = (cnt + NC - 1) / NC;
+    if (nchunk > 0) {
+        fetch(0);
+        store(0);
+    }
+    __syncthreads();
+
+    for (int c = 0; c < nchunk; ++c) {
+        if (c + 1 < nchunk) fetch(c + 1);                 // loads in flight during the chunk
+        const int nin = min(NC, cnt - c * NC);
+        const Item* stg = stage[c & 1];
+        for (int ii = 0; ii < nin; ++ii) {
+            const uint32_t key = rfl(key_at(c * NC + ii));
+            // S = 0: g = -f (parent at the own bin, partner at the mirror); S = 1: g = +f
+            // (partner at the own bin, parent at the mirror). Y- is zero for m = 0 harmonics.
+            const int s = (int)(key & 1);
+            const Item* it = stg + ii;
+            const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
+            const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
+            if (khi <= w_lo || klo >= w_hi) continue;     // misses this wave's chunk
+            const double gs = s ? 1.0 : -1.0;
+            bool okall = true;
+            bool act[BPL];
+            double zr[BPL], zi[BPL];
+#pragma unroll
+            for (int i = 0; i < BPL; ++i) {
+                const int32_t k = w_lo + 64 * i + lane;
+                act[i] = k >= klo && k < khi;
+                bool ok;
+#ifdef EFD_EXP_NOCOMPUTE
+                zr[i] = fk[i] * it->ar[0]; zi[i] = gs * it->ai[1]; ok = true;
+#else
+                spa_fast<CAUSTIC>(it, gs * fk[i], zr[i], zi[i], ok);
+#endif
+                zr[i] = act[i] ? zr[i] : 0.0;
+                zi[i] = act[i] ? zi[i] : 0.0;
+                okall = okall && (ok || !act[i]);
+                act[i] = act[i] && !ok;   // lanes left for the general path
+            }
+            if (__builtin_expect(!__all(okall), 0)) {     // cold: general path for some lanes
+                const Item* git = items + (key >> 1);
+                const int h = git->h;
 #pragma unroll
                 for (int i = 0; i < BPL; ++i) {
-                    const int32_t sub = w_lo + 64 * i;
-                    if (khi <= sub || klo >= sub + 64) continue;      // uniform
-                    const int32_t k = sub + lane;
-                    if (k < klo || k >= khi) continue;                // per lane
-                    const double g = s ? fk[i] : -fk[i];               // exact negation
-                    double zr, zi;
-                    spa_eval<CAUSTIC>(it, g, t, nt, h, K, marr[h], narr[h], coefA, coefT, zr, zi);
-                    if (s == 0) {
-                        own_r[i] += ypr * zr - ypi * zi;   // parent at f = -g (own bin)
-                        own_i[i] += ypr * zi + ypi * zr;
-                        if (PAIRED && sg.partner) {        // partner at f = +g (mirror bin)
-                            mir_r[i] += ymr * zr + ymi * zi;
-                            mir_i[i] += ymi * zr - ymr * zi;
-                        }
-                    } else {
-                        if (sg.partner) {                  // partner at f = +g (own bin)
-                            own_r[i] += ymr * zr + ymi * zi;
-                            own_i[i] += ymi * zr - ymr * zi;
-                        }
-                        if (PAIRED) {                      // parent at f = -g (mirror bin)
-                            mir_r[i] += ypr * zr - ypi * zi;
-                            mir_i[i] += ypr * zi + ypi * zr;
-                        }
+                    if (act[i]) {
+                        spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K, marr[h], narr[h],
+                                             coefA, coefT, zr[i], zi[i]);
                     }
                 }
             }
-            const int jn = j + sg.dir;
-            if (jn < sg.ja || jn >= sg.jb) break;
-            j = jn;
+            const double ypr = it->yp[0], ypi = it->yp[1];
+            const double ymr = it->ym[0], ymi = it->ym[1];
+#pragma unroll
+            for (int i = 0; i < BPL; ++i) {
+                // P = Y+ z (parent, f = -g), Q = Y- conj(z) (partner, f = +g)
+                const double pr = ypr * zr[i] - ypi * zi[i], pi = ypr * zi[i] + ypi * zr[i];
+                const double qr = ymr * zr[i] + ymi * zi[i], qi = ymi * zr[i] - ymr * zi[i];
+                own_r[i] += s ? qr : pr;
+                own_i[i] += s ? qi : pi;
+                if (PAIRED) {
+                    mir_r[i] += s ? pr : qr;
+                    mir_i[i] += s ? pi : qi;
+                }
+            }
         }
+        // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
+        // barrier that closed it; the barrier below publishes the new stage for chunk c+1
+        if (c + 1 < nchunk) store((c + 1) & 1);
+        __syncthreads();
     }
 
     if (!valid_call) return;
@@ -1031,7 +1078,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     // capacity from the bytes we were given
     Layout L0 = make_layout(a->nt, a->K, a->nf, 0, paired);
     if (workspace_bytes < L0.total) return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small");
-    const int64_t cap = (int64_t)((workspace_bytes - L0.total) / sizeof(uint64_t));
+    const int64_t cap = (int64_t)((workspace_bytes - L0.total) / sizeof(uint32_t));
     Layout L = make_layout(a->nt, a->K, a->nf, cap, paired);
     while (L.total > workspace_bytes && L.capacity > 0) {
         L = make_layout(a->nt, a->K, a->nf, L.capacity - 64, paired);
@@ -1048,11 +1095,10 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     double* invdp = (double*)(ws + L.invdp);
     int32_t* runs = (int32_t*)(ws + L.runs);
     Item* items = (Item*)(ws + L.items);
-    Seg* segs = (Seg*)(ws + L.segs);
     int32_t* counts = (int32_t*)(ws + L.counts);
     int32_t* offsets = (int32_t*)(ws + L.offsets);
     int32_t* cursor = (int32_t*)(ws + L.cursor);
-    uint64_t* entries = (uint64_t*)(ws + L.entries);
+    uint32_t* entries = (uint32_t*)(ws + L.entries);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
@@ -1096,18 +1142,18 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
                            a->freq, nf, paired, nl, nl1, a->scale_re, a->scale_im, items);
         HIP_TRY(hipGetLastError());
     }
-    // K5..K7: segments, scan, fill
+    // K5..K7: per-tile counts, scan, fill
     {
-        const int nseg = K * MAXRUNS * 2;
+        const int64_t nitems = (int64_t)(nt - 1) * K;
         const int threads = 256;
-        const int blocks = (nseg + threads - 1) / threads;
-        hipLaunchKernelGGL(k_segments, dim3(blocks), dim3(threads), 0, st, runs, items, nt, K,
-                           paired, segs, counts, hdr);
+        const int64_t blocks = (2 * nitems + threads - 1) / threads;
+        hipLaunchKernelGGL(k_count, dim3((unsigned)blocks), dim3(threads), 0, st, items, nitems,
+                           paired, counts, hdr);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, L.ntiles, offsets, cursor,
                            hdr);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(threads), 0, st, segs, items, nt, K,
+        hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(threads), 0, st, items, nitems,
                            offsets, cursor, entries, hdr);
         HIP_TRY(hipGetLastError());
     }
@@ -1118,7 +1164,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
-    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, segs, offsets, entries,   \
+    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, offsets, entries,       \
                        a->freq, nf, nl, L.ntiles, nt, K, a->m, a->n, a->t, coefA, coefT, hdr, \
                        acc, a->out)
         if (paired) {
