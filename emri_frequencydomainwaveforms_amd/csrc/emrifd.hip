@@ -749,11 +749,10 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, 
 
 // General (cold) path: scipy interval selection for t(g) and the full K_{1/3} evaluation.
 template <int CAUSTIC>
-__device__ __noinline__ void spa_general(const Item* __restrict__ it, double g,
-                                         const double* __restrict__ t, int nt, int h, int K, int m,
-                                         int n, const double* __restrict__ coefA,
-                                         const double* __restrict__ coefT, double& zr,
-                                         double& zi) {
+__device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double g,
+                                            const double* __restrict__ t, int nt, int h, int K,
+                                            int m, int n, const double* __restrict__ coefA,
+                                            const double* __restrict__ coefT) {
     const double u = g - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     double ar, ai, ph, fd, fdd;
@@ -788,8 +787,9 @@ __device__ __noinline__ void spa_general(const Item* __restrict__ it, double g,
     }
     double sn, cs;
     sincos_big(psi, sn, cs);
-    zr = amp * (ar * cs - ai * sn);
-    zi = amp * (ar * sn + ai * cs);
+    // returned by value: references into the caller's register arrays would force them into
+    // scratch memory
+    return make_double2(amp * (ar * cs - ai * sn), amp * (ar * sn + ai * cs));
 }
 
 // ----------------------------------------------------------------------------------------
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
             }
         }
     }
-    auto key_at = [&](int e) -> uint32_t { return sorted ? keys[e] : entries[off + e]; };
+#define key_at(e) (sorted ? keys[(e)] : entries[off + (e)])
 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
@@ -863,36 +863,31 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
 
-    // staging: a record is 16 pieces of 16 B; NC records = 16 NC pieces, PPT per thread
-    constexpr int PPT = 16 * NC / TILE;
-    uint4 pre[PPT];
-    auto fetch = [&](int c) {
-#pragma unroll
-        for (int p = 0; p < PPT; ++p) {
-            const int piece = tid + p * TILE;
-            const int e = c * NC + (piece >> 4);
-            if (e < cnt) {
-                const uint32_t key = key_at(e);
-                pre[p] = reinterpret_cast<const uint4*>(items + (key >> 1))[piece & 15];
-            }
-        }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int p = 0; p < PPT; ++p) {
-            const int piece = tid + p * TILE;
-            reinterpret_cast<uint4*>(&stage[buf][piece >> 4])[piece & 15] = pre[p];
-        }
-    };
+    // staging: a record is 16 pieces of 16 B; NC records = 16 NC pieces, PPT per thread.
+    // (Plain registers, no lambda-captured arrays: those were demoted to scratch memory.)
+    static_assert(16 * NC == 2 * TILE, "staging assumes two 16-B pieces per thread");
+    const int pc0 = tid, pc1 = tid + TILE;
+    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
+#define EFD_FETCH(c)                                                                          \
+    do {                                                                                      \
+        const int e0_ = (c) * NC + (pc0 >> 4), e1_ = (c) * NC + (pc1 >> 4);                   \
+        if (e0_ < cnt) pre0 = reinterpret_cast<const uint4*>(items + (key_at(e0_) >> 1))[pc0 & 15]; \
+        if (e1_ < cnt) pre1 = reinterpret_cast<const uint4*>(items + (key_at(e1_) >> 1))[pc1 & 15]; \
+    } while (0)
+#define EFD_STORE(buf)                                                                        \
+    do {                                                                                      \
+        reinterpret_cast<uint4*>(&stage[(buf)][pc0 >> 4])[pc0 & 15] = pre0;                   \
+        reinterpret_cast<uint4*>(&stage[(buf)][pc1 >> 4])[pc1 & 15] = pre1;                   \
+    } while (0)
     const int nchunk = (cnt + NC - 1) / NC;
     if (nchunk > 0) {
-        fetch(0);
-        store(0);
+        EFD_FETCH(0);
+        EFD_STORE(0);
     }
     __syncthreads();
 
     for (int c = 0; c < nchunk; ++c) {
-        if (c + 1 < nchunk) fetch(c + 1);                 // loads in flight during the chunk
+        if (c + 1 < nchunk) EFD_FETCH(c + 1);             // loads in flight during the chunk
         const int nin = min(NC, cnt - c * NC);
         const Item* stg = stage[c & 1];
         for (int ii = 0; ii < nin; ++ii) {
@@ -929,8 +924,10 @@ __global__ __launch_bounds__(TILE) void k_modesum(
 #pragma unroll
                 for (int i = 0; i < BPL; ++i) {
                     if (act[i]) {
-                        spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K, marr[h], narr[h],
-                                             coefA, coefT, zr[i], zi[i]);
+                        const double2 zg = spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K,
+                                                                marr[h], narr[h], coefA, coefT);
+                        zr[i] = zg.x;
+                        zi[i] = zg.y;
                     }
                 }
             }
@@ -951,9 +948,12 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         }
         // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
         // barrier that closed it; the barrier below publishes the new stage for chunk c+1
-        if (c + 1 < nchunk) store((c + 1) & 1);
+        if (c + 1 < nchunk) EFD_STORE((c + 1) & 1);
         __syncthreads();
     }
+#undef EFD_FETCH
+#undef EFD_STORE
+#undef key_at
 
     if (!valid_call) return;
     double2* o = reinterpret_cast<double2*>(out);

@@ -144,17 +144,20 @@ def fd_modesum(t, amps, phi_phi, phi_r, f_phi, f_r, m, n, ylm_p, ylm_m, freq, pr
 
 
 def contributions(t, f_phi, f_r, m, n, freq):
-    """C = number of (harmonic branch, bin) SPA contributions."""
+    """C = number of (harmonic branch, bin) SPA contributions.
+
+    Same supports as fd_modesum (open intervals on the mirror grid), counted by binary search
+    on the sorted grid: -freq in (lo, hi) <=> freq in (-hi, -lo).
+    """
     freq = np.asarray(freq)
-    mirror = -freq
     total = 0
     for mk, nk in zip(m, n):
         F = mk * f_phi + nk * f_r
         for a, b, sgn in monotonic_runs(F):
             lo, hi = (F[a], F[b]) if sgn > 0 else (F[b], F[a])
-            total += int(np.count_nonzero((mirror > lo) & (mirror < hi)))
+            total += int(np.searchsorted(freq, -lo, "left") - np.searchsorted(freq, -hi, "right"))
             if mk != 0:
-                total += int(np.count_nonzero((mirror > -hi) & (mirror < -lo)))
+                total += int(np.searchsorted(freq, hi, "left") - np.searchsorted(freq, lo, "right"))
     return total
 
 
