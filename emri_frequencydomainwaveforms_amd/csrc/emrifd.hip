@@ -52,7 +52,7 @@ constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 constexpr int XCD_GROUP = 4;        // consecutive tiles per XCD in the k_modesum dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
-constexpr int MAX_NT = 2048;        // knots (FEW max_init_len is 1000)
+constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
 constexpr int LDS_SORT_CAP = 4096;  // tile-list entries sorted in LDS
 constexpr int NC = 32;              // interval records per LDS stage in k_modesum
 constexpr double PI = 3.141592653589793238462643383279502884;
@@ -104,7 +104,8 @@ struct Header {
 };
 
 struct Layout {
-    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, counts, offsets,
+    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, counts,
+        offsets,
         cursor, entries, total;
     int64_t ntiles, nlanes, capacity;
 };
@@ -128,6 +129,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int64_t capacity, int pair
     L.invdp = take(sizeof(double) * nt * K);
     L.runs = take(sizeof(int32_t) * 4 * MAXRUNS * K);
     L.items = take(sizeof(Item) * ni * K);
+    L.ranges = take(sizeof(int4) * ni * K);
     L.counts = take(sizeof(int32_t) * (L.ntiles + 1));
     L.offsets = take(sizeof(int32_t) * (L.ntiles + 1));
     L.cursor = take(sizeof(int32_t) * (L.ntiles + 1));
@@ -206,11 +208,14 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
         const double mm = b - a * cpm;
         s_next = (r - a * dpm) / mm;
     }
-    // back substitution, emitting interval coefficients from the right
+    // back substitution, emitting interval coefficients from the right (the next row's
+    // scratch and knot values are loaded one iteration ahead: the chain is latency-bound)
     double xr = X(n - 1), yr = Y(n - 1);
+    double dpi = DP(n - 2), cpi = CP(n - 2), xl = X(n - 2), yl = Y(n - 2);
     for (int i = n - 2; i >= 0; --i) {
-        const double s_i = DP(i) - CP(i) * s_next;
-        const double xl = X(i), yl = Y(i);
+        double dpn = 0.0, cpn = 0.0, xln = 0.0, yln = 0.0;
+        if (i > 0) { dpn = DP(i - 1); cpn = CP(i - 1); xln = X(i - 1); yln = Y(i - 1); }
+        const double s_i = dpi - cpi * s_next;
         const double dx = xr - xl;
         const double sl = (yr - yl) / dx;
         const double tt = (s_i + s_next - 2.0 * sl) / dx;
@@ -220,6 +225,7 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
         OUT(i, 3, yl);
         s_next = s_i;
         xr = xl; yr = yl;
+        dpi = dpn; cpi = cpn; xl = xln; yl = yln;
     }
 }
 
@@ -232,41 +238,52 @@ __device__ __forceinline__ double dcubic(const double* c, double w) {
 // K1: trajectory splines (one wave; lanes 0..3 the knot data, then lanes 4..5 the slopes)
 // coefT layout: [interval][coef c][q], q: 0 Phi_phi, 1 Phi_r, 2 f_phi, 3 f_r, 4 f_phi', 5 f_r'
 // ----------------------------------------------------------------------------------------
-__global__ void k_traj_splines(const double* __restrict__ t, const double* __restrict__ phi_phi,
+__device__ void traj_splines(const double* __restrict__ t, const double* __restrict__ phi_phi,
                                const double* __restrict__ phi_r, const double* __restrict__ f_phi,
                                const double* __restrict__ f_r, int nt, double* __restrict__ coefT,
                                double* __restrict__ kslope, double* __restrict__ scratch) {
+    // the serial Thomas chains read their knots from LDS instead of global memory
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xs = lds;                 // t
+    double* ys = lds + nt;            // 6 interpolants: Phi_phi, Phi_r, f_phi, f_r, f_phi', f_r'
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+        xs[i] = t[i];
+        ys[i] = phi_phi[i];
+        ys[nt + i] = phi_r[i];
+        ys[2 * nt + i] = f_phi[i];
+        ys[3 * nt + i] = f_r[i];
+    }
+    __syncthreads();
     const int q = threadIdx.x;
     double* cp = scratch + (size_t)q * nt;
     double* dp = scratch + (size_t)(8 + q) * nt;
-    auto X = [&](int i) { return t[i]; };
+    auto X = [&](int i) { return xs[i]; };
     auto CP = [&](int i) -> double& { return cp[i]; };
     auto DP = [&](int i) -> double& { return dp[i]; };
     if (q < 4) {
-        const double* y = q == 0 ? phi_phi : (q == 1 ? phi_r : (q == 2 ? f_phi : f_r));
+        const double* y = ys + (size_t)q * nt;
         auto Y = [&](int i) { return y[i]; };
         auto OUT = [&](int i, int c, double v) { coefT[((size_t)i * 4 + c) * 8 + q] = v; };
         spline_not_a_knot(nt, X, Y, CP, DP, OUT);
     }
     __syncthreads();
     // knot values of f_phi'(t) and f_r'(t), evaluated like scipy's derivative PPoly at the knots
-    if (q < 2) {
-        const int qq = 2 + q;
-        for (int i = 0; i < nt; ++i) {
-            double v;
-            if (i < nt - 1) {
-                v = coefT[((size_t)i * 4 + 2) * 8 + qq];
-            } else {
-                double c[4];
-                for (int cc = 0; cc < 4; ++cc) c[cc] = coefT[((size_t)(nt - 2) * 4 + cc) * 8 + qq];
-                v = dcubic(c, t[nt - 1] - t[nt - 2]);
-            }
-            kslope[(size_t)q * nt + i] = v;
+    for (int idx = threadIdx.x; idx < 2 * nt; idx += blockDim.x) {
+        const int qq = 2 + idx / nt, i = idx % nt;
+        double v;
+        if (i < nt - 1) {
+            v = coefT[((size_t)i * 4 + 2) * 8 + qq];
+        } else {
+            double c[4];
+            for (int cc = 0; cc < 4; ++cc) c[cc] = coefT[((size_t)(nt - 2) * 4 + cc) * 8 + qq];
+            v = dcubic(c, xs[nt - 1] - xs[nt - 2]);
         }
+        ys[(size_t)(4 + idx / nt) * nt + i] = v;
+        kslope[idx] = v;
     }
     __syncthreads();
     if (q >= 4 && q < 6) {
-        const double* y = kslope + (size_t)(q - 4) * nt;
+        const double* y = ys + (size_t)q * nt;
         auto Y = [&](int i) { return y[i]; };
         auto OUT = [&](int i, int c, double v) { coefT[((size_t)i * 4 + c) * 8 + q] = v; };
         spline_not_a_knot(nt, X, Y, CP, DP, OUT);
@@ -277,21 +294,98 @@ __global__ void k_traj_splines(const double* __restrict__ t, const double* __res
 // K2: shared-knot splines of the amplitudes, one lane per interpolant (Re/Im of each harmonic).
 // y is knot-major [n][ninterp] (FEW's teuk_modes[N_t][K] complex layout), coef [n-1][4][ninterp].
 // ----------------------------------------------------------------------------------------
-__global__ void k_spline_shared(const double* __restrict__ x, int n, const double* __restrict__ y,
-                                int ninterp, double* coef, int64_t scratch_stride) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void spline_shared(const double* __restrict__ x, int n, const double* __restrict__ y,
+                              int ninterp, double* coef, int64_t scratch_stride, int block) {
+    // The not-a-knot matrix depends only on the shared knots: one thread factors it into LDS
+    // (cp_i, 1/m_i, a_i of the Thomas sweep), then every lane runs the two division-free
+    // recurrences for its right-hand side. DP(i) lives in the c1 slot of interval i of the
+    // output (read back, one row ahead, by the back substitution before that row is written).
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xs = lds;
+    double* cpl = lds + n;
+    double* iml = lds + 2 * n;
+    double* all = lds + 3 * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) xs[i] = x[i];
+    __syncthreads();
+    if (threadIdx.x == 0 && n >= 4) {
+        double dxm = xs[1] - xs[0], dxi = xs[2] - xs[1];
+        double d = xs[2] - xs[0];
+        cpl[0] = d / dxi; iml[0] = 1.0 / dxi; all[0] = 0.0;
+        for (int i = 1; i <= n - 2; ++i) {
+            dxm = xs[i] - xs[i - 1];
+            dxi = xs[i + 1] - xs[i];
+            const double mm = 2.0 * (dxm + dxi) - dxi * cpl[i - 1];
+            cpl[i] = dxm / mm; iml[i] = 1.0 / mm; all[i] = dxi;
+        }
+        const double dl = xs[n - 1] - xs[n - 3];
+        const double mm = (xs[n - 2] - xs[n - 3]) - dl * cpl[n - 2];
+        iml[n - 1] = 1.0 / mm; all[n - 1] = dl; cpl[n - 1] = 0.0;
+    }
+    __syncthreads();
+    const int q = block * blockDim.x + threadIdx.x;
     if (q >= ninterp) return;
-    // Thomas scratch CP(i), DP(i) (rows i <= n-2) live in the c0 / c1 slots of interval i of
-    // the output itself: the back substitution reads CP(i), DP(i) before it writes interval i,
-    // and the forward sweep never reads an interval the back substitution has written.
-    double* cpbuf = coef;
-    double* dpbuf = coef + ninterp;
-    auto X = [&](int i) { return x[i]; };
     auto Y = [&](int i) { return y[(size_t)i * ninterp + q]; };
-    auto CP = [&](int i) -> double& { return cpbuf[(size_t)i * scratch_stride + q]; };
-    auto DP = [&](int i) -> double& { return dpbuf[(size_t)i * scratch_stride + q]; };
     auto OUT = [&](int i, int c, double v) { coef[((size_t)i * 4 + c) * ninterp + q] = v; };
-    spline_not_a_knot(n, X, Y, CP, DP, OUT);
+    if (n < 4) {
+        double* cpbuf = coef;
+        double* dpbuf = coef + ninterp;
+        auto X = [&](int i) { return xs[i]; };
+        auto CP = [&](int i) -> double& { return cpbuf[(size_t)i * scratch_stride + q]; };
+        auto DP = [&](int i) -> double& { return dpbuf[(size_t)i * scratch_stride + q]; };
+        spline_not_a_knot(n, X, Y, CP, DP, OUT);
+        return;
+    }
+    double* dpb = coef + ninterp;   // DP(i) at coef[(i*4+1)*ninterp + q]
+    auto DPs = [&](int i) -> double& { return dpb[(size_t)i * scratch_stride + q]; };
+    // forward sweep: dp_i = (r_i - a_i dp_{i-1}) / m_i
+    double y0 = Y(0), y1 = Y(1), y2 = Y(2);
+    double dxm = xs[1] - xs[0], dxi = xs[2] - xs[1];
+    double slm = (y1 - y0) / dxm, sli = (y2 - y1) / dxi;
+    double dp;
+    {
+        const double d = xs[2] - xs[0];
+        const double r0 = ((dxm + 2.0 * d) * dxi * slm + dxm * dxm * sli) / d;
+        dp = r0 * iml[0];
+        DPs(0) = dp;
+    }
+    double yi = y2;
+    double ynext = (n > 3) ? Y(3) : 0.0;
+    for (int i = 1; i <= n - 2; ++i) {
+        const double r = 3.0 * (dxi * slm + dxm * sli);
+        dp = (r - all[i] * dp) * iml[i];
+        DPs(i) = dp;
+        if (i + 2 <= n - 1) {
+            const double yn = ynext;
+            if (i + 3 <= n - 1) ynext = Y(i + 3);
+            dxm = dxi; slm = sli;
+            dxi = xs[i + 2] - xs[i + 1]; sli = (yn - yi) / dxi;
+            yi = yn;
+        }
+    }
+    double s_next;
+    {
+        const double d = dxm + dxi;
+        const double r = (dxi * dxi * slm + (2.0 * d + dxi) * dxm * sli) / d;
+        s_next = (r - all[n - 1] * dp) * iml[n - 1];
+    }
+    // back substitution with one-row prefetch of DP and y
+    double yr = Y(n - 1);
+    double dpi = DPs(n - 2), yl = Y(n - 2);
+    for (int i = n - 2; i >= 0; --i) {
+        double dpn = 0.0, yln = 0.0;
+        if (i > 0) { dpn = DPs(i - 1); yln = Y(i - 1); }
+        const double s_i = dpi - cpl[i] * s_next;
+        const double dx = xs[i + 1] - xs[i];
+        const double sl = (yr - yl) / dx;
+        const double tt = (s_i + s_next - 2.0 * sl) / dx;
+        OUT(i, 0, tt / dx);
+        OUT(i, 1, (sl - s_i) / dx - tt);
+        OUT(i, 2, s_i);
+        OUT(i, 3, yl);
+        s_next = s_i;
+        yr = yl;
+        dpi = dpn; yl = yln;
+    }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -305,13 +399,23 @@ __device__ __forceinline__ double knotF(const double* f_phi, const double* f_r, 
     return __dadd_rn(__dmul_rn((double)m, f_phi[i]), __dmul_rn((double)n, f_r[i]));
 }
 
-__global__ void k_inverse_splines(const double* __restrict__ t, const double* __restrict__ f_phi,
+__device__ void inverse_splines(const double* __restrict__ t, const double* __restrict__ f_phi,
                                   const double* __restrict__ f_r, const int32_t* __restrict__ marr,
                                   const int32_t* __restrict__ narr, int nt, int K,
                                   int32_t* __restrict__ runs, Item* __restrict__ items,
                                   double* __restrict__ cpbuf, double* __restrict__ dpbuf,
-                                  int32_t* __restrict__ err) {
-    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+                                  int32_t* __restrict__ err, int block) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* ts = lds;              // t, f_phi, f_r staged in LDS for the serial chains
+    double* fps = lds + nt;
+    double* frs = lds + 2 * nt;
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+        ts[i] = t[i];
+        fps[i] = f_phi[i];
+        frs[i] = f_r[i];
+    }
+    __syncthreads();
+    const int h = block * blockDim.x + threadIdx.x;
     if (h >= K) return;
     const int m = marr[h], n = narr[h];
     const int ni = nt - 1;
@@ -320,14 +424,14 @@ __global__ void k_inverse_splines(const double* __restrict__ t, const double* __
     for (int r = 0; r < MAXRUNS; ++r) { rr[4 * r] = 0; rr[4 * r + 1] = 0; rr[4 * r + 2] = 0; }
     int nrun = 0;
     int j = 0;
-    double Fprev = knotF(f_phi, f_r, m, n, 0);
+    double Fprev = knotF(fps, frs, m, n, 0);
     // scan the interval signs and emit maximal strictly monotonic runs
     int cur_sign = 0, ja = 0;
     for (j = 0; j <= ni; ++j) {
         int sg = 0;
         double Fn = 0.0;
         if (j < ni) {
-            Fn = knotF(f_phi, f_r, m, n, j + 1);
+            Fn = knotF(fps, frs, m, n, j + 1);
             sg = (Fn > Fprev) ? 1 : ((Fn < Fprev) ? -1 : 0);
         }
         if (sg != cur_sign || j == ni) {
@@ -350,8 +454,8 @@ __global__ void k_inverse_splines(const double* __restrict__ t, const double* __
         const int npts = b - a + 1;
         // ascending index q -> knot index
         auto KI = [&](int qq) { return sg > 0 ? a + qq : b - qq; };
-        auto X = [&](int qq) { return knotF(f_phi, f_r, m, n, KI(qq)); };
-        auto Y = [&](int qq) { return t[KI(qq)]; };
+        auto X = [&](int qq) { return knotF(fps, frs, m, n, KI(qq)); };
+        auto Y = [&](int qq) { return ts[KI(qq)]; };
         auto CP = [&](int qq) -> double& { return cpbuf[(size_t)(a + qq) * K + h]; };
         auto DP = [&](int qq) -> double& { return dpbuf[(size_t)(a + qq) * K + h]; };
         // ascending interval qq covers knots KI(qq), KI(qq+1) -> forward interval
@@ -364,6 +468,34 @@ __global__ void k_inverse_splines(const double* __restrict__ t, const double* __
     }
 }
 
+// K1-K3 fused into one launch: the three spline stages are independent, latency-bound serial
+// chains on few workgroups, so running them side by side costs max() instead of sum().
+// Block 0: trajectory splines; blocks [1, 1 + nb_amp): amplitude splines (64 interpolants per
+// block); the rest: inverse splines (64 harmonics per block).
+__global__ __launch_bounds__(64) void k_prep(
+    const double* __restrict__ t, const double* __restrict__ phi_phi,
+    const double* __restrict__ phi_r, const double* __restrict__ f_phi,
+    const double* __restrict__ f_r, const double* __restrict__ amp, const int32_t* __restrict__ m,
+    const int32_t* __restrict__ n, int nt, int K, int nb_amp, double* __restrict__ coefT,
+    double* __restrict__ kslope, double* __restrict__ tscratch, double* coefA,
+    int32_t* __restrict__ runs, Item* __restrict__ items, double* __restrict__ invcp,
+    double* __restrict__ invdp, int32_t* __restrict__ err) {
+    const int b = blockIdx.x;
+    if (b == 0) {
+        traj_splines(t, phi_phi, phi_r, f_phi, f_r, nt, coefT, kslope, tscratch);
+    } else if (b < 1 + nb_amp) {
+        spline_shared(t, nt, amp, 2 * K, coefA, (int64_t)4 * 2 * K, b - 1);
+    } else {
+        inverse_splines(t, f_phi, f_r, m, n, nt, K, runs, items, invcp, invdp, err, b - 1 - nb_amp);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_spline_shared(const double* __restrict__ x, int n,
+                                                      const double* __restrict__ y, int ninterp,
+                                                      double* coef, int64_t scratch_stride) {
+    spline_shared(x, n, y, ninterp, coef, scratch_stride, blockIdx.x);
+}
+
 // ----------------------------------------------------------------------------------------
 // K4: interval records. Lane ranges per sub-branch s over the "lane" index k of the output:
 //   s = 0: g = -freq[k];  s = 1: g = +freq[k].
@@ -372,22 +504,50 @@ __global__ void k_inverse_splines(const double* __restrict__ t, const double* __
 // Paired (symmetric) grids restrict lanes to the non-positive half: s = 0 to [0, nl),
 // s = 1 to [0, nl1) (nl1 excludes the f = 0 bin so it is counted once).
 // ----------------------------------------------------------------------------------------
-__device__ int64_t lower_bound(const double* f, int64_t nf, double v) {  // first f >= v
-    int64_t lo = 0, hi = nf;
+// First index with f[i] >= v (UPPER = false) or f[i] > v (UPPER = true) on the sorted grid.
+// Starts from the linear-interpolation guess g (exact to +-1 bin on the uniform FEW grids) and
+// gallops outward before bisecting, so a typical call reads 2-3 grid values instead of the
+// ~23 dependent loads of a plain binary search over 6.3M bins.
+template <bool UPPER>
+__device__ int64_t grid_bound(const double* __restrict__ f, int64_t nf, double v, int64_t g) {
+    auto pred = [&](int64_t i) { return UPPER ? (f[i] > v) : (f[i] >= v); };
+    g = g < 0 ? 0 : (g > nf ? nf : g);
+    int64_t lo, hi;   // answer in [lo, hi]
+    if (g < nf && !pred(g)) {
+        lo = g + 1;
+        int64_t step = 1;
+        while (true) {
+            const int64_t p = lo + step - 1;
+            if (p >= nf) { hi = nf; break; }
+            if (pred(p)) { hi = p; break; }
+            lo = p + 1;
+            step <<= 1;
+        }
+    } else {
+        hi = g;
+        int64_t step = 1;
+        while (true) {
+            const int64_t p = hi - step;
+            if (p < 0) { lo = 0; break; }
+            if (pred(p)) { hi = p; step <<= 1; }
+            else { lo = p + 1; break; }
+        }
+    }
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        if (f[mid] < v) lo = mid + 1; else hi = mid;
+        if (pred(mid)) hi = mid; else lo = mid + 1;
     }
     return lo;
 }
-__device__ int64_t upper_bound(const double* f, int64_t nf, double v) {  // first f > v
-    int64_t lo = 0, hi = nf;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (f[mid] <= v) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
+
+__device__ unsigned long long build_item(
+    const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
+    const int32_t* __restrict__ marr, const int32_t* __restrict__ narr,
+    const double* __restrict__ ylm_p, const double* __restrict__ ylm_m, int ni, int K,
+    const double* __restrict__ coefA, const double* __restrict__ coefT,
+    const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
+    int64_t nl, int64_t nl1, double sc_re, double sc_im, Item* __restrict__ items,
+    int4* __restrict__ ranges, int32_t* __restrict__ counts, int h, int j);
 
 __global__ void k_items(const double* __restrict__ t, const double* __restrict__ f_phi,
                         const double* __restrict__ f_r, const int32_t* __restrict__ marr,
@@ -396,12 +556,34 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
                         const double* __restrict__ coefA, const double* __restrict__ coefT,
                         const int32_t* __restrict__ runs, const double* __restrict__ freq,
                         int64_t nf, int paired, int64_t nl, int64_t nl1, double sc_re,
-                        double sc_im, Item* __restrict__ items) {
+                        double sc_im, Item* __restrict__ items, int4* __restrict__ ranges,
+                        int32_t* __restrict__ counts, Header* __restrict__ hdr) {
     const int ni = nt - 1;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (int64_t)ni * K) return;
-    const int h = (int)(gid % K);
-    const int j = (int)(gid / K);
+    __shared__ unsigned long long red[4];
+    unsigned long long contrib = 0;
+    if (gid < (int64_t)ni * K) contrib = build_item(t, f_phi, f_r, marr, narr, ylm_p, ylm_m, ni, K,
+                                                     coefA, coefT, runs, freq, nf, paired, nl,
+                                                     nl1, sc_re, sc_im, items, ranges, counts,
+                                                     (int)(gid % K), (int)(gid / K));
+    for (int o = 32; o > 0; o >>= 1) contrib += __shfl_xor(contrib, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = contrib;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long v = red[0] + red[1] + red[2] + red[3];
+        if (v) atomicAdd((unsigned long long*)&hdr->contributions, v);
+    }
+}
+
+// One interval record; returns its contribution count and bumps the per-tile counters.
+__device__ unsigned long long build_item(
+    const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
+    const int32_t* __restrict__ marr, const int32_t* __restrict__ narr,
+    const double* __restrict__ ylm_p, const double* __restrict__ ylm_m, int ni, int K,
+    const double* __restrict__ coefA, const double* __restrict__ coefT,
+    const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
+    int64_t nl, int64_t nl1, double sc_re, double sc_im, Item* __restrict__ items,
+    int4* __restrict__ ranges, int32_t* __restrict__ counts, int h, int j) {
     Item& it = items[(size_t)h * ni + j];
     const int m = marr[h], n = narr[h];
     const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
@@ -414,7 +596,8 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
     if (run < 0) {  // flat interval (F_{j+1} == F_j): no support; place empty ranges at 0
         it.flags = 0;
         it.klo[0] = it.khi[0] = it.klo[1] = it.khi[1] = 0;
-        return;
+        ranges[(size_t)h * ni + j] = make_int4(0, 0, 0, 0);
+        return 0;
     }
     const int a = rr[4 * run], sg = rr[4 * run + 2];
     it.flags = 1 | (partner << 1);
@@ -453,12 +636,18 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
     const double xlo = sg > 0 ? Fj : Fj1;
     const double xhi = sg > 0 ? Fj1 : Fj;
     const bool strict_lo = sg > 0 ? (j == a) : (j + 1 == rr[4 * run + 1]);
+    // linear-interpolation guess of the grid index of a frequency value
+    const double f0 = freq[0], span = freq[nf - 1] - f0;
+    const double gsc = span > 0.0 ? (double)(nf - 1) / span : 0.0;
+    auto guess = [&](double v) { return (int64_t)floor((v - f0) * gsc); };
     // s = 0: g = -f  ->  f in (-xhi, -xlo]  (or (-xhi, -xlo) if strict)
-    int64_t lo0 = upper_bound(freq, nf, -xhi);
-    int64_t hi0 = strict_lo ? lower_bound(freq, nf, -xlo) : upper_bound(freq, nf, -xlo);
+    int64_t lo0 = grid_bound<true>(freq, nf, -xhi, guess(-xhi));
+    int64_t hi0 = strict_lo ? grid_bound<false>(freq, nf, -xlo, guess(-xlo))
+                            : grid_bound<true>(freq, nf, -xlo, guess(-xlo));
     // s = 1: g = +f  ->  f in [xlo, xhi)  (or (xlo, xhi))
-    int64_t lo1 = strict_lo ? upper_bound(freq, nf, xlo) : lower_bound(freq, nf, xlo);
-    int64_t hi1 = lower_bound(freq, nf, xhi);
+    int64_t lo1 = strict_lo ? grid_bound<true>(freq, nf, xlo, guess(xlo))
+                            : grid_bound<false>(freq, nf, xlo, guess(xlo));
+    int64_t hi1 = grid_bound<false>(freq, nf, xhi, guess(xhi));
     const int64_t lim0 = paired ? nl : nf;
     const int64_t lim1 = paired ? nl1 : (partner ? nf : 0);
     auto clampr = [](int64_t& lo, int64_t& hi, int64_t lim) {
@@ -470,37 +659,24 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
     clampr(lo1, hi1, lim1);
     it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
     it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
-}
-
-// ----------------------------------------------------------------------------------------
-// K5: per-tile counts of (interval record, sub-branch) incidences, and the contribution count C
-// (block-reduced: one 64-bit atomic per workgroup)
-// ----------------------------------------------------------------------------------------
-__global__ void k_count(const Item* __restrict__ items, int64_t nitems, int paired,
-                        int32_t* __restrict__ counts, Header* __restrict__ hdr) {
-    __shared__ unsigned long long red[4];
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    ranges[(size_t)h * ni + j] = make_int4((int)lo0, (int)hi0, (int)lo1, (int)hi1);
+    // per-tile incidence counts (K5 fused here) and contributions
     unsigned long long contrib = 0;
-    if (gid < 2 * nitems) {
-        const Item& it = items[gid >> 1];
-        const int s = (int)(gid & 1);
-        const int32_t lo = it.klo[s], hi = it.khi[s];
-        if (hi > lo) {
-            const int partner = (it.flags >> 1) & 1;
-            contrib = (unsigned long long)(hi - lo) * (paired ? 1 + partner : 1);
-            for (int tt = lo / TILE_LANES; tt <= (hi - 1) / TILE_LANES; ++tt)
-                atomicAdd(&counts[tt], 1);
-        }
+    const int mult = paired ? 1 + partner : 1;
+    if (hi0 > lo0) {
+        for (int64_t tt = lo0 / TILE_LANES; tt <= (hi0 - 1) / TILE_LANES; ++tt) atomicAdd(&counts[tt], 1);
+        contrib += (unsigned long long)(hi0 - lo0) * mult;
     }
-    for (int o = 32; o > 0; o >>= 1) contrib += __shfl_xor(contrib, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = contrib;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned long long v = red[0] + red[1] + red[2] + red[3];
-        if (v) atomicAdd((unsigned long long*)&hdr->contributions, v);
+    if (hi1 > lo1) {
+        for (int64_t tt = lo1 / TILE_LANES; tt <= (hi1 - 1) / TILE_LANES; ++tt) atomicAdd(&counts[tt], 1);
+        contrib += (unsigned long long)(hi1 - lo1) * mult;
     }
+    return contrib;
 }
 
+// ----------------------------------------------------------------------------------------
+// (K5, the per-tile counting, is fused into k_items)
+// ----------------------------------------------------------------------------------------
 // K6: exclusive scan of counts[ntiles] into offsets[ntiles + 1] (single workgroup)
 __global__ void k_scan(const int32_t* __restrict__ counts, int64_t ntiles,
                        int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
@@ -532,19 +708,21 @@ __global__ void k_scan(const int32_t* __restrict__ counts, int64_t ntiles,
 }
 
 // K7: per-tile entry lists: key = (interval record index << 1) | s
-__global__ void k_fill(const Item* __restrict__ items, int64_t nitems,
+__global__ void k_fill(const int4* __restrict__ ranges, int64_t nitems,
                        const int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
                        uint32_t* __restrict__ entries, const Header* __restrict__ hdr) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= 2 * nitems) return;
+    if (gid >= nitems) return;
     if (hdr->needed > hdr->capacity) return;
-    const Item& it = items[gid >> 1];
-    const int s = (int)(gid & 1);
-    const int32_t lo = it.klo[s], hi = it.khi[s];
-    if (hi <= lo) return;
-    for (int tt = lo / TILE_LANES; tt <= (hi - 1) / TILE_LANES; ++tt) {
-        const int32_t pos = offsets[tt] + atomicAdd(&cursor[tt], 1);
-        entries[pos] = (uint32_t)gid;
+    const int4 rg = ranges[gid];
+    const int32_t los[2] = {rg.x, rg.z}, his[2] = {rg.y, rg.w};
+    for (int s = 0; s < 2; ++s) {
+        const int32_t lo = los[s], hi = his[s];
+        if (hi <= lo) continue;
+        for (int tt = lo / TILE_LANES; tt <= (hi - 1) / TILE_LANES; ++tt) {
+            const int32_t pos = offsets[tt] + atomicAdd(&cursor[tt], 1);
+            entries[pos] = ((uint32_t)gid << 1) | (uint32_t)s;
+        }
     }
 }
 
@@ -1050,10 +1228,10 @@ int efd_spline_build(const double* x, int n, const double* y, int ninterp, doubl
                      void* stream) {
     if (!x || !y || !coef || n < 2 || ninterp <= 0 || n > MAX_NT)
         return fail(EFD_ERR_ARG, "efd_spline_build: bad arguments");
-    const int threads = 64;
+    const int threads = 64;   // spline_shared assumes 64-thread blocks
     const int blocks = (ninterp + threads - 1) / threads;
-    hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, x, n,
-                       y, ninterp, coef, (int64_t)4 * ninterp);
+    hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), sizeof(double) * 4 * n,
+                       (hipStream_t)stream, x, n, y, ninterp, coef, (int64_t)4 * ninterp);
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }
@@ -1095,6 +1273,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     double* invdp = (double*)(ws + L.invdp);
     int32_t* runs = (int32_t*)(ws + L.runs);
     Item* items = (Item*)(ws + L.items);
+    int4* ranges = (int4*)(ws + L.ranges);
     int32_t* counts = (int32_t*)(ws + L.counts);
     int32_t* offsets = (int32_t*)(ws + L.offsets);
     int32_t* cursor = (int32_t*)(ws + L.cursor);
@@ -1110,26 +1289,14 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     HIP_TRY(hipMemcpyAsync(hdr, &h0, sizeof(Header), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int32_t) * (L.ntiles + 1), st));
 
-    // K1: trajectory splines
-    hipLaunchKernelGGL(k_traj_splines, dim3(1), dim3(64), 0, st, a->t, a->phi_phi, a->phi_r,
-                       a->f_phi, a->f_r, nt, coefT, kslope, (double*)(ws + L.tscratch));
-    HIP_TRY(hipGetLastError());
-    // K2: amplitude splines (2K interpolants, Thomas scratch in place)
+    // K1-K3: trajectory splines, amplitude splines, inverse splines (one fused launch)
     {
-        const int ninterp = 2 * K;
-        const int threads = 64;
-        const int blocks = (ninterp + threads - 1) / threads;
-        hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), 0, st, a->t, nt, a->amp,
-                           ninterp, coefA, (int64_t)4 * ninterp);
-        HIP_TRY(hipGetLastError());
-    }
-    // K3: inverse splines (writes Item.gx/ic, runs)
-    {
-        const int threads = 64;
-        const int blocks = (K + threads - 1) / threads;
-        hipLaunchKernelGGL(k_inverse_splines, dim3(blocks), dim3(threads), 0, st, a->t, a->f_phi,
-                           a->f_r, a->m, a->n, nt, K, runs, items, invcp, invdp,
-                           (int32_t*)&hdr->pad[0]);
+        const int nb_amp = (2 * K + 63) / 64;
+        const int nb_inv = (K + 63) / 64;
+        hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp + nb_inv), dim3(64), sizeof(double) * 7 * nt, st,
+                           a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, a->amp, a->m, a->n, nt, K,
+                           nb_amp, coefT, kslope, (double*)(ws + L.tscratch), coefA, runs, items,
+                           invcp, invdp, (int32_t*)&hdr->pad[0]);
         HIP_TRY(hipGetLastError());
     }
     // K4: interval records
@@ -1139,21 +1306,19 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         const int64_t blocks = (total + threads - 1) / threads;
         hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(threads), 0, st, a->t, a->f_phi,
                            a->f_r, a->m, a->n, a->ylm_p, a->ylm_m, nt, K, coefA, coefT, runs,
-                           a->freq, nf, paired, nl, nl1, a->scale_re, a->scale_im, items);
+                           a->freq, nf, paired, nl, nl1, a->scale_re, a->scale_im, items, ranges,
+                           counts, hdr);
         HIP_TRY(hipGetLastError());
     }
-    // K5..K7: per-tile counts, scan, fill
+    // K6..K7: scan of the per-tile counts (made by k_items), fill
     {
         const int64_t nitems = (int64_t)(nt - 1) * K;
         const int threads = 256;
-        const int64_t blocks = (2 * nitems + threads - 1) / threads;
-        hipLaunchKernelGGL(k_count, dim3((unsigned)blocks), dim3(threads), 0, st, items, nitems,
-                           paired, counts, hdr);
-        HIP_TRY(hipGetLastError());
+        const int64_t blocks = (nitems + threads - 1) / threads;
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, L.ntiles, offsets, cursor,
                            hdr);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(threads), 0, st, items, nitems,
+        hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(threads), 0, st, ranges, nitems,
                            offsets, cursor, entries, hdr);
         HIP_TRY(hipGetLastError());
     }
