@@ -134,7 +134,7 @@ def main():
     hp = torch.empty(nf - k0, dtype=torch.complex128, device=dev)
     hc = torch.empty_like(hp)
     eng = ModeSumEngine(caustic=args.caustic)
-    eng.run(inp, freq, out=S, grid_symmetric=True, scale=w["prefactor"])  # sizes the workspace
+    eng.run(inp, freq, out=S, grid_symmetric=True, scale=w["prefactor"])  # allocates the workspace
     lib = eng.lib
     stream = torch.cuda.current_stream(dev)
     st = stream.cuda_stream
@@ -168,9 +168,9 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    ok, needed = eng.status()
+    ok, _ = eng.status()
     if not ok:
-        raise RuntimeError("tile-list workspace overflowed during the timed region")
+        raise RuntimeError(f"efd_modesum reported a device error: {_lib.last_error(lib)}")
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     C = eng.contributions()
 

@@ -11,22 +11,24 @@
 // The oracle (oracle/fd_oracle.py) states the same maths in numpy; tests pin them together.
 //
 // Pipeline (all on one stream, no host sync, no allocation):
-//   K1 k_traj_splines     1 wave: not-a-knot splines of Phi_phi, Phi_r, f_phi, f_r and of the
-//                         knot derivatives f_phi'(t_i), f_r'(t_i) (for F'' as in notebook :583)
-//   K2 k_spline_shared    1 lane per amplitude interpolant (Re/Im A_k): 2K lanes
-//   K3 k_inverse_splines  1 lane per harmonic: F knots, monotonic runs, inverse spline per run
+//   K1-K3 k_prep          one launch, three independent roles by workgroup:
+//                         - 1 wave: not-a-knot splines of Phi_phi, Phi_r, f_phi, f_r and of the
+//                           knot derivatives f_phi'(t_i), f_r'(t_i) (for F'' as notebook :583)
+//                         - 1 lane per amplitude interpolant (Re/Im A_k, 2K lanes), sharing one
+//                           LDS factorisation of the knot matrix
+//                         - 1 lane per harmonic: F knots, monotonic runs, inverse spline per run
 //   K4 k_items            1 thread per (harmonic, knot interval): gathers every cubic the SPA
 //                         needs for that interval into one 256-B record + its bin (lane) ranges
-//   K5 k_count            1 thread per (record, sub-branch): per-tile incidence counts, C
-//   K6 k_scan             exclusive scan of per-tile counts
-//   K7 k_fill             per-tile lists of record keys
-//   K8 k_modesum          OUTPUT-STATIONARY: one 4-wave workgroup per tile of 256*BPL bins;
+//   K5 k_segment_slots    1 thread per (harmonic, run, sub-branch): its segment of records,
+//      k_segment_compact  trimmed of clamped empty records; then compacted in slot order
+//   K6 k_modesum          OUTPUT-STATIONARY: one 4-wave workgroup per tile of 256*BPL bins;
 //                         each lane owns BPL bins (and their mirrors -f when the grid is
 //                         symmetric: the +m branch and its -m partner share t(g), the
 //                         amplitude/phase splines and sin/cos, so one evaluation feeds two
-//                         bins); the tile's record list is sorted in LDS (deterministic
-//                         summation order), records are streamed through a double-buffered LDS
-//                         stage, and results are written once -- no atomics on the spectrum.
+//                         bins); each tile builds its own record list in LDS from the segment
+//                         table (bisection, fixed order -> bitwise reproducible), streams the
+//                         records through a double-buffered LDS stage, and writes its bins once
+//                         -- no atomics, no global lists, no host synchronisation.
 // The SPA evaluation is FP64 VALU work (phases reach ~1e7 rad); MFMA is not applicable.
 
 #include <hip/hip_runtime.h>
@@ -53,7 +55,8 @@ constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 constexpr int XCD_GROUP = 4;        // consecutive tiles per XCD in the k_modesum dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
-constexpr int LDS_SORT_CAP = 4096;  // tile-list entries sorted in LDS
+constexpr int KEYCAP = 2048;        // record keys per tile pass held in LDS
+constexpr int SEGWIN = 1024;        // segments examined per window when building a tile list
 constexpr int NC = 32;              // interval records per LDS stage in k_modesum
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
@@ -96,17 +99,16 @@ struct __attribute__((aligned(16))) Item {
 static_assert(sizeof(Item) == 256, "Item must be 256 B");
 
 struct Header {
-    int64_t needed;       // incidences required by the last call
-    int64_t capacity;     // incidences the workspace holds
+    int64_t reserved0;
+    int64_t reserved1;
     int64_t contributions;
     int64_t pad0;
     int64_t pad[4];
 };
 
 struct Layout {
-    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, counts,
-        offsets,
-        cursor, entries, total;
+    size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
+        seginfo, nseg, slotlh, slotinfo, slotcnt, total;
     int64_t ntiles, nlanes, capacity;
 };
 
@@ -130,10 +132,12 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int64_t capacity, int pair
     L.runs = take(sizeof(int32_t) * 4 * MAXRUNS * K);
     L.items = take(sizeof(Item) * ni * K);
     L.ranges = take(sizeof(int4) * ni * K);
-    L.counts = take(sizeof(int32_t) * (L.ntiles + 1));
-    L.offsets = take(sizeof(int32_t) * (L.ntiles + 1));
-    L.cursor = take(sizeof(int32_t) * (L.ntiles + 1));
-    L.entries = take(sizeof(uint32_t) * capacity);
+    L.seglh = take(sizeof(int2) * 2 * MAXRUNS * K);
+    L.seginfo = take(sizeof(int4) * 2 * MAXRUNS * K);
+    L.nseg = take(sizeof(int32_t));
+    L.slotlh = take(sizeof(int2) * 2 * MAXRUNS * K);
+    L.slotinfo = take(sizeof(int4) * 2 * MAXRUNS * K);
+    L.slotcnt = take(sizeof(int32_t) * ((2 * MAXRUNS * K + 255) / 256));
     L.total = off;
     return L;
 }
@@ -547,7 +551,7 @@ __device__ unsigned long long build_item(
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
     int64_t nl, int64_t nl1, double sc_re, double sc_im, Item* __restrict__ items,
-    int4* __restrict__ ranges, int32_t* __restrict__ counts, int h, int j);
+    int4* __restrict__ ranges, int h, int j);
 
 __global__ void k_items(const double* __restrict__ t, const double* __restrict__ f_phi,
                         const double* __restrict__ f_r, const int32_t* __restrict__ marr,
@@ -557,14 +561,14 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
                         const int32_t* __restrict__ runs, const double* __restrict__ freq,
                         int64_t nf, int paired, int64_t nl, int64_t nl1, double sc_re,
                         double sc_im, Item* __restrict__ items, int4* __restrict__ ranges,
-                        int32_t* __restrict__ counts, Header* __restrict__ hdr) {
+                        Header* __restrict__ hdr) {
     const int ni = nt - 1;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     __shared__ unsigned long long red[4];
     unsigned long long contrib = 0;
     if (gid < (int64_t)ni * K) contrib = build_item(t, f_phi, f_r, marr, narr, ylm_p, ylm_m, ni, K,
                                                      coefA, coefT, runs, freq, nf, paired, nl,
-                                                     nl1, sc_re, sc_im, items, ranges, counts,
+                                                     nl1, sc_re, sc_im, items, ranges,
                                                      (int)(gid % K), (int)(gid / K));
     for (int o = 32; o > 0; o >>= 1) contrib += __shfl_xor(contrib, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = contrib;
@@ -583,7 +587,7 @@ __device__ unsigned long long build_item(
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
     int64_t nl, int64_t nl1, double sc_re, double sc_im, Item* __restrict__ items,
-    int4* __restrict__ ranges, int32_t* __restrict__ counts, int h, int j) {
+    int4* __restrict__ ranges, int h, int j) {
     Item& it = items[(size_t)h * ni + j];
     const int m = marr[h], n = narr[h];
     const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
@@ -660,70 +664,107 @@ __device__ unsigned long long build_item(
     it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
     it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
     ranges[(size_t)h * ni + j] = make_int4((int)lo0, (int)hi0, (int)lo1, (int)hi1);
-    // per-tile incidence counts (K5 fused here) and contributions
-    unsigned long long contrib = 0;
+    // contributions C (harmonic branch x bin evaluations) for the roofline
     const int mult = paired ? 1 + partner : 1;
-    if (hi0 > lo0) {
-        for (int64_t tt = lo0 / TILE_LANES; tt <= (hi0 - 1) / TILE_LANES; ++tt) atomicAdd(&counts[tt], 1);
-        contrib += (unsigned long long)(hi0 - lo0) * mult;
-    }
-    if (hi1 > lo1) {
-        for (int64_t tt = lo1 / TILE_LANES; tt <= (hi1 - 1) / TILE_LANES; ++tt) atomicAdd(&counts[tt], 1);
-        contrib += (unsigned long long)(hi1 - lo1) * mult;
-    }
-    return contrib;
+    return (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
 }
 
 // ----------------------------------------------------------------------------------------
-// (K5, the per-tile counting, is fused into k_items)
+// K5: segment table. A segment is (harmonic, monotonic run, sub-branch s) with a non-empty lane
+// range; its interval records are consecutive (h * ni + j, j in [ja, jb)) and, walked in lane
+// order (j += dir), cover consecutive, disjoint lane ranges. K5a: one thread per (h, run, s)
+// slot writes the slot's segment (or an empty marker) into a dense table plus a per-block count;
+// K5b compacts the non-empty slots in slot order (block offsets from the counts), so the table
+// is deterministic.
+// seglh = (lo, hi) lane range; seginfo = (first record, count, dir, s).
 // ----------------------------------------------------------------------------------------
-// K6: exclusive scan of counts[ntiles] into offsets[ntiles + 1] (single workgroup)
-__global__ void k_scan(const int32_t* __restrict__ counts, int64_t ntiles,
-                       int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
-                       Header* __restrict__ hdr) {
-    __shared__ int64_t part[1024];
-    const int tid = threadIdx.x;
-    const int64_t chunk = (ntiles + blockDim.x - 1) / blockDim.x;
-    const int64_t b0 = tid * chunk, b1 = min(ntiles, b0 + chunk);
-    int64_t s = 0;
-    for (int64_t i = b0; i < b1; ++i) s += counts[i];
-    part[tid] = s;
-    __syncthreads();
-    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-        int64_t v = (tid >= off) ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    int64_t run = part[tid] - s;
-    for (int64_t i = b0; i < b1; ++i) {
-        offsets[i] = (int32_t)min(run, (int64_t)INT32_MAX);
-        cursor[i] = 0;
-        run += counts[i];
-    }
-    if (tid == blockDim.x - 1) {
-        offsets[ntiles] = (int32_t)min(part[tid], (int64_t)INT32_MAX);
-        hdr->needed = part[tid];
-    }
-}
-
-// K7: per-tile entry lists: key = (interval record index << 1) | s
-__global__ void k_fill(const int4* __restrict__ ranges, int64_t nitems,
-                       const int32_t* __restrict__ offsets, int32_t* __restrict__ cursor,
-                       uint32_t* __restrict__ entries, const Header* __restrict__ hdr) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= nitems) return;
-    if (hdr->needed > hdr->capacity) return;
-    const int4 rg = ranges[gid];
-    const int32_t los[2] = {rg.x, rg.z}, his[2] = {rg.y, rg.w};
-    for (int s = 0; s < 2; ++s) {
-        const int32_t lo = los[s], hi = his[s];
-        if (hi <= lo) continue;
-        for (int tt = lo / TILE_LANES; tt <= (hi - 1) / TILE_LANES; ++tt) {
-            const int32_t pos = offsets[tt] + atomicAdd(&cursor[tt], 1);
-            entries[pos] = ((uint32_t)gid << 1) | (uint32_t)s;
+__global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict__ runs,
+                                                       const int4* __restrict__ ranges, int nt,
+                                                       int K, int lim0, int lim1,
+                                                       int2* __restrict__ slot_lh,
+                                                       int4* __restrict__ slot_info,
+                                                       int32_t* __restrict__ blockcnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int wc[4];
+    bool valid = false;
+    if (i < K * MAXRUNS * 2) {
+        const int h = i / (2 * MAXRUNS), r = (i >> 1) % MAXRUNS, sb = i & 1;
+        const int ni = nt - 1;
+        int2 lh = make_int2(0, 0);
+        int4 info = make_int4(0, 0, 0, 0);
+        const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS + 4 * r;
+        if (rr[2] != 0) {
+            const int ja = rr[0], jb = rr[1], n = jb - ja;
+            const int dir = (sb == 0) ? -rr[2] : rr[2];   // s = 0 walks g downward in lane order
+            const int lim = sb ? lim1 : lim0;
+            const int4* rg = ranges + (size_t)h * ni;
+            // Records whose branch lies outside the lane range are empty and clamped to its
+            // ends (lane 0 or lim); they sit at the two ends of the segment in lane order and
+            // are trimmed, so the tiles holding lane 0 and lim do not collect all of them.
+            int lo = 0, hi = n;                            // first p with khi > 0
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const int4 v = rg[dir > 0 ? ja + mid : jb - 1 - mid];
+                if ((sb ? v.w : v.y) > 0) hi = mid; else lo = mid + 1;
+            }
+            const int pa = lo;
+            hi = n;                                        // first p with klo >= lim
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const int4 v = rg[dir > 0 ? ja + mid : jb - 1 - mid];
+                if ((sb ? v.z : v.x) >= lim) hi = mid; else lo = mid + 1;
+            }
+            const int pb = lo;
+            if (pb > pa) {
+                const int4 rf = rg[dir > 0 ? ja + pa : jb - 1 - pa];
+                const int4 rl = rg[dir > 0 ? ja + pb - 1 : jb - pb];
+                const int klo = sb ? rf.z : rf.x, khi = sb ? rl.w : rl.y;
+                if (khi > klo) {
+                    lh = make_int2(klo, khi);
+                    const int jfirst = dir > 0 ? ja + pa : jb - pb;   // lowest record index kept
+                    info = make_int4(h * ni + jfirst, pb - pa, dir, sb);
+                }
+            }
         }
+        slot_lh[i] = lh;
+        slot_info[i] = info;
+        valid = info.y > 0;
     }
+    const unsigned long long bal = __ballot(valid);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) blockcnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+// one workgroup per slot block: its output offset is the sum of the earlier blocks' counts
+__global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict__ slot_lh,
+                                                         const int4* __restrict__ slot_info,
+                                                         const int32_t* __restrict__ blockcnt,
+                                                         int nslot, int2* __restrict__ seglh,
+                                                         int4* __restrict__ seginfo,
+                                                         int32_t* __restrict__ nseg) {
+    __shared__ int wc[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int blk = blockIdx.x;
+    int before = 0;
+    for (int b = tid; b < blk; b += 256) before += blockcnt[b];
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o);
+    if (lane == 0) wc[wave] = before;
+    __syncthreads();
+    const int base = wc[0] + wc[1] + wc[2] + wc[3];
+    __syncthreads();
+    const int i = blk * 256 + tid;
+    int4 info = make_int4(0, 0, 0, 0);
+    if (i < nslot) info = slot_info[i];
+    const bool valid = info.y > 0;
+    const unsigned long long bal = __ballot(valid);
+    if (lane == 0) wc[wave] = __popcll(bal);
+    __syncthreads();
+    int pos = base;
+    for (int w = 0; w < wave; ++w) pos += wc[w];
+    pos += __popcll(bal & ((1ull << lane) - 1ull));
+    if (valid) { seglh[pos] = slot_lh[i]; seginfo[pos] = info; }
+    if (blk == (int)gridDim.x - 1 && tid == 0) *nseg = base + wc[0] + wc[1] + wc[2] + wc[3];
 }
 
 // ----------------------------------------------------------------------------------------
@@ -982,14 +1023,18 @@ __device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double 
 // ----------------------------------------------------------------------------------------
 template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) void k_modesum(
-    const Item* __restrict__ items, const int32_t* __restrict__ offsets,
-    const uint32_t* __restrict__ entries, const double* __restrict__ freq, int64_t nf,
+    const Item* __restrict__ items, const int4* __restrict__ ranges,
+    const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
+    const int32_t* __restrict__ nsegp, const double* __restrict__ freq, int64_t nf,
     int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ marr,
     const int32_t* __restrict__ narr, const double* __restrict__ t,
-    const double* __restrict__ coefA, const double* __restrict__ coefT,
-    const Header* __restrict__ hdr, int accumulate, double* __restrict__ out) {
-    __shared__ uint32_t keys[LDS_SORT_CAP];
+    const double* __restrict__ coefA, const double* __restrict__ coefT, int accumulate,
+    double* __restrict__ out) {
+    __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
+    __shared__ int part[TILE];
+    __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
+    __shared__ int wcnt[4];
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
     // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
@@ -1003,32 +1048,17 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     if (tile >= ntiles) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const bool valid_call = hdr->needed <= hdr->capacity;
+    const int ni = nt - 1;
 
-    const int32_t off = offsets[tile];
-    const int32_t cnt = valid_call ? offsets[tile + 1] - off : 0;
-    const bool sorted = cnt <= LDS_SORT_CAP;
-    if (sorted) {
-        int p2 = 1;
-        while (p2 < cnt) p2 <<= 1;
-        for (int i = tid; i < p2; i += TILE) keys[i] = (i < cnt) ? entries[off + i] : 0xffffffffu;
-        __syncthreads();
-        for (int size = 2; size <= p2; size <<= 1) {   // bitonic sort
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                for (int i = tid; i < p2; i += TILE) {
-                    const int pr = i ^ stride;
-                    if (pr > i) {
-                        const uint32_t a = keys[i], bb = keys[pr];
-                        const bool up = (i & size) == 0;
-                        if ((a > bb) == up) { keys[i] = bb; keys[pr] = a; }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-    }
-#define key_at(e) (sorted ? keys[(e)] : entries[off + (e)])
-
+    // ---- the tile's record list, built in LDS from the segment table (no global list, no
+    // atomics). Segments are taken in windows of SEGWIN: (1) each thread tests SEGWIN/TILE
+    // segments (strided, coalesced) for overlap with the tile, and a ballot compaction keeps the
+    // hits in segment order; (2) one thread per hit bisects that segment's records for the
+    // sub-range [p0, p0 + n) reaching into the tile; (3) a block scan places the keys. Keys go to
+    // keys[] until KEYCAP, then the chunked evaluation below drains them. The summation order
+    // (segment, then lane order) is fixed, so the result is bitwise reproducible.
+    const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
+    const int nseg = *nsegp;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
     const int32_t w_hi = w_lo + 64 * BPL;
@@ -1041,7 +1071,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
 
-    // staging: a record is 16 pieces of 16 B; NC records = 16 NC pieces, PPT per thread.
+    // staging: a record is 16 pieces of 16 B; NC records = 16 NC pieces, two per thread.
     // (Plain registers, no lambda-captured arrays: those were demoted to scratch memory.)
     static_assert(16 * NC == 2 * TILE, "staging assumes two 16-B pieces per thread");
     const int pc0 = tid, pc1 = tid + TILE;
@@ -1049,91 +1079,192 @@ __global__ __launch_bounds__(TILE) void k_modesum(
 #define EFD_FETCH(c)                                                                          \
     do {                                                                                      \
         const int e0_ = (c) * NC + (pc0 >> 4), e1_ = (c) * NC + (pc1 >> 4);                   \
-        if (e0_ < cnt) pre0 = reinterpret_cast<const uint4*>(items + (key_at(e0_) >> 1))[pc0 & 15]; \
-        if (e1_ < cnt) pre1 = reinterpret_cast<const uint4*>(items + (key_at(e1_) >> 1))[pc1 & 15]; \
+        if (e0_ < cnt) pre0 = reinterpret_cast<const uint4*>(items + (keys[e0_] >> 1))[pc0 & 15]; \
+        if (e1_ < cnt) pre1 = reinterpret_cast<const uint4*>(items + (keys[e1_] >> 1))[pc1 & 15]; \
     } while (0)
 #define EFD_STORE(buf)                                                                        \
     do {                                                                                      \
         reinterpret_cast<uint4*>(&stage[(buf)][pc0 >> 4])[pc0 & 15] = pre0;                   \
         reinterpret_cast<uint4*>(&stage[(buf)][pc1 >> 4])[pc1 & 15] = pre1;                   \
     } while (0)
-    const int nchunk = (cnt + NC - 1) / NC;
-    if (nchunk > 0) {
+
+    int win = 0;        // next segment window
+    int nhit = 0;       // overlapping segments of the current window
+    int wtotal = 0;     // keys of the current window
+    int wdone = 0;      // keys of the current window already written
+    int nkeys = 0;      // keys waiting in keys[]
+    while (true) {
+        // ---- fill keys[] (block-uniform control flow)
+        while (nkeys < KEYCAP) {
+            if (wdone == wtotal) {                 // need a new window of segments
+                if (win >= nseg) break;
+                // (1) overlap test + ordered compaction
+                nhit = 0;
+                for (int row = 0; row < SEGWIN / TILE; ++row) {
+                    const int sgi = win + row * TILE + tid;
+                    bool hit = false;
+                    if (sgi < nseg) {
+                        const int2 lh = seglh[sgi];
+                        hit = lh.y > tlo && lh.x < thi;
+                    }
+                    const unsigned long long bal = __ballot(hit);
+                    if (lane == 0) wcnt[wave] = __popcll(bal);
+                    __syncthreads();
+                    int before = nhit;
+                    for (int w = 0; w < wave; ++w) before += wcnt[w];
+                    if (hit) {
+                        const unsigned long long below = bal & ((1ull << lane) - 1ull);
+                        hits[before + __popcll(below)] = sgi;
+                    }
+                    nhit += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+                    __syncthreads();
+                }
+                win += SEGWIN;
+                // (2) bisect each hit segment for its records reaching into the tile
+                for (int i = tid; i < nhit; i += TILE) {
+                    const int4 info = seginfo[hits[i]];
+                    const int base = info.x, n = info.y, dir = info.z, sb = info.w;
+                    int lo = 0, hi = n;            // first p (lane order) with khi > tlo
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        const int4 rg = ranges[base + (dir > 0 ? mid : n - 1 - mid)];
+                        if ((sb ? rg.w : rg.y) > tlo) hi = mid; else lo = mid + 1;
+                    }
+                    const int p0 = lo;
+                    hi = n;                        // first p with klo >= thi
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        const int4 rg = ranges[base + (dir > 0 ? mid : n - 1 - mid)];
+                        if ((sb ? rg.z : rg.x) >= thi) hi = mid; else lo = mid + 1;
+                    }
+                    hp0[i] = p0;
+                    hcnt[i] = lo - p0;
+                }
+                __syncthreads();
+                // (3) exclusive scan of the counts (serial per thread over a block of hits)
+                const int hper = (nhit + TILE - 1) / TILE;
+                const int h0 = min(nhit, tid * hper), h1 = min(nhit, h0 + hper);
+                int mine = 0;
+                for (int i = h0; i < h1; ++i) mine += hcnt[i];
+                part[tid] = mine;
+                __syncthreads();
+                for (int o = 1; o < TILE; o <<= 1) {
+                    const int v = tid >= o ? part[tid - o] : 0;
+                    __syncthreads();
+                    part[tid] += v;
+                    __syncthreads();
+                }
+                int run_off = part[tid] - mine;
+                for (int i = h0; i < h1; ++i) { hoff[i] = run_off; run_off += hcnt[i]; }
+                wtotal = part[TILE - 1];
+                wdone = 0;
+                __syncthreads();
+                continue;
+            }
+            // write keys [wdone, wdone + take) of this window at keys[nkeys ...], scattered by
+            // the bijection x -> x * P mod take (P prime, take % P != 0): a segment's records
+            // cover neighbouring lanes, i.e. mostly one wave, and unscattered a chunk of NC
+            // consecutive records would keep one wave busy while the others wait at its barrier
+            const int take = min(KEYCAP - nkeys, wtotal - wdone);
+            const int P = (take % 97) ? 97 : 101;
+            for (int i = tid; i < nhit; i += TILE) {
+                const int o = hoff[i], c = hcnt[i];
+                const int lo = max(o, wdone), hi = min(o + c, wdone + take);
+                if (lo >= hi) continue;
+                const int4 info = seginfo[hits[i]];
+                for (int g = lo; g < hi; ++g) {
+                    const int p = hp0[i] + (g - o);
+                    const int j = info.z > 0 ? p : info.y - 1 - p;
+                    keys[nkeys + (int)(((unsigned)(g - wdone) * (unsigned)P) % (unsigned)take)] =
+                        ((uint32_t)(info.x + j) << 1) | (uint32_t)info.w;
+                }
+            }
+            nkeys += take;
+            wdone += take;
+            __syncthreads();
+        }
+        if (nkeys == 0) break;
+#ifdef EFD_EXP_NOEVAL
+        if (nkeys < 0x7fffffff) { own_r[0] += nkeys; nkeys = 0; continue; }
+#endif
+
+        // ---- evaluate the nkeys records in chunks of NC through the double-buffered stage
+        const int cnt = nkeys;
+        const int nchunk = (cnt + NC - 1) / NC;
         EFD_FETCH(0);
         EFD_STORE(0);
-    }
-    __syncthreads();
+        __syncthreads();
 
-    for (int c = 0; c < nchunk; ++c) {
-        if (c + 1 < nchunk) EFD_FETCH(c + 1);             // loads in flight during the chunk
-        const int nin = min(NC, cnt - c * NC);
-        const Item* stg = stage[c & 1];
-        for (int ii = 0; ii < nin; ++ii) {
-            const uint32_t key = rfl(key_at(c * NC + ii));
-            // S = 0: g = -f (parent at the own bin, partner at the mirror); S = 1: g = +f
-            // (partner at the own bin, parent at the mirror). Y- is zero for m = 0 harmonics.
-            const int s = (int)(key & 1);
-            const Item* it = stg + ii;
-            const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
-            const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
-            if (khi <= w_lo || klo >= w_hi) continue;     // misses this wave's chunk
-            const double gs = s ? 1.0 : -1.0;
-            bool okall = true;
-            bool act[BPL];
-            double zr[BPL], zi[BPL];
-#pragma unroll
-            for (int i = 0; i < BPL; ++i) {
-                const int32_t k = w_lo + 64 * i + lane;
-                act[i] = k >= klo && k < khi;
-                bool ok;
-#ifdef EFD_EXP_NOCOMPUTE
-                zr[i] = fk[i] * it->ar[0]; zi[i] = gs * it->ai[1]; ok = true;
-#else
-                spa_fast<CAUSTIC>(it, gs * fk[i], zr[i], zi[i], ok);
-#endif
-                zr[i] = act[i] ? zr[i] : 0.0;
-                zi[i] = act[i] ? zi[i] : 0.0;
-                okall = okall && (ok || !act[i]);
-                act[i] = act[i] && !ok;   // lanes left for the general path
-            }
-            if (__builtin_expect(!__all(okall), 0)) {     // cold: general path for some lanes
-                const Item* git = items + (key >> 1);
-                const int h = git->h;
+        for (int c = 0; c < nchunk; ++c) {
+            if (c + 1 < nchunk) EFD_FETCH(c + 1);             // loads in flight during the chunk
+            const int nin = min(NC, cnt - c * NC);
+            const Item* stg = stage[c & 1];
+            for (int ii = 0; ii < nin; ++ii) {
+                const uint32_t key = rfl(keys[c * NC + ii]);
+                // S = 0: g = -f (parent at the own bin, partner at the mirror); S = 1: g = +f
+                // (partner at the own bin, parent at the mirror). Y- is zero for m = 0 harmonics.
+                const int s = (int)(key & 1);
+                const Item* it = stg + ii;
+                const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
+                const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
+                if (khi <= w_lo || klo >= w_hi) continue;     // misses this wave's chunk
+                const double gs = s ? 1.0 : -1.0;
+                bool okall = true;
+                bool act[BPL];
+                double zr[BPL], zi[BPL];
 #pragma unroll
                 for (int i = 0; i < BPL; ++i) {
-                    if (act[i]) {
-                        const double2 zg = spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K,
-                                                                marr[h], narr[h], coefA, coefT);
-                        zr[i] = zg.x;
-                        zi[i] = zg.y;
+                    const int32_t k = w_lo + 64 * i + lane;
+                    act[i] = k >= klo && k < khi;
+                    bool ok;
+#ifdef EFD_EXP_NOCOMPUTE
+                    zr[i] = fk[i] * it->ar[0]; zi[i] = gs * it->ai[1]; ok = true;
+#else
+                    spa_fast<CAUSTIC>(it, gs * fk[i], zr[i], zi[i], ok);
+#endif
+                    zr[i] = act[i] ? zr[i] : 0.0;
+                    zi[i] = act[i] ? zi[i] : 0.0;
+                    okall = okall && (ok || !act[i]);
+                    act[i] = act[i] && !ok;   // lanes left for the general path
+                }
+                if (__builtin_expect(!__all(okall), 0)) {     // cold: general path for some lanes
+                    const Item* git = items + (key >> 1);
+                    const int h = git->h;
+#pragma unroll
+                    for (int i = 0; i < BPL; ++i) {
+                        if (act[i]) {
+                            const double2 zg = spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K,
+                                                                    marr[h], narr[h], coefA, coefT);
+                            zr[i] = zg.x;
+                            zi[i] = zg.y;
+                        }
+                    }
+                }
+                const double ypr = it->yp[0], ypi = it->yp[1];
+                const double ymr = it->ym[0], ymi = it->ym[1];
+#pragma unroll
+                for (int i = 0; i < BPL; ++i) {
+                    // P = Y+ z (parent, f = -g), Q = Y- conj(z) (partner, f = +g)
+                    const double pr = ypr * zr[i] - ypi * zi[i], pi = ypr * zi[i] + ypi * zr[i];
+                    const double qr = ymr * zr[i] + ymi * zi[i], qi = ymi * zr[i] - ymr * zi[i];
+                    own_r[i] += s ? qr : pr;
+                    own_i[i] += s ? qi : pi;
+                    if (PAIRED) {
+                        mir_r[i] += s ? pr : qr;
+                        mir_i[i] += s ? pi : qi;
                     }
                 }
             }
-            const double ypr = it->yp[0], ypi = it->yp[1];
-            const double ymr = it->ym[0], ymi = it->ym[1];
-#pragma unroll
-            for (int i = 0; i < BPL; ++i) {
-                // P = Y+ z (parent, f = -g), Q = Y- conj(z) (partner, f = +g)
-                const double pr = ypr * zr[i] - ypi * zi[i], pi = ypr * zi[i] + ypi * zr[i];
-                const double qr = ymr * zr[i] + ymi * zi[i], qi = ymi * zr[i] - ymr * zi[i];
-                own_r[i] += s ? qr : pr;
-                own_i[i] += s ? qi : pi;
-                if (PAIRED) {
-                    mir_r[i] += s ? pr : qr;
-                    mir_i[i] += s ? pi : qi;
-                }
-            }
+            // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
+            // barrier that closed it; the barrier below publishes the new stage for chunk c+1
+            if (c + 1 < nchunk) EFD_STORE((c + 1) & 1);
+            __syncthreads();
         }
-        // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
-        // barrier that closed it; the barrier below publishes the new stage for chunk c+1
-        if (c + 1 < nchunk) EFD_STORE((c + 1) & 1);
-        __syncthreads();
+        nkeys = 0;
     }
 #undef EFD_FETCH
 #undef EFD_STORE
-#undef key_at
 
-    if (!valid_call) return;
     double2* o = reinterpret_cast<double2*>(out);
 #pragma unroll
     for (int i = 0; i < BPL; ++i) {
@@ -1253,15 +1384,9 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     if (a->caustic != EFD_CAUSTIC_SPA && a->caustic != EFD_CAUSTIC_UNIFORM)
         return fail(EFD_ERR_ARG, "efd_modesum: unknown caustic mode");
     const int paired = a->grid_symmetric ? 1 : 0;
-    // capacity from the bytes we were given
-    Layout L0 = make_layout(a->nt, a->K, a->nf, 0, paired);
-    if (workspace_bytes < L0.total) return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small");
-    const int64_t cap = (int64_t)((workspace_bytes - L0.total) / sizeof(uint32_t));
-    Layout L = make_layout(a->nt, a->K, a->nf, cap, paired);
-    while (L.total > workspace_bytes && L.capacity > 0) {
-        L = make_layout(a->nt, a->K, a->nf, L.capacity - 64, paired);
-    }
-    if (L.total > workspace_bytes) return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small");
+    const Layout L = make_layout(a->nt, a->K, a->nf, 0, paired);
+    if (workspace_bytes < L.total)
+        return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small (see efd_modesum_workspace_bytes)");
 
     hipStream_t st = (hipStream_t)stream;
     char* ws = (char*)workspace;
@@ -1274,20 +1399,16 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     int32_t* runs = (int32_t*)(ws + L.runs);
     Item* items = (Item*)(ws + L.items);
     int4* ranges = (int4*)(ws + L.ranges);
-    int32_t* counts = (int32_t*)(ws + L.counts);
-    int32_t* offsets = (int32_t*)(ws + L.offsets);
-    int32_t* cursor = (int32_t*)(ws + L.cursor);
-    uint32_t* entries = (uint32_t*)(ws + L.entries);
+    int2* seglh = (int2*)(ws + L.seglh);
+    int4* seginfo = (int4*)(ws + L.seginfo);
+    int32_t* nseg = (int32_t*)(ws + L.nseg);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
     const int64_t nl = L.nlanes;
     const int64_t nl1 = paired ? ((nf % 2) ? nl - 1 : nl) : nf;
 
-    Header h0{};
-    h0.capacity = L.capacity;
-    HIP_TRY(hipMemcpyAsync(hdr, &h0, sizeof(Header), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int32_t) * (L.ntiles + 1), st));
+    HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
 
     // K1-K3: trajectory splines, amplitude splines, inverse splines (one fused launch)
     {
@@ -1307,21 +1428,24 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(threads), 0, st, a->t, a->f_phi,
                            a->f_r, a->m, a->n, a->ylm_p, a->ylm_m, nt, K, coefA, coefT, runs,
                            a->freq, nf, paired, nl, nl1, a->scale_re, a->scale_im, items, ranges,
-                           counts, hdr);
-        HIP_TRY(hipGetLastError());
-    }
-    // K6..K7: scan of the per-tile counts (made by k_items), fill
-    {
-        const int64_t nitems = (int64_t)(nt - 1) * K;
-        const int threads = 256;
-        const int64_t blocks = (nitems + threads - 1) / threads;
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, L.ntiles, offsets, cursor,
                            hdr);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(threads), 0, st, ranges, nitems,
-                           offsets, cursor, entries, hdr);
-        HIP_TRY(hipGetLastError());
     }
+    // K5: segment table
+    {
+        const int nslot = K * MAXRUNS * 2;
+        int2* slot_lh = (int2*)(ws + L.slotlh);
+        int4* slot_info = (int4*)(ws + L.slotinfo);
+        const int nblk = (nslot + 255) / 256;
+        int32_t* blockcnt = (int32_t*)(ws + L.slotcnt);
+        hipLaunchKernelGGL(k_segment_slots, dim3(nblk), dim3(256), 0, st, runs, ranges, nt, K,
+                           (int)(paired ? nl : nf), (int)(paired ? nl1 : nf), slot_lh, slot_info,
+                           blockcnt);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_segment_compact, dim3(nblk), dim3(256), 0, st, slot_lh, slot_info,
+                           blockcnt, nslot, seglh, seginfo, nseg);
+    }
+    HIP_TRY(hipGetLastError());
     // K8: mode sum
     {
         const int64_t gq = 8 * XCD_GROUP;
@@ -1329,8 +1453,8 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
-    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, offsets, entries,       \
-                       a->freq, nf, nl, L.ntiles, nt, K, a->m, a->n, a->t, coefA, coefT, hdr, \
+    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh, seginfo,  \
+                       nseg, a->freq, nf, nl, L.ntiles, nt, K, a->m, a->n, a->t, coefA, coefT,    \
                        acc, a->out)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
@@ -1351,10 +1475,9 @@ int efd_modesum_status(const void* workspace, int64_t* needed, void* stream) {
     Header h{};
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
-    if (needed) *needed = h.needed;
-    if (h.pad[0] != 0) return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
-    if (h.needed > h.capacity)
-        return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small for the tile lists");
+    if (needed) *needed = 0;   // tile lists are built in LDS: nothing to size on the host
+    if (h.pad[0] != 0)
+        return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
     return EFD_OK;
 }
 

@@ -89,19 +89,18 @@ class DeviceInputs:
 class ModeSumEngine:
     """Owns the workspace and launches efd_modesum on the current torch stream."""
 
-    def __init__(self, caustic="uniform", initial_incidences=1 << 20):
+    def __init__(self, caustic="uniform"):
         if caustic not in CAUSTIC_MODES:
             raise ValueError(f"caustic must be one of {sorted(CAUSTIC_MODES)}")
         self.caustic = caustic
         self.lib = _lib.load()
         self._ws = None
         self._ws_key = None
-        self._cap = int(initial_incidences)
         self.last_contributions = None
 
     def _workspace(self, nt, K, nf, device):
         torch = _torch()
-        nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf, self._cap))
+        nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf, 0))
         if nbytes == 0:
             raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
         if self._ws is None or self._ws.numel() < nbytes or self._ws.device != device:
@@ -134,8 +133,6 @@ class ModeSumEngine:
         st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         needed = ctypes.c_int64(0)
         rc = self.lib.efd_modesum_status(self._ws.data_ptr(), ctypes.byref(needed), st)
-        if rc not in (_lib.EFD_OK, _lib.EFD_ERR_WORKSPACE):
-            _lib.check(rc, "efd_modesum_status", self.lib)
         return rc == _lib.EFD_OK, int(needed.value)
 
     def contributions(self, stream=None):
@@ -147,21 +144,20 @@ class ModeSumEngine:
                    "efd_modesum_contributions", self.lib)
         return int(c.value)
 
-    def run(self, inp, freq, out=None, grid_symmetric=None, scale=1.0 + 0.0j, accumulate=False):
-        """Launch, check the tile-list capacity (one sync), regrow and relaunch if needed."""
+    def run(self, inp, freq, out=None, grid_symmetric=None, scale=1.0 + 0.0j, accumulate=False,
+            check=True):
+        """Launch on the current stream; with check=True synchronise and surface device errors."""
         torch = _torch()
         if grid_symmetric is None:
             grid_symmetric = is_symmetric(freq.detach().cpu().numpy())
         if out is None:
             out = torch.empty(int(freq.numel()), dtype=torch.complex128, device=freq.device)
-        fout = torch.view_as_real(out)
-        for _ in range(8):
-            self.launch(inp, freq, fout, grid_symmetric, scale, accumulate)
-            ok, needed = self.status()
-            if ok:
-                return out
-            self._cap = max(2 * self._cap, int(needed * 1.25) + 1024)
-        raise _lib.EFDError("efd_modesum: could not size the tile-list workspace")
+        self.launch(inp, freq, torch.view_as_real(out), grid_symmetric, scale, accumulate)
+        if check:
+            ok, _ = self.status()
+            if not ok:
+                raise _lib.EFDError(f"efd_modesum: {_lib.last_error(self.lib)}")
+        return out
 
 
 class FDInterpolatedModeSum:

@@ -90,21 +90,21 @@ typedef struct efd_modesum_args {
     void* prof_end;
 } efd_modesum_args;
 
-/* Bytes of workspace efd_modesum needs for (nt, K, nf) with room for `incidences`
- * (tile, harmonic-segment) pairs. */
+/* Bytes of workspace efd_modesum needs for (nt, K, nf). `incidences` is accepted for ABI
+ * stability and ignored (the per-tile record lists are built in LDS by the kernel). */
 size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf, int64_t incidences);
 
 /*
  * Full FD mode sum: spline build -> per-harmonic t(f) inverse splines -> interval records ->
- * per-tile harmonic lists -> SPA evaluation and output-stationary accumulation.
- * Asynchronous. The number of incidences the call needed is written into the workspace; read
- * it with efd_modesum_status after the stream completes. If it exceeded the capacity the
- * output is NOT valid (status returns EFD_ERR_WORKSPACE): grow the workspace and call again.
+ * segment table -> SPA evaluation with output-stationary accumulation (each tile of frequency
+ * bins builds its own record list in LDS). Asynchronous, allocation-free, no host sync, no
+ * atomics on the spectrum; bitwise reproducible.
  */
 int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Synchronises `stream`, then reports the incidences the last efd_modesum on this workspace
- * needed (*needed) and returns EFD_OK or EFD_ERR_WORKSPACE. */
+/* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
+ * this workspace (a harmonic with more than 8 monotonic frequency runs -> EFD_ERR_ARG).
+ * *needed is set to 0 (kept for ABI stability). */
 int efd_modesum_status(const void* workspace, int64_t* needed, void* stream);
 
 /* Contributions C (harmonic branch x bin pairs) evaluated by the last efd_modesum on this

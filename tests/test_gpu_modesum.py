@@ -131,14 +131,18 @@ def test_complex_scale_and_accumulate(multimode):
     assert _relerr(out.cpu().numpy(), 2.0 * _oracle(d, d["freq"], scale=1.0)) < RTOL
 
 
-def test_workspace_regrow(multimode):
-    d = multimode
-    inp = DeviceInputs.from_host(d["t"], d["amp"].T, d["phi_phi"], d["phi_r"], d["f_phi"],
-                                 d["f_r"], d["m"], d["n"], d["ylm_p"], d["ylm_m"])
-    freq = torch.as_tensor(d["freq"], device="cuda")
-    eng = ModeSumEngine(initial_incidences=4)     # forces the overflow path
-    S = eng.run(inp, freq, scale=float(d["prefactor"])).cpu().numpy()
-    assert _relerr(S, _oracle(d, d["freq"])) < RTOL
+def test_coarse_grid_many_records_per_tile():
+    # a coarse symmetric grid puts thousands of interval records in one tile: exercises the
+    # multi-pass (KEYCAP = 2048 keys) path of the in-LDS tile lists
+    d = source_inputs(M=3e5, mu=10.0, e0=0.35, T=0.01, dt=20.0, eps=1e-4)
+    fmax = d["freq"].max()
+    p_freq = np.linspace(0.0, fmax, 400)
+    f_arr = np.hstack((-p_freq[::-1][:-1], p_freq))      # 799 bins -> 400 lanes, one tile
+    nrec = len(d["m"]) * (len(d["t"]) - 1)
+    assert nrec > 2 * 2048
+    S, _ = _gpu(d, f_arr)
+    R = _oracle(d, f_arr)
+    assert _relerr(S, R) < RTOL
 
 
 def test_spline_build_matches_scipy():

@@ -1,0 +1,70 @@
+"""Turn tools/profile_round.sh's raw rocprofv3 output into the committed profiles/ files.
+
+    python tools/summarize_profiles.py r01
+
+writes profiles/<tag>_kernel_stats.csv (the --kernel-trace --stats summary as produced),
+profiles/<tag>_bench.json (the bench line of the same round), profiles/<tag>_pmc.json
+(per-launch counter values of k_modesum) and profiles/pmc_traffic.json, which bench.py reads
+for roofline.traffic. HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (kB units from
+rocprofv3): MI355X_MICROARCH.md, section HBM: on gfx950 FETCH_SIZE reports half of the bytes
+of wide coalesced reads, WRITE_SIZE reads exactly for 16-B stores.
+"""
+
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(path):
+    agg = collections.defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        agg[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
+    disp = sorted({d for d, _ in agg})
+    names = sorted({c for _, c in agg})
+    # the first dispatch belongs to the workspace-allocating run; use the steady-state median
+    out = {}
+    for c in names:
+        vals = sorted(agg[(d, c)] for d in disp[1:] or disp)
+        out[c] = vals[len(vals) // 2]
+    return out, len(disp)
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
+    pmc = {}
+    ndisp = {}
+    for p in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        vals, n = per_dispatch(os.path.join(src, p, "run_counter_collection.csv"))
+        pmc.update(vals)
+        ndisp[p] = n
+    hbm = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
+        if "k_modesum" in r["Name"]:
+            stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    summary = {"tag": tag, "kernel": "k_modesum", "workload": "config2",
+               "caustic": "uniform", "counters_per_launch": pmc, "dispatches": ndisp,
+               "hbm_bytes_per_launch": hbm,
+               "hbm_formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (kB; gfx950 FETCH_SIZE x2)",
+               "rocprof_avg_ms": stats.get("avg_ns", 0.0) / 1e6,
+               "bench_event_ms": bench["roofline"]["kernel_ms"]}
+    json.dump(summary, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+    json.dump({"workload": "config2", "caustic": "uniform", "kernel": "k_modesum",
+               "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc.json"},
+              open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
