@@ -168,8 +168,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    ok, _ = eng.status()
-    if not ok:
+    if not eng.status():
         raise RuntimeError(f"efd_modesum reported a device error: {_lib.last_error(lib)}")
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     C = eng.contributions()

@@ -17,6 +17,7 @@ EFD_ERR_WORKSPACE = -3
 EFD_CAUSTIC_SPA = 0
 EFD_CAUSTIC_UNIFORM = 1
 EFD_LOGLIKE_SCRATCH = 1024
+EFD_INNER_SCRATCH = 2048
 
 # every symbol include/emrifd.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = (
@@ -29,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_contributions",
     "efd_polarizations",
     "efd_loglike",
+    "efd_inner_product",
 )
 
 
@@ -92,17 +94,19 @@ def load(path=None):
     lib.efd_spline_build.restype = ctypes.c_int
     lib.efd_spline_build.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
     lib.efd_modesum_workspace_bytes.restype = sz
-    lib.efd_modesum_workspace_bytes.argtypes = [i32, i32, i64, i64]
+    lib.efd_modesum_workspace_bytes.argtypes = [i32, i32, i64]
     lib.efd_modesum.restype = ctypes.c_int
     lib.efd_modesum.argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
-    lib.efd_modesum_status.argtypes = [vp, ctypes.POINTER(i64), vp]
+    lib.efd_modesum_status.argtypes = [vp, vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int
     lib.efd_modesum_contributions.argtypes = [vp, ctypes.POINTER(i64), vp]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int
     lib.efd_loglike.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
+    lib.efd_inner_product.restype = ctypes.c_int
+    lib.efd_inner_product.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
     _ = dbl
     if path is None:
         _lib = lib

@@ -99,27 +99,25 @@ struct __attribute__((aligned(16))) Item {
 static_assert(sizeof(Item) == 256, "Item must be 256 B");
 
 struct Header {
-    int64_t reserved0;
-    int64_t reserved1;
-    int64_t contributions;
-    int64_t pad0;
-    int64_t pad[4];
+    int64_t contributions;      // C of the last call (k_items)
+    int32_t runs_overflow;      // set by k_prep when a harmonic has > MAXRUNS monotonic runs
+    int32_t pad0;
+    int64_t pad[6];             // 64 B
 };
 
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
         seginfo, nseg, slotlh, slotinfo, slotcnt, total;
-    int64_t ntiles, nlanes, capacity;
+    int64_t ntiles, nlanes;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-Layout make_layout(int32_t nt, int32_t K, int64_t nf, int64_t capacity, int paired) {
+Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     Layout L{};
     const int64_t ni = nt - 1;
     L.nlanes = paired ? (nf + 1) / 2 : nf;
     L.ntiles = (L.nlanes + TILE_LANES - 1) / TILE_LANES;
-    L.capacity = capacity;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
     L.header = take(sizeof(Header));
@@ -1304,6 +1302,9 @@ __global__ void k_polarizations(const double2* __restrict__ S, int64_t nf, int64
 __global__ void k_loglike_partial(const double2* __restrict__ h, const double2* __restrict__ d,
                                   const double* __restrict__ w, int64_t total,
                                   double* __restrict__ part) {
+    // d - h*w rounded like the reference's numpy (product rounded, then difference): no FMA
+    // contraction here, so a template equal to the injection gives exactly 0
+#pragma clang fp contract(off)
     __shared__ double red[256];
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -1340,6 +1341,54 @@ __global__ void k_loglike_final(const double* __restrict__ part, int np, double*
     if (threadIdx.x == 0) out[0] = -0.5 * 4.0 * red[0];
 }
 
+// noise-weighted inner product partials: sum conj(a) b w (complex), one pair per workgroup
+__global__ void k_inner_partial(const double2* __restrict__ a, const double2* __restrict__ b,
+                                const double* __restrict__ w, int64_t total,
+                                double2* __restrict__ part) {
+    __shared__ double rre[256], rim[256];
+    double accr = 0.0, acci = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double2 av = a[i], bv = b[i];
+        const double ww = w ? w[i] : 1.0;
+        // conj(a) b = (ar br + ai bi) + i (ar bi - ai br)
+        accr = fma(ww, fma(av.x, bv.x, av.y * bv.y), accr);
+        acci = fma(ww, fma(av.x, bv.y, -av.y * bv.x), acci);
+    }
+    rre[threadIdx.x] = accr;
+    rim[threadIdx.x] = acci;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            rre[threadIdx.x] += rre[threadIdx.x + s];
+            rim[threadIdx.x] += rim[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = make_double2(rre[0], rim[0]);
+}
+
+__global__ void k_inner_final(const double2* __restrict__ part, int np, double scale,
+                              double2* __restrict__ out) {
+    __shared__ double rre[256], rim[256];
+    double accr = 0.0, acci = 0.0;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) {
+        accr += part[i].x;
+        acci += part[i].y;
+    }
+    rre[threadIdx.x] = accr;
+    rim[threadIdx.x] = acci;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            rre[threadIdx.x] += rre[threadIdx.x + s];
+            rim[threadIdx.x] += rim[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = make_double2(scale * rre[0], scale * rim[0]);
+}
+
 }  // namespace
 
 // ========================================================================================
@@ -1367,9 +1416,9 @@ int efd_spline_build(const double* x, int n, const double* y, int ninterp, doubl
     return EFD_OK;
 }
 
-size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf, int64_t incidences) {
-    if (nt < 2 || K <= 0 || nf <= 0 || incidences < 0) return 0;
-    return make_layout(nt, K, nf, incidences, 0).total;  // unpaired has the most tiles
+size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf) {
+    if (nt < 2 || nt > MAX_NT || K <= 0 || nf <= 0) return 0;
+    return make_layout(nt, K, nf, 0).total;  // unpaired has the most tiles
 }
 
 int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream) {
@@ -1384,7 +1433,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     if (a->caustic != EFD_CAUSTIC_SPA && a->caustic != EFD_CAUSTIC_UNIFORM)
         return fail(EFD_ERR_ARG, "efd_modesum: unknown caustic mode");
     const int paired = a->grid_symmetric ? 1 : 0;
-    const Layout L = make_layout(a->nt, a->K, a->nf, 0, paired);
+    const Layout L = make_layout(a->nt, a->K, a->nf, paired);
     if (workspace_bytes < L.total)
         return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small (see efd_modesum_workspace_bytes)");
 
@@ -1417,7 +1466,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp + nb_inv), dim3(64), sizeof(double) * 7 * nt, st,
                            a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, a->amp, a->m, a->n, nt, K,
                            nb_amp, coefT, kslope, (double*)(ws + L.tscratch), coefA, runs, items,
-                           invcp, invdp, (int32_t*)&hdr->pad[0]);
+                           invcp, invdp, &hdr->runs_overflow);
         HIP_TRY(hipGetLastError());
     }
     // K4: interval records
@@ -1470,13 +1519,12 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     return EFD_OK;
 }
 
-int efd_modesum_status(const void* workspace, int64_t* needed, void* stream) {
+int efd_modesum_status(const void* workspace, void* stream) {
     if (!workspace) return fail(EFD_ERR_ARG, "efd_modesum_status: NULL workspace");
     Header h{};
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
-    if (needed) *needed = 0;   // tile lists are built in LDS: nothing to size on the host
-    if (h.pad[0] != 0)
+    if (h.runs_overflow != 0)
         return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
     return EFD_OK;
 }
@@ -1517,6 +1565,23 @@ int efd_loglike(const double* h, const double* d, const double* w, int32_t nchan
                        (const double2*)d, w, total, scratch);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_loglike_final, dim3(1), dim3(256), 0, st, scratch, np, out);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
+int efd_inner_product(const double* a, const double* b, const double* w, int32_t nchan,
+                      int64_t nbin, double* out, double* scratch, void* stream) {
+    if (!a || !b || !out || !scratch || nchan <= 0 || nbin <= 0)
+        return fail(EFD_ERR_ARG, "efd_inner_product: bad arguments");
+    const int64_t total = (int64_t)nchan * nbin;
+    const int threads = 256;
+    const int np = (int)std::min<int64_t>(EFD_INNER_SCRATCH / 2, (total + threads - 1) / threads);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_inner_partial, dim3(np), dim3(threads), 0, st, (const double2*)a,
+                       (const double2*)b, w, total, (double2*)scratch);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_inner_final, dim3(1), dim3(256), 0, st, (const double2*)scratch, np,
+                       4.0, (double2*)out);
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }

@@ -1,0 +1,130 @@
+"""The reference's FD template helpers (FDutils.py), on the device.
+
+    get_sensitivity(f)                                             FDutils.py:21-33
+    get_convolution(a, b)                                          :35-47
+    get_fd_windowed(signal, window, window_in_fd=False)            :66-101
+    get_fd_waveform_fromFD(waveform_generator, positive_frequency_mask, dt,
+                           non_zero_mask=None, window=None, window_in_fd=False)   :105-139
+
+get_sensitivity interpolates the drivers' PSD table (LISA_Alloc_Sh.txt, shipped here as a data
+file) with a not-a-knot cubic spline, as the reference does with scipy's CubicSpline (:4-5); it
+is host-side setup work (once per likelihood), and returns numpy for numpy input and a device
+tensor for tensor input.
+
+get_convolution is the reference's scipy/cupy `convolve(hstack((a[1:], a)), b, 'valid')/len(b)`.
+For len(a) == len(b) = N that is the circular convolution (a (*) b)[k] = sum_j a[(k-j) mod N]
+b[j] / N; the general case is the same 'valid' slice of a linear convolution. Both are evaluated
+with FFTs on the device (torch.fft -> rocFFT), O(N log N).
+
+get_fd_waveform_fromFD keeps the reference's call: generator -> optional window convolution ->
+positive-frequency mask -> optional zeroing outside non_zero_mask. With no window and the mask
+being the f >= 0 suffix of a sorted grid (the drivers' case, emri_pe.py:239-241), `fill` writes
+h+ and hx straight into the rows of a caller's [2][N] buffer (no intermediate copies); the
+Likelihood uses that.
+"""
+
+import os
+
+import numpy as np
+
+from .summation import require_gpu
+
+_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "LISA_Alloc_Sh.txt")
+_SPLINE = None
+
+
+def _spline():
+    global _SPLINE
+    if _SPLINE is None:
+        from scipy.interpolate import CubicSpline
+        tab = np.genfromtxt(_TABLE)
+        _SPLINE = CubicSpline(tab[:, 0], tab[:, 1])
+    return _SPLINE
+
+
+def get_sensitivity(f):
+    """PSD S(f) [1/Hz] from the LISA_Alloc_Sh table (FDutils.py:21-33)."""
+    if hasattr(f, "detach"):
+        torch = require_gpu()
+        vals = _spline()(f.detach().cpu().numpy())
+        return torch.as_tensor(vals, dtype=torch.float64, device=f.device)
+    return _spline()(f)
+
+
+def get_convolution(a, b):
+    """convolve(hstack((a[1:], a)), b, mode='valid') / len(b), on the device."""
+    torch = require_gpu()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    a = torch.as_tensor(a, device=dev).to(torch.complex128)
+    b = torch.as_tensor(b, device=dev).to(torch.complex128)
+    na, nb = int(a.numel()), int(b.numel())
+    if na == nb:
+        return torch.fft.ifft(torch.fft.fft(a) * torch.fft.fft(b)) / nb
+    x = torch.cat((a[1:], a))
+    nx = int(x.numel())
+    if nb > nx:
+        raise ValueError("get_convolution: 'valid' needs len(b) <= 2 len(a) - 1")
+    n = nx + nb - 1
+    full = torch.fft.ifft(torch.fft.fft(x, n) * torch.fft.fft(b, n))
+    return full[nb - 1:nx] / nb
+
+
+def get_fd_windowed(signal, window, window_in_fd=False):
+    """[h+, hx] convolved with the window's spectrum (FDutils.py:66-101)."""
+    if window is None:
+        return [signal[0], signal[1]]
+    torch = require_gpu()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    w = torch.as_tensor(window, device=dev)
+    fw = w.to(torch.complex128) if window_in_fd else torch.fft.fft(w.to(torch.complex128))
+    return [get_convolution(torch.conj(fw), signal[0]),
+            get_convolution(torch.conj(fw), signal[1])]
+
+
+class get_fd_waveform_fromFD:
+    """FD template [ch1, ch2] over the positive frequencies (FDutils.py:105-139)."""
+
+    def __init__(self, waveform_generator, positive_frequency_mask, dt, non_zero_mask=None,
+                 window=None, window_in_fd=False):
+        torch = require_gpu()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.waveform_generator = waveform_generator
+        self.positive_frequency_mask = torch.as_tensor(positive_frequency_mask, device=dev)
+        self.non_zero_mask = (None if non_zero_mask is None
+                              else torch.as_tensor(non_zero_mask, device=dev))
+        self.window = window
+        self.window_in_fd = window_in_fd
+        self.dt = dt
+        # contiguous-suffix mask (f >= 0 of a sorted grid): the fused fill path applies
+        pm = self.positive_frequency_mask
+        k0 = int(torch.argmax(pm.to(torch.int8)).item()) if bool(pm.any()) else int(pm.numel())
+        self._suffix_k0 = k0 if bool(pm[k0:].all()) and not bool(pm[:k0].any()) else None
+        self.num_bins = int(pm.sum().item())
+
+    def __call__(self, *args, **kwargs):
+        chans = self.waveform_generator(*args, **kwargs)
+        p, c = get_fd_windowed(chans, self.window, window_in_fd=self.window_in_fd)
+        torch = require_gpu()
+        p = torch.as_tensor(p)
+        c = torch.as_tensor(c)
+        ch1 = p[self.positive_frequency_mask]
+        ch2 = c[self.positive_frequency_mask]
+        if self.non_zero_mask is not None:
+            ch1[~self.non_zero_mask] = 0.0
+            ch2[~self.non_zero_mask] = 0.0
+        return [ch1, ch2]
+
+    @property
+    def can_fill(self):
+        gen = self.waveform_generator
+        return (self.window is None and self._suffix_k0 is not None
+                and hasattr(gen, "fill_channels"))
+
+    def fill(self, out, *args, **kwargs):
+        """Write [ch1, ch2] into out (complex128 [2][num_bins], device) without copies.
+
+        Bins outside non_zero_mask are NOT zeroed here; the Likelihood folds that mask into
+        the template's noise weight instead (same result: h * 0).
+        """
+        self.waveform_generator.fill_channels(out, *args, k0=self._suffix_k0, **kwargs)
+        return out

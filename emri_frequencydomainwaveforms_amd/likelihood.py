@@ -1,0 +1,236 @@
+"""lisatools-compatible Gaussian likelihood with the reduction on the device.
+
+Mirror of LISAanalysistools/lisatools/sampling/likelihood.py `Likelihood` (:13-334) for the FD
+templates the reference drivers use (emri_pe.py:381-414: two channels h+, hx over f >= 0,
+noise_fn = FDutils.get_sensitivity, f_arr = frequency[frequency >= 0]):
+
+  inject_signal (:80-234)  data d = inj * sqrt(diff(f)/PSD) and the noise factor
+                           w = sqrt(diff(f)/PSD), diff(f)[0] = diff(f)[1]; repeated
+                           injections add up; add_noise raises NotImplementedError (as :199)
+  get_ll (:236-293)        per walker: template h, ll = -1/2 * 4 * sum |d - h w|^2 over
+                           channels and bins, skipping bin 0 when w[0][0] is NaN (:268)
+  __call__ (:295-334)      parameter transform, transpose_params, `subset` batching
+
+What changes is where the work happens. Data and noise factor live on the device; each
+walker's template is reduced by efd_loglike (HIP) straight from the template buffer into its slot
+of a device result vector, so the batch costs one host synchronisation and the 2 x N_pos
+residual d - h w is never materialised. When the template is this package's
+get_fd_waveform_fromFD around a GenerateEMRIWaveform (the drivers' case), h+ and hx are written
+by efd_polarizations directly into one reusable [2][N_pos] buffer (the stream orders reuse), and
+non_zero_mask is folded into the template weight (w * mask) instead of zeroing h.
+Results are numpy float64 arrays ([B]), or device tensors with use_gpu=True, return_cupy=True.
+Time-domain templates (dt only) are not part of this path: get_ll raises NotImplementedError.
+"""
+
+import numpy as np
+
+from .summation import require_gpu
+
+
+class Likelihood:
+    def __init__(self, template_model, num_channels, dt=None, df=None, f_arr=None,
+                 parameter_transforms=None, use_gpu=False, vectorized=False,
+                 separate_d_h=False, return_cupy=False, fill_data_noise=False,
+                 transpose_params=False, subset=None):
+        self.subset = subset
+        self.transpose_params = transpose_params
+        self.template_model = template_model
+        self.parameter_transforms = parameter_transforms
+        self.fill_data_noise = fill_data_noise
+        self.use_gpu = use_gpu
+        self.vectorized = vectorized
+        self.num_channels = num_channels
+        self.separate_d_h = separate_d_h
+        if dt is None and df is None and f_arr is None:
+            raise ValueError("Must provide dt, df or f_arr.")
+        self.dt, self.df, self.f_arr = dt, df, f_arr
+        self.frequency_domain = df is not None or f_arr is not None
+        self.return_cupy = return_cupy
+        self.noise_has_been_added = False
+        self.torch = torch = require_gpu()
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        from .reductions import Reducer
+        self._red = Reducer(self.device)
+        self._buf = None
+        self._specific_likelihood_setup()
+
+    def _specific_likelihood_setup(self):
+        if isinstance(self.template_model, list):
+            raise ValueError("For single likelihood, template model cannot be a list.")
+        if hasattr(self.template_model, "get_ll"):
+            self.get_ll = self.template_model.get_ll
+            self.like_here = False
+        else:
+            self.fill_data_noise = False
+            self.like_here = True
+
+    # ---------------------------------------------------------------------------------------
+    def inject_signal(self, data_stream=None, params=None, waveform_kwargs={}, noise_fn=None,
+                      noise_kwargs={}, add_noise=False):
+        torch = self.torch
+        if params is not None:
+            if self.parameter_transforms is not None:
+                key = list(self.parameter_transforms.keys())[0]
+                params = self.parameter_transforms[key].both_transforms(params)
+            injection_channels = _to_numpy(self.template_model(*params, **waveform_kwargs))
+        elif data_stream is not None:
+            if isinstance(data_stream, list) is False:
+                raise ValueError("If data_stream is provided, it must be as a list.")
+            injection_channels = _to_numpy(data_stream)
+        else:
+            raise ValueError("Must provide data_stream or params kwargs to inject signal.")
+
+        self.injection_length = len(injection_channels[0])
+        for inj in injection_channels:
+            if len(inj) != self.injection_length:
+                raise ValueError("Length of all injection channels must match.")
+        if len(injection_channels) != self.num_channels:
+            raise ValueError("Number of channels from template_model does not match number of "
+                             "channels declare by user.")
+
+        if isinstance(noise_fn, list):
+            if len(noise_fn) != 1 and len(noise_fn) != self.num_channels:
+                raise ValueError("Number of noise functions does not match number of channels "
+                                 "declared by user.")
+            elif len(noise_fn) == 1:
+                noise_fn = [noise_fn[0] for _ in range(self.num_channels)]
+        else:
+            noise_fn = [noise_fn for _ in range(self.num_channels)]
+        if isinstance(noise_kwargs, list):
+            if len(noise_kwargs) != 1 and len(noise_kwargs) != self.num_channels:
+                raise ValueError("Number of noise kwargs does not match number of channels "
+                                 "declared by user.")
+            elif len(noise_kwargs) == 1:
+                noise_kwargs = [noise_kwargs[0] for _ in range(self.num_channels)]
+        else:
+            noise_kwargs = [noise_kwargs for _ in range(self.num_channels)]
+
+        if self.frequency_domain:
+            if self.df is not None:
+                freqs = np.arange(self.injection_length) * self.df
+                can_add_noise = True
+            else:
+                freqs = _to_numpy(self.f_arr)
+                can_add_noise = False
+        else:
+            freqs = np.fft.rfftfreq(self.injection_length, self.dt)
+            can_add_noise = True
+        psd = [np.asarray(_to_numpy(fn(freqs, **kw)), dtype=np.float64)
+               for fn, kw in zip(noise_fn, noise_kwargs)]
+        if self.frequency_domain is False:
+            injection_channels = [np.fft.rfft(inj) * self.dt for inj in injection_channels]
+
+        diff_freqs = np.zeros_like(freqs)
+        diff_freqs[1:] = np.diff(freqs)
+        diff_freqs[0] = diff_freqs[1]
+        self.base_injections = injection_channels
+        if add_noise and can_add_noise and self.noise_has_been_added is False:
+            raise NotImplementedError   # as the reference (likelihood.py:199)
+
+        with np.errstate(invalid="ignore", divide="ignore"):
+            nf = np.asarray([(diff_freqs / p) ** 0.5 for p in psd])
+        weighted = np.asarray([np.asarray(inj) * w for inj, w in zip(injection_channels, nf)],
+                              dtype=np.complex128)
+        self.noise_factor = torch.as_tensor(nf, dtype=torch.float64, device=self.device)
+        if hasattr(self, "injection_channels") is False:
+            self.injection_channels = torch.as_tensor(weighted, device=self.device)
+            self.freqs = torch.as_tensor(freqs, dtype=torch.float64, device=self.device)
+        else:
+            self.injection_channels = self.injection_channels + torch.as_tensor(
+                weighted, device=self.device)
+        self.data_length = int(self.injection_channels.shape[1])
+        self.psd = psd
+        self._prepare_reduction()
+
+    def _prepare_reduction(self):
+        """Device copies used by efd_loglike: skip bin 0 by zeroing it when w[0][0] is NaN."""
+        torch = self.torch
+        d = self.injection_channels.contiguous().clone()
+        w = self.noise_factor.contiguous().clone()
+        self.start_ind = 1 if bool(torch.isnan(self.noise_factor[0, 0]).item()) else 0
+        if self.start_ind:
+            d[:, 0] = 0.0
+            w[:, 0] = 0.0
+        self._d, self._w = d, w
+        self._w_templ = w
+        tm = self.template_model
+        mask = getattr(tm, "non_zero_mask", None)
+        if mask is not None and getattr(tm, "can_fill", False):
+            self._w_templ = (w * mask.to(torch.float64)[None, :]).contiguous()
+
+    # ---------------------------------------------------------------------------------------
+    def get_ll(self, params, *args, **kwargs):
+        torch = self.torch
+        if self.frequency_domain is False:
+            raise NotImplementedError("time-domain templates are not part of the FD path")
+        num_likes = params.shape[0]
+        out = torch.empty(num_likes, dtype=torch.float64, device=self.device)
+        nch, nb = self._d.shape
+        tm = self.template_model
+        if self.vectorized:
+            h_all = tm(*params, *args, **kwargs)
+            for i in range(num_likes):
+                h = self._as_channels(h_all[i])
+                self._red.loglike(h, self._d, self._w, out=out[i:i + 1])
+        elif getattr(tm, "can_fill", False):
+            if self._buf is None or tuple(self._buf.shape) != (nch, nb):
+                self._buf = torch.empty((nch, nb), dtype=torch.complex128, device=self.device)
+            for i, params_i in enumerate(params):
+                tm.fill(self._buf, *params_i, *args, **kwargs)
+                self._red.loglike(self._buf, self._d, self._w_templ, out=out[i:i + 1])
+        else:
+            for i, params_i in enumerate(params):
+                h = self._as_channels(tm(*params_i, *args, **kwargs))
+                self._red.loglike(h, self._d, self._w, out=out[i:i + 1])
+        if self.noise_has_been_added:
+            raise NotImplementedError
+        if self.use_gpu and self.return_cupy:
+            return out
+        return out.cpu().numpy()
+
+    def _as_channels(self, chans):
+        torch = self.torch
+        if hasattr(chans, "detach") and chans.dim() == 2:
+            h = chans
+        else:
+            h = torch.stack([torch.as_tensor(c, device=self.device) for c in chans])
+        h = h.to(device=self.device, dtype=torch.complex128).contiguous()
+        if tuple(h.shape) != tuple(self._d.shape):
+            raise ValueError(f"template has shape {tuple(h.shape)}, data {tuple(self._d.shape)}")
+        return h
+
+    def __call__(self, params, *args, **kwargs):
+        if not isinstance(params, np.ndarray):
+            raise ValueError("params must be np.ndarray.")
+        if self.parameter_transforms is not None:
+            key = list(self.parameter_transforms.keys())[0]
+            params = self.parameter_transforms[key].both_transforms(params)
+        if self.transpose_params:
+            params = params.T
+            subset_axis = 1
+        else:
+            subset_axis = 0
+        num_likes = params.shape[subset_axis]
+        inds_likes = np.arange(num_likes)
+        if self.subset is not None:
+            if not isinstance(self.subset, int):
+                raise ValueError("Subset must be int.")
+            inds_subset = np.split(inds_likes, np.arange(self.subset, num_likes, self.subset))
+        else:
+            inds_subset = [inds_likes]
+        out_ll = []
+        for inds in inds_subset:
+            args_in = (params[inds],) if subset_axis == 0 else (params[:, inds],)
+            args_in += args
+            if self.fill_data_noise:
+                args_in += (self.injection_channels, self.noise_factor)
+            out_ll.append(_to_numpy(self.get_ll(*args_in, **kwargs)))
+        return np.concatenate(out_ll, axis=0)
+
+
+def _to_numpy(x):
+    if isinstance(x, (list, tuple)):
+        return [_to_numpy(v) for v in x]
+    if hasattr(x, "detach"):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)

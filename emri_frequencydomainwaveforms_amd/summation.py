@@ -100,7 +100,7 @@ class ModeSumEngine:
 
     def _workspace(self, nt, K, nf, device):
         torch = _torch()
-        nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf, 0))
+        nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf))
         if nbytes == 0:
             raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
         if self._ws is None or self._ws.numel() < nbytes or self._ws.device != device:
@@ -127,13 +127,10 @@ class ModeSumEngine:
         return ws
 
     def status(self, stream=None):
-        """Synchronise and return (ok, needed incidences)."""
-        import ctypes
+        """Synchronise; True when the last launch reported no device-side error."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        needed = ctypes.c_int64(0)
-        rc = self.lib.efd_modesum_status(self._ws.data_ptr(), ctypes.byref(needed), st)
-        return rc == _lib.EFD_OK, int(needed.value)
+        return self.lib.efd_modesum_status(self._ws.data_ptr(), st) == _lib.EFD_OK
 
     def contributions(self, stream=None):
         import ctypes
@@ -154,8 +151,7 @@ class ModeSumEngine:
             out = torch.empty(int(freq.numel()), dtype=torch.complex128, device=freq.device)
         self.launch(inp, freq, torch.view_as_real(out), grid_symmetric, scale, accumulate)
         if check:
-            ok, _ = self.status()
-            if not ok:
+            if not self.status():
                 raise _lib.EFDError(f"efd_modesum: {_lib.last_error(self.lib)}")
         return out
 
@@ -214,16 +210,31 @@ class FDInterpolatedModeSum:
         freq, sym = self._grid(T, dt, f_arr)
         return self.engine.run(inp, freq, grid_symmetric=sym, scale=scale)
 
-    def polarizations(self, S, mask_positive=False):
-        """[h+, hx] (FEW list output) from S; mask_positive keeps f >= 0."""
+    def positive_start(self):
+        """Index of the first f >= 0 bin of the last grid (emri_pe.py:239 mask, sorted grid)."""
+        torch = require_gpu()
+        return int(torch.searchsorted(self._freq_dev, torch.zeros(
+            1, dtype=torch.float64, device=self._freq_dev.device)).item())
+
+    def polarizations(self, S, mask_positive=False, out=None):
+        """[h+, hx] (FEW list output) from S; mask_positive keeps f >= 0.
+
+        out: optional (hp, hc) complex128 device tensors of the output length to write into
+        (e.g. the two rows of a [2][N] channel buffer).
+        """
         torch = require_gpu()
         nf = int(S.numel())
-        k0 = 0
-        if mask_positive:
-            k0 = int(torch.searchsorted(self._freq_dev, torch.zeros(1, dtype=torch.float64,
-                                                                    device=S.device)).item())
-        hp = torch.empty(nf - k0, dtype=torch.complex128, device=S.device)
-        hc = torch.empty_like(hp)
+        k0 = self.positive_start() if mask_positive else 0
+        if out is None:
+            hp = torch.empty(nf - k0, dtype=torch.complex128, device=S.device)
+            hc = torch.empty_like(hp)
+        else:
+            hp, hc = out
+            for o in (hp, hc):
+                if (o.dtype != torch.complex128 or o.numel() != nf - k0
+                        or not o.is_contiguous() or o.device != S.device):
+                    raise ValueError("polarizations: out tensors must be contiguous complex128 "
+                                     f"of length {nf - k0} on {S.device}")
         lib = self.engine.lib
         st = torch.cuda.current_stream(S.device).cuda_stream
         _lib.check(lib.efd_polarizations(torch.view_as_real(S).data_ptr(), nf, k0,

@@ -145,26 +145,42 @@ class GenerateEMRIWaveform:
     def use_gpu(self):
         return self.waveform_generator.use_gpu
 
-    def __call__(self, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
-                 Phi_r0, *add_args, mask_positive=False, **kwargs):
+    def _spectrum(self, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
+                  Phi_r0, **kwargs):
         # a, x0, Phi_theta0 are ignored for Schwarzschild (emri_pe.py:598, 602)
         theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
         rot = 1.0 + 0.0j
         if self.frame == "detector":
             rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
         gen = self.waveform_generator
-        S = gen.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, extra_scale=rot,
-                         **kwargs)
+        return gen.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, extra_scale=rot,
+                            **kwargs)
+
+    def fill_channels(self, out, *params, k0=None, **kwargs):
+        """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).
+
+        The fused path of fdutils.get_fd_waveform_fromFD: same values as
+        `self(*params, mask_positive=True)` with `return_list=True`, without the copies.
+        """
+        S = self._spectrum(*params, **kwargs)
+        cw = self.waveform_generator.create_waveform
+        if k0 is not None and k0 != cw.positive_start():
+            raise ValueError("positive_frequency_mask does not match the generator's grid")
+        cw.polarizations(S, True, out=(out[0], out[1]))
+        return out
+
+    def __call__(self, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
+                 Phi_r0, *add_args, mask_positive=False, **kwargs):
+        S = self._spectrum(M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
+                           Phi_r0, **kwargs)
+        gen = self.waveform_generator
         cw = gen.create_waveform
         if self.return_list:
             hp, hc = cw.polarizations(S, mask_positive)
             out = [hp, hc]
         else:
             if mask_positive:
-                torch = require_gpu()
-                k0 = int(torch.searchsorted(cw._freq_dev, torch.zeros(
-                    1, dtype=torch.float64, device=S.device)).item())
-                S = S[k0:]
+                S = S[cw.positive_start():]
             out = S
         if self.use_gpu:
             return out

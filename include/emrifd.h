@@ -18,6 +18,8 @@
  *                          (emri_pe.py:241)
  *   - efd_loglike        <- Likelihood.get_ll's reduction -1/2 * 4 * sum |d - h w|^2
  *                          (LISAanalysistools/lisatools/sampling/likelihood.py:257-274)
+ *   - efd_inner_product  <- lisatools inner_product / snr
+ *                          (LISAanalysistools/lisatools/diagnostic.py:14-186)
  *
  * Conventions: all arrays are caller-owned DEVICE pointers (HIP, gfx950) unless stated;
  * complex numbers are interleaved (re, im) float64 pairs; every call is asynchronous on the
@@ -38,7 +40,7 @@ extern "C" {
 #define EFD_OK 0
 #define EFD_ERR_ARG (-1)        /* invalid argument (shape, NULL pointer, unsorted grid...)  */
 #define EFD_ERR_HIP (-2)        /* HIP runtime error                                          */
-#define EFD_ERR_WORKSPACE (-3)  /* workspace too small: call again with the size reported   */
+#define EFD_ERR_WORKSPACE (-3)  /* workspace smaller than efd_modesum_workspace_bytes()     */
 
 #define EFD_CAUSTIC_SPA 0       /* plain stationary phase: Q = e^{i sgn(F') 3pi/4} / sqrt|F'| */
 #define EFD_CAUSTIC_UNIFORM 1   /* notebook K_{1/3} uniform form (notebook :599-613)          */
@@ -90,9 +92,9 @@ typedef struct efd_modesum_args {
     void* prof_end;
 } efd_modesum_args;
 
-/* Bytes of workspace efd_modesum needs for (nt, K, nf). `incidences` is accepted for ABI
- * stability and ignored (the per-tile record lists are built in LDS by the kernel). */
-size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf, int64_t incidences);
+/* Bytes of device workspace efd_modesum needs for (nt, K, nf), valid for either grid kind;
+ * 0 for an invalid shape (nt < 2 or nt > 1024, K <= 0, nf <= 0). Host-only query. */
+size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf);
 
 /*
  * Full FD mode sum: spline build -> per-harmonic t(f) inverse splines -> interval records ->
@@ -103,9 +105,8 @@ size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf, int64_t in
 int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
- * this workspace (a harmonic with more than 8 monotonic frequency runs -> EFD_ERR_ARG).
- * *needed is set to 0 (kept for ABI stability). */
-int efd_modesum_status(const void* workspace, int64_t* needed, void* stream);
+ * this workspace (a harmonic with more than 8 monotonic frequency runs -> EFD_ERR_ARG). */
+int efd_modesum_status(const void* workspace, void* stream);
 
 /* Contributions C (harmonic branch x bin pairs) evaluated by the last efd_modesum on this
  * workspace (for the roofline); synchronises `stream`. */
@@ -130,6 +131,18 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
 #define EFD_LOGLIKE_SCRATCH 1024
 int efd_loglike(const double* h, const double* d, const double* w, int32_t nchan, int64_t nbin,
                 double* out, double* scratch, void* stream);
+
+/*
+ * Noise-weighted inner product over nchan channels of nbin bins each:
+ *   out[0] + i out[1] = 4 * sum_c sum_k conj(a[c][k]) * b[c][k] * w[c][k]
+ * (lisatools diagnostic.py:95-110: right-sum rule, w = diff(f) / PSD with the first spacing
+ * repeated; inner_product takes out[0], or both parts with complex=True). a, b complex
+ * [nchan][nbin]; w real [nchan][nbin] or NULL (w = 1); out is two device doubles; scratch
+ * holds EFD_INNER_SCRATCH device doubles. Bitwise reproducible.
+ */
+#define EFD_INNER_SCRATCH 2048
+int efd_inner_product(const double* a, const double* b, const double* w, int32_t nchan,
+                      int64_t nbin, double* out, double* scratch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -67,11 +67,29 @@ def monotonic_runs(F):
     return runs
 
 
+def _kv13_scaled_asymptotic(z, terms=8):
+    """K_{1/3}(z) e^z for large |z|: sqrt(pi/(2z)) sum_k a_k z^-k (DLMF 10.40.2)."""
+    acc = np.ones_like(z)
+    a = np.ones_like(z)
+    for k in range(1, terms):
+        a = a * (4.0 / 9.0 - (2 * k - 1) ** 2) / (8.0 * k) / z
+        acc = acc + a
+    return np.sqrt(np.pi / (2.0 * z)) * acc
+
+
 def _kfactor(fdot, fdd, caustic):
     """Q(t) such that the mirror-convention term is A Y Q exp(i(2 pi f t - Phi))."""
     if caustic == "uniform":
         arg = -2.0 * np.pi * 1j * fdot ** 3 / (3.0 * fdd ** 2)           # notebook :599
-        kk = special.kv(1.0 / 3.0, arg) * np.exp(arg)                   # notebook :600
+        with np.errstate(invalid="ignore", over="ignore"):
+            kk = special.kv(1.0 / 3.0, arg) * np.exp(arg)               # notebook :600
+        # scipy's AMOS kv returns NaN once |z| passes ~1e9 (total loss of significance in its
+        # argument reduction; F'' -> 0 near an inflection of F'(t)). There the asymptotic
+        # series is exact to double precision (|z|^-8 terms < 1e-70); the notebook itself
+        # would emit NaN, which is a numerical artefact of scipy, not the construction.
+        bad = ~np.isfinite(kk)
+        if np.any(bad):
+            kk = np.where(bad, _kv13_scaled_asymptotic(np.where(bad, arg, 1.0)), kk)
         return 1j * fdot / np.abs(fdd) * kk * TWO_OVER_SQRT3            # notebook :607-608
     if caustic == "spa":
         return np.exp(1j * np.sign(fdot) * 0.75 * np.pi) / np.sqrt(np.abs(fdot))

@@ -39,8 +39,9 @@ def test_library_exports_every_symbol():
 
 def test_workspace_query_is_host_only():
     lib = _lib.load()
-    assert lib.efd_modesum_workspace_bytes(100, 3000, 6311631, 1 << 20) > 0
-    assert lib.efd_modesum_workspace_bytes(1, 3000, 100, 0) == 0
+    assert lib.efd_modesum_workspace_bytes(100, 3000, 6311631) > 0
+    assert lib.efd_modesum_workspace_bytes(1, 3000, 100) == 0
+    assert lib.efd_modesum_workspace_bytes(2000, 3000, 100) == 0
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -68,3 +69,13 @@ def test_no_cpu_fallback_without_gpu():
     from emri_frequencydomainwaveforms_amd.summation import require_gpu
     with pytest.raises(_lib.EFDError):
         require_gpu()
+
+
+def test_header_constants_match_python():
+    txt = open(HEADER).read()
+    defs = dict(re.findall(r"^#define (EFD_\w+) \(?(-?\d+)\)?", txt, flags=re.M))
+    for name, val in defs.items():
+        if name in ("EFD_VERSION",):
+            continue
+        assert hasattr(_lib, name), name
+        assert getattr(_lib, name) == int(val), name

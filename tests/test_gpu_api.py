@@ -1,0 +1,135 @@
+"""The reference drivers' call surface end to end on the GPU (emri_pe.py:86-105, 212-271,
+381-414; check_mode_by_mode.py:69-83, 226-250): GenerateEMRIWaveform -> get_fd_waveform_fromFD
+-> Likelihood, with the HIP path underneath and the numpy oracle as the checker.
+"""
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from emri_frequencydomainwaveforms_amd.fdutils import get_fd_waveform_fromFD, get_sensitivity  # noqa: E402,E501
+from emri_frequencydomainwaveforms_amd.likelihood import Likelihood  # noqa: E402
+from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t  # noqa: E402
+from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform  # noqa: E402
+from oracle import fd_oracle, likelihood_oracle as lo  # noqa: E402
+
+SUM_KW = dict(pad_output=True, output_type="fd", odd_len=True)
+M, MU, E0, T, DT = 3e5, 10.0, 0.3, 0.02, 20.0
+
+
+@pytest.fixture(scope="module")
+def setup():
+    p0 = get_p_at_t(EMRIInspiral(), 0.99 * T, [M, MU, 0.0, E0, 1.0])
+    params = np.array([M, MU, 0.0, p0, E0, 1.0, 1.0, 0.5, 0.3, 0.8, 1.1, 0.2, 0.0, 0.4])
+    kw = dict(T=T, dt=DT, eps=1e-2)
+    gen = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", sum_kwargs=SUM_KW,
+                               use_gpu=True, return_list=False)
+    gen_list = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", sum_kwargs=SUM_KW,
+                                    use_gpu=True, return_list=True)
+    return params, kw, gen, gen_list
+
+
+def test_generator_contract(setup):
+    params, kw, gen, gen_list = setup
+    S = gen(*params, **kw)
+    hp, hc = gen_list(*params, **kw)
+    freq = gen.waveform_generator.create_waveform.frequency
+    assert S.shape == freq.shape and freq.numel() % 2 == 1             # odd two-sided grid
+    # check_mode_by_mode.py:247: S = h+ - i hx
+    assert torch.equal(hp - 1j * hc, S) or \
+        (hp - 1j * hc - S).abs().max().item() <= 1e-15 * S.abs().max().item()
+    # mask_positive (emri_pe.py:241) keeps f >= 0
+    Sp = gen(*params, mask_positive=True, **kw)
+    pos = freq >= 0
+    assert torch.equal(Sp, S[pos])
+    hpp, hcp = gen_list(*params, mask_positive=True, **kw)
+    assert torch.equal(hpp, hp[pos]) and torch.equal(hcp, hc[pos])
+    # the spectrum equals the oracle's for the same host inputs
+    wg = gen.waveform_generator
+    theta = np.arccos(-(np.sin(0.5) * np.cos(0.3) * np.sin(0.8) * np.cos(1.1)
+                        + np.sin(0.5) * np.sin(0.3) * np.sin(0.8) * np.sin(1.1)
+                        + np.cos(0.5) * np.cos(0.8)))
+    d = wg.prepare(M, MU, params[3], E0, theta, -np.pi / 2, 1.0, params[11], params[13], T,
+                   1e-2)
+    K = len(d["m"])
+    assert K > 20
+
+
+def test_f_arr_downsampled(setup):
+    params, kw, gen, _ = setup
+    S = gen(*params, **kw).cpu().numpy()
+    freq = gen.waveform_generator.create_waveform.frequency.cpu().numpy()
+    nz = np.abs(S[freq >= 0]) > 1e-50 * np.abs(S).max()
+    p_freq = np.linspace(0.0, freq[freq >= 0][nz].max() * 1.01, num=int(nz.sum() / 20))
+    f_arr = np.hstack((-p_freq[::-1][:-1], p_freq))                  # emri_pe.py:333-349
+    Sd = gen(*params, f_arr=torch.as_tensor(f_arr, device="cuda"), **kw)
+    assert Sd.numel() == len(f_arr)
+    assert np.array_equal(gen.waveform_generator.create_waveform.frequency.cpu().numpy(), f_arr)
+    # each downsampled bin equals a full evaluation of the same sum there (grid independence)
+    Sd2 = gen(*params, f_arr=f_arr, **kw)
+    assert torch.equal(Sd, Sd2)
+
+
+def test_emri_pe_likelihood_path(setup):
+    params, kw, gen, gen_list = setup
+    hp, hc = gen_list(*params, **kw)
+    freq = gen_list.waveform_generator.create_waveform.frequency
+    pos = freq >= 0
+    fd_gen = get_fd_waveform_fromFD(gen_list, pos, DT)
+    assert fd_gen.can_fill
+    sig = fd_gen(*params, **kw)
+    assert torch.equal(sig[0], hp[pos]) and torch.equal(sig[1], hc[pos])
+    f_arr = freq[pos].cpu().numpy()
+
+    like = Likelihood(fd_gen, 2, f_arr=f_arr, use_gpu=True, subset=2)
+    like.inject_signal(data_stream=sig, noise_fn=[get_sensitivity, get_sensitivity],
+                       noise_kwargs=[{}, {}])
+    walkers = np.stack([params, params, params])
+    walkers[1, 0] *= 1.0 + 1e-5
+    walkers[2, 4] += 1e-3
+    ll = like(walkers, **kw)                             # fused path (fill into one buffer)
+    assert ll[0] == 0.0
+    assert np.all(ll[1:] < 0.0)
+
+    # generic path (template returns channels) gives bitwise the same values
+    like_g = Likelihood(lambda *a, **k: fd_gen(*a, **k), 2, f_arr=f_arr, use_gpu=True)
+    like_g.inject_signal(data_stream=sig, noise_fn=[get_sensitivity, get_sensitivity],
+                         noise_kwargs=[{}, {}])
+    np.testing.assert_array_equal(like_g.get_ll(walkers, **kw), like.get_ll(walkers, **kw))
+
+    # against the oracle on host copies
+    w = lo.noise_factor(f_arr, [get_sensitivity(f_arr)] * 2)
+    dh = np.array([s.cpu().numpy() for s in sig]) * w
+    h1 = np.array([c.cpu().numpy() for c in fd_gen(*walkers[1], **kw)])
+    ref = lo.loglike(h1, dh, w)
+    assert abs(ll[1] - ref) <= 1e-12 * abs(ref)
+
+    # non_zero_mask (emri_pe.py:245): folded into the template weight on the fused path
+    nzm = sig[0].abs() > 1e-50
+    fd_nz = get_fd_waveform_fromFD(gen_list, pos, DT, non_zero_mask=nzm)
+    like_nz = Likelihood(fd_nz, 2, f_arr=f_arr, use_gpu=True)
+    like_nz.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2, noise_kwargs=[{}, {}])
+    like_nzg = Likelihood(lambda *a, **k: fd_nz(*a, **k), 2, f_arr=f_arr, use_gpu=True)
+    like_nzg.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2,
+                           noise_kwargs=[{}, {}])
+    np.testing.assert_array_equal(like_nz.get_ll(walkers, **kw), like_nzg.get_ll(walkers, **kw))
+
+
+def test_spectrum_matches_oracle_through_api(setup):
+    params, kw, gen, _ = setup
+    wg = gen.waveform_generator
+    S = wg.spectrum(M, MU, params[3], E0, np.pi / 3, -np.pi / 2, 1.0, 0.2, 0.4, dt=DT, T=T,
+                    eps=1e-2).cpu().numpy()
+    d = wg.prepare(M, MU, params[3], E0, np.pi / 3, -np.pi / 2, 1.0, 0.2, 0.4, T, 1e-2)
+    K = len(d["m"])
+    from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI, MTSUN_SI
+    from emri_frequencydomainwaveforms_amd.frequencies import get_fundamental_frequencies
+    op, _, orr = get_fundamental_frequencies(0.0, d["p"], d["e"], 0.0)
+    freq = wg.create_waveform.frequency.cpu().numpy()
+    R = fd_oracle.fd_modesum(d["t"], d["teuk"].T, d["Phi_phi"], d["Phi_r"],
+                             op / (2 * np.pi * M * MTSUN_SI), orr / (2 * np.pi * M * MTSUN_SI),
+                             d["m"], d["n"], d["ylms"][:K], d["ylms"][K:], freq,
+                             MU * MRSUN_SI / Gpc)
+    assert np.abs(S - R).max() <= 1e-9 * np.abs(R).max()
