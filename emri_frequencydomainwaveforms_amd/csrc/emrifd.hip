@@ -769,18 +769,23 @@ __global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict_
 // SPA arithmetic
 // ----------------------------------------------------------------------------------------
 
-// sin/cos of a phase up to |x| ~ 1e9 rad: two-term FMA Cody-Waite reduction by pi/2 and
-// fdlibm's kernel polynomials on [-pi/4, pi/4].
+// sin/cos of a phase up to |x| ~ 1e9 rad: two-term FMA Cody-Waite reduction by pi/2 (the
+// third term, q * 1.5e-33, is below half an ulp of r for |q| < 2^31) and fdlibm's kernel
+// polynomials on [-pi/4, pi/4]. The quadrant is applied with a select (odd q swaps sin/cos)
+// and sign-bit flips, all branch-free.
+__device__ __forceinline__ double flip_sign_if(double v, int flip_bit_2) {
+    // flip_bit_2 is 0 or 2: moves to bit 63
+    return __longlong_as_double(__double_as_longlong(v) ^
+                                ((unsigned long long)(unsigned)flip_bit_2 << 62));
+}
 __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
     constexpr double INV_PIO2 = 6.36619772367581382433e-01;
     constexpr double PIO2_1 = 1.57079632679489655800e+00;   // first 53 bits of pi/2
     constexpr double PIO2_2 = 6.12323399573676603587e-17;   // pi/2 - PIO2_1
-    constexpr double PIO2_3 = -1.4973849048591698e-33;      // pi/2 - PIO2_1 - PIO2_2
     const double q = rint(x * INV_PIO2);
     double r = fma(-q, PIO2_1, x);
     r = fma(-q, PIO2_2, r);
-    r = fma(-q, PIO2_3, r);
-    const int64_t iq = (int64_t)q;
+    const int iq = (int)q;
     const double z = r * r;
     // fdlibm __kernel_sin / __kernel_cos coefficients
     const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10,
@@ -795,11 +800,18 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double cr = w + (((1.0 - w) - hz) + z * z * pc);
-    const int quad = (int)(iq & 3);
-    const double ss = (quad & 1) ? cr : sr;
-    const double cc = (quad & 1) ? sr : cr;
-    s = (quad & 2) ? -ss : ss;
-    c = ((quad + 1) & 2) ? -cc : cc;
+    const bool odd = (iq & 1) != 0;
+    s = flip_sign_if(odd ? cr : sr, iq & 2);
+    c = flip_sign_if(odd ? sr : cr, (iq + 1) & 2);
+}
+
+// 1/sqrt(x) for finite x > 0 to full double precision: the hardware estimate plus one
+// third-order correction (the OCML sequence without its special-value fix-up, which the
+// callers make unnecessary by masking x <= 0).
+__device__ __forceinline__ double rsqrt_pos(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
 // Q factor. The mirror-convention term of one branch is A Y Q e^{i(2 pi g t - Phi)} with
@@ -928,27 +940,31 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_re
 
 // Branch-free SPA evaluation of interval record `it` at g on the fast path: returns
 // zc = A Q e^{i(2 pi g t - Phi)} (the mirror-convention term before Y and scale; see the
-// Q-factor notes above) and ok = false when this lane needs the general path (t(g) overshot the
-// record's knot interval, or |y| < 555 in the uniform mode) -- then zc is 0.
+// Q-factor notes above) for lanes with `act` set. need_general is set for active lanes that
+// the general path must redo (t(g) overshot the record's knot interval, F' = 0, or |y| < 555 in
+// the uniform mode); zc is 0 for those and for inactive lanes. Everything is computed
+// unconditionally and masked once at the end (selects, no divergent branches).
 template <int CAUSTIC>
-__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, double& zr,
-                                         double& zi, bool& ok) {
+__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, bool act,
+                                         double& zr, double& zi, bool& need_general) {
     const double u = g - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     const double w = tt - it->tj;
-    bool good = (tt >= it->tj) && (tt < it->tj1);
+    bool good = (tt >= it->tj) & (tt < it->tj1);
     double ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
     double ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
     const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-    const double amp = fd != 0.0 ? rsqrt(fabs(fd)) : 0.0;
-    const double psi = fma(TWO_PI * g, tt, -ph) + (fd > 0.0 ? 0.75 * PI : -0.75 * PI);
+    const double afd = fabs(fd);
+    good = good & (afd > 0.0);
+    const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
+    const double psi = fma(TWO_PI * g, tt, -ph) + copysign(0.75 * PI, fd);
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
         const double fdd = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
         const double a2 = amp * amp;
         const double a6 = a2 * a2 * a2;   // 1/|F'|^3
-        const double ww = (fd > 0.0 ? 1.0 : -1.0) * (3.0 / TWO_PI) * fdd * fdd * a6;
-        good = good && (fabs(ww) * 555.0 <= 1.0);
+        const double ww = copysign((3.0 / TWO_PI) * fdd * fdd * a6, fd);
+        good = good & (fabs(ww) * 555.0 <= 1.0);
         const double uu = ww * ww;
         const double R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
         const double I = ww * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
@@ -958,10 +974,10 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, 
     }
     double sn, cs;
     sincos_big(psi, sn, cs);
-    const double a = good ? amp : 0.0;
+    const double a = (act & good) ? amp : 0.0;
     zr = a * (ar * cs - ai * sn);
     zi = a * (ar * sn + ai * cs);
-    ok = good;
+    need_general = act & !good;
 }
 
 // General (cold) path: scipy interval selection for t(g) and the full K_{1/3} evaluation.
@@ -1207,30 +1223,26 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                 const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
                 if (khi <= w_lo || klo >= w_hi) continue;     // misses this wave's chunk
                 const double gs = s ? 1.0 : -1.0;
-                bool okall = true;
-                bool act[BPL];
+                bool anyneed = false;
+                bool need[BPL];
                 double zr[BPL], zi[BPL];
 #pragma unroll
                 for (int i = 0; i < BPL; ++i) {
                     const int32_t k = w_lo + 64 * i + lane;
-                    act[i] = k >= klo && k < khi;
-                    bool ok;
+                    const bool act = (k >= klo) & (k < khi);
 #ifdef EFD_EXP_NOCOMPUTE
-                    zr[i] = fk[i] * it->ar[0]; zi[i] = gs * it->ai[1]; ok = true;
+                    zr[i] = act ? fk[i] * it->ar[0] : 0.0; zi[i] = gs * it->ai[1]; need[i] = false;
 #else
-                    spa_fast<CAUSTIC>(it, gs * fk[i], zr[i], zi[i], ok);
+                    spa_fast<CAUSTIC>(it, gs * fk[i], act, zr[i], zi[i], need[i]);
 #endif
-                    zr[i] = act[i] ? zr[i] : 0.0;
-                    zi[i] = act[i] ? zi[i] : 0.0;
-                    okall = okall && (ok || !act[i]);
-                    act[i] = act[i] && !ok;   // lanes left for the general path
+                    anyneed = anyneed | need[i];
                 }
-                if (__builtin_expect(!__all(okall), 0)) {     // cold: general path for some lanes
+                if (__builtin_expect(__any(anyneed), 0)) {     // cold: general path, some lanes
                     const Item* git = items + (key >> 1);
                     const int h = git->h;
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
-                        if (act[i]) {
+                        if (need[i]) {
                             const double2 zg = spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K,
                                                                     marr[h], narr[h], coefA, coefT);
                             zr[i] = zg.x;
@@ -1238,18 +1250,28 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                         }
                     }
                 }
+                // own bin: s = 0 -> Y+ z (parent, f = -g); s = 1 -> Y- conj(z) (partner, f = +g)
+                // mirror:  s = 0 -> Y- conj(z);                s = 1 -> Y+ z
+                // With Y- conj(z) = conj(conj(Y-) z), both are (Yo z) with the imaginary part's
+                // sign so: Yo = s ? conj(Y-) : Y+, so = s ? -1 : 1 (and Ym, -so for the
+                // mirror) -- four FMAs per accumulator, no selects per bin.
                 const double ypr = it->yp[0], ypi = it->yp[1];
                 const double ymr = it->ym[0], ymi = it->ym[1];
+                const double so = s ? -1.0 : 1.0;
+                const double o1 = s ? ymr : ypr, o2 = s ? -ymi : ypi;   // Yo = o1 + i o2
+                const double m1 = s ? ypr : ymr, m2 = s ? ypi : -ymi;   // Ym = m1 + i m2
+                const double o3 = so * o1, o4 = so * o2, m3 = -so * m1, m4 = -so * m2;
 #pragma unroll
                 for (int i = 0; i < BPL; ++i) {
-                    // P = Y+ z (parent, f = -g), Q = Y- conj(z) (partner, f = +g)
-                    const double pr = ypr * zr[i] - ypi * zi[i], pi = ypr * zi[i] + ypi * zr[i];
-                    const double qr = ymr * zr[i] + ymi * zi[i], qi = ymi * zr[i] - ymr * zi[i];
-                    own_r[i] += s ? qr : pr;
-                    own_i[i] += s ? qi : pi;
+                    own_r[i] = fma(o1, zr[i], own_r[i]);
+                    own_r[i] = fma(-o2, zi[i], own_r[i]);
+                    own_i[i] = fma(o3, zi[i], own_i[i]);
+                    own_i[i] = fma(o4, zr[i], own_i[i]);
                     if (PAIRED) {
-                        mir_r[i] += s ? pr : qr;
-                        mir_i[i] += s ? pi : qi;
+                        mir_r[i] = fma(m1, zr[i], mir_r[i]);
+                        mir_r[i] = fma(-m2, zi[i], mir_r[i]);
+                        mir_i[i] = fma(m3, zi[i], mir_i[i]);
+                        mir_i[i] = fma(m4, zr[i], mir_i[i]);
                     }
                 }
             }
