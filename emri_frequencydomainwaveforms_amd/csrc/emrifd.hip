@@ -60,6 +60,8 @@ constexpr int SEGWIN = 1024;        // segments examined per window when buildin
 constexpr int NC = 32;              // interval records per LDS stage in k_modesum
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
+constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
+constexpr double INV_SQRT_3_2PI = 1.44720250911653531871; // sqrt(2 pi / 3)
 
 thread_local std::string g_err;
 
@@ -89,7 +91,7 @@ struct __attribute__((aligned(16))) Item {
     double ai[4];     // Im A(t)
     double ph[4];     // Phi_k(t) = m Phi_phi + n Phi_r
     double fd[3];     // F'(t)
-    double fdd[3];    // F''(t): derivative of the spline of F'(t_i) (notebook :583)
+    double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
     double yp[2];     // -scale * Y+        (parent branch, f = -g)
     double ym[2];     // -scale * Y-        (partner branch, f = +g)
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
@@ -622,7 +624,10 @@ __device__ unsigned long long build_item(
         const double G0 = dm * ct[0 * 8 + 4] + dn * ct[0 * 8 + 5];
         const double G1 = dm * ct[1 * 8 + 4] + dn * ct[1 * 8 + 5];
         const double G2 = dm * ct[2 * 8 + 4] + dn * ct[2 * 8 + 5];
-        it.fdd[0] = 3.0 * G0; it.fdd[1] = 2.0 * G1; it.fdd[2] = G2;
+        // pre-scaled so the fast path's w = 3 F''^2 / (2 pi |F'|^3) is one square
+        it.fdd[0] = SQRT_3_2PI * (3.0 * G0);
+        it.fdd[1] = SQRT_3_2PI * (2.0 * G1);
+        it.fdd[2] = SQRT_3_2PI * G2;
     }
     // S = -h_nb(-f) * scale: fold the minus sign and the complex scale into Y
     {
@@ -945,9 +950,11 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_re
 // the uniform mode); zc is 0 for those and for inactive lanes. Everything is computed
 // unconditionally and masked once at the end (selects, no divergent branches).
 template <int CAUSTIC>
-__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, bool act,
-                                         double& zr, double& zi, bool& need_general) {
-    const double u = g - it->gx;
+__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs, double fk,
+                                         double tfk, bool act, double& zr, double& zi,
+                                         bool& need_general) {
+    // g = gs * fk (gs = +-1, fk the lane's bin frequency, tfk = 2 pi fk)
+    const double u = fma(gs, fk, -it->gx);
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     const double w = tt - it->tj;
     bool good = (tt >= it->tj) & (tt < it->tj1);
@@ -958,12 +965,13 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double g, 
     const double afd = fabs(fd);
     good = good & (afd > 0.0);
     const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
-    const double psi = fma(TWO_PI * g, tt, -ph) + copysign(0.75 * PI, fd);
+    const double psi = fma(gs * tfk, tt, -ph) + copysign(0.75 * PI, fd);
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
-        const double fdd = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
-        const double a2 = amp * amp;
-        const double a6 = a2 * a2 * a2;   // 1/|F'|^3
-        const double ww = copysign((3.0 / TWO_PI) * fdd * fdd * a6, fd);
+        // w = 3 F''^2 / (2 pi F'^3) = (fdd_scaled * |F'|^-3/2)^2 with the sign of F'
+        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        const double a3 = amp * amp * amp;
+        const double t3 = fdds * a3;
+        const double ww = copysign(t3 * t3, fd);
         good = good & (fabs(ww) * 555.0 <= 1.0);
         const double uu = ww * ww;
         const double R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
@@ -995,7 +1003,7 @@ __device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double 
         ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-        fdd = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        fdd = INV_SQRT_3_2PI * fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
     } else {  // t(g) overshot the record's knot interval: evaluate like scipy
         const FwdEval fe = forward_generic(tt, t, nt, h, K, m, n, coefA, coefT);
         ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd; fdd = fe.fdd;
@@ -1076,12 +1084,13 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
     const int32_t w_hi = w_lo + 64 * BPL;
-    double fk[BPL];
+    double fk[BPL], tfk[BPL];
     double own_r[BPL], own_i[BPL], mir_r[BPL], mir_i[BPL];
 #pragma unroll
     for (int i = 0; i < BPL; ++i) {
         const int32_t k = w_lo + 64 * i + lane;
         fk[i] = k < nlanes ? freq[k] : 0.0;
+        tfk[i] = TWO_PI * fk[i];
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
 
@@ -1233,7 +1242,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
 #ifdef EFD_EXP_NOCOMPUTE
                     zr[i] = act ? fk[i] * it->ar[0] : 0.0; zi[i] = gs * it->ai[1]; need[i] = false;
 #else
-                    spa_fast<CAUSTIC>(it, gs * fk[i], act, zr[i], zi[i], need[i]);
+                    spa_fast<CAUSTIC>(it, gs, fk[i], tfk[i], act, zr[i], zi[i], need[i]);
 #endif
                     anyneed = anyneed | need[i];
                 }
