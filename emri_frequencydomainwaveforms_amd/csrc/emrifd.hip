@@ -189,9 +189,9 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
         // row i: a = dx_i, b = 2(dx_{i-1} + dx_i), c = dx_{i-1}, r = 3(dx_i sl_{i-1} + dx_{i-1} sl_i)
         const double a = dxi, b = 2.0 * (dxm + dxi), c = dxm;
         const double r = 3.0 * (dxi * slm + dxm * sli);
-        const double mm = b - a * cpm;
-        cpm = c / mm;
-        dpm = (r - a * dpm) / mm;
+        const double inv = 1.0 / (b - a * cpm);   // one division on the serial chain
+        cpm = c * inv;
+        dpm = (r - a * dpm) * inv;
         CP(i) = cpm;
         DP(i) = dpm;
         if (i + 2 <= n - 1) {
@@ -212,24 +212,35 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
         const double mm = b - a * cpm;
         s_next = (r - a * dpm) / mm;
     }
-    // back substitution, emitting interval coefficients from the right (the next row's
-    // scratch and knot values are loaded one iteration ahead: the chain is latency-bound)
+    // back substitution, emitting interval coefficients from the right. CP/DP may live in
+    // global memory: they are fetched PF rows at a time (independent loads, one wait per
+    // block) so the serial chain does not pay a memory round trip per row.
+    constexpr int PF = 8;
     double xr = X(n - 1), yr = Y(n - 1);
-    double dpi = DP(n - 2), cpi = CP(n - 2), xl = X(n - 2), yl = Y(n - 2);
-    for (int i = n - 2; i >= 0; --i) {
-        double dpn = 0.0, cpn = 0.0, xln = 0.0, yln = 0.0;
-        if (i > 0) { dpn = DP(i - 1); cpn = CP(i - 1); xln = X(i - 1); yln = Y(i - 1); }
-        const double s_i = dpi - cpi * s_next;
-        const double dx = xr - xl;
-        const double sl = (yr - yl) / dx;
-        const double tt = (s_i + s_next - 2.0 * sl) / dx;
-        OUT(i, 0, tt / dx);
-        OUT(i, 1, (sl - s_i) / dx - tt);
-        OUT(i, 2, s_i);
-        OUT(i, 3, yl);
-        s_next = s_i;
-        xr = xl; yr = yl;
-        dpi = dpn; cpi = cpn; xl = xln; yl = yln;
+    for (int i0 = n - 2; i0 >= 0; i0 -= PF) {
+        double cpb[PF], dpb[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int i = i0 - k;
+            cpb[k] = i >= 0 ? CP(i) : 0.0;
+            dpb[k] = i >= 0 ? DP(i) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int i = i0 - k;
+            if (i < 0) break;
+            const double xl = X(i), yl = Y(i);
+            const double s_i = dpb[k] - cpb[k] * s_next;
+            const double dx = xr - xl;
+            const double sl = (yr - yl) / dx;
+            const double tt = (s_i + s_next - 2.0 * sl) / dx;
+            OUT(i, 0, tt / dx);
+            OUT(i, 1, (sl - s_i) / dx - tt);
+            OUT(i, 2, s_i);
+            OUT(i, 3, yl);
+            s_next = s_i;
+            xr = xl; yr = yl;
+        }
     }
 }
 
@@ -339,12 +350,16 @@ __device__ void spline_shared(const double* __restrict__ x, int n, const double*
         spline_not_a_knot(n, X, Y, CP, DP, OUT);
         return;
     }
-    double* dpb = coef + ninterp;   // DP(i) at coef[(i*4+1)*ninterp + q]
-    auto DPs = [&](int i) -> double& { return dpb[(size_t)i * scratch_stride + q]; };
-    // forward sweep: dp_i = (r_i - a_i dp_{i-1}) / m_i
-    double y0 = Y(0), y1 = Y(1), y2 = Y(2);
+    double* dpbase = coef + ninterp;   // DP(i) at coef[(i*4+1)*ninterp + q]
+    auto DPs = [&](int i) -> double& { return dpbase[(size_t)i * scratch_stride + q]; };
+    // Global loads (y, and DP on the way back) are issued PF rows at a time, ahead of the
+    // serial recurrence, so each block of rows waits for memory once.
+    constexpr int PF = 8;
+    // forward sweep: dp_i = (r_i - a_i dp_{i-1}) / m_i, r_i from sl_{i-1}, sl_i
+    const double y0 = Y(0), y1 = Y(1);
+    double yprev = Y(2);
     double dxm = xs[1] - xs[0], dxi = xs[2] - xs[1];
-    double slm = (y1 - y0) / dxm, sli = (y2 - y1) / dxi;
+    double slm = (y1 - y0) / dxm, sli = (yprev - y1) / dxi;
     double dp;
     {
         const double d = xs[2] - xs[0];
@@ -352,18 +367,26 @@ __device__ void spline_shared(const double* __restrict__ x, int n, const double*
         dp = r0 * iml[0];
         DPs(0) = dp;
     }
-    double yi = y2;
-    double ynext = (n > 3) ? Y(3) : 0.0;
-    for (int i = 1; i <= n - 2; ++i) {
-        const double r = 3.0 * (dxi * slm + dxm * sli);
-        dp = (r - all[i] * dp) * iml[i];
-        DPs(i) = dp;
-        if (i + 2 <= n - 1) {
-            const double yn = ynext;
-            if (i + 3 <= n - 1) ynext = Y(i + 3);
-            dxm = dxi; slm = sli;
-            dxi = xs[i + 2] - xs[i + 1]; sli = (yn - yi) / dxi;
-            yi = yn;
+    for (int i0 = 1; i0 <= n - 2; i0 += PF) {
+        double yb[PF];   // y_{i+2} for rows i0 .. i0+PF-1
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int j = i0 + k + 2;
+            yb[k] = j <= n - 1 ? Y(j) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int i = i0 + k;
+            if (i > n - 2) break;
+            const double r = 3.0 * (dxi * slm + dxm * sli);
+            dp = (r - all[i] * dp) * iml[i];
+            DPs(i) = dp;
+            if (i + 2 <= n - 1) {
+                dxm = dxi; slm = sli;
+                dxi = xs[i + 2] - xs[i + 1];
+                sli = (yb[k] - yprev) / dxi;
+                yprev = yb[k];
+            }
         }
     }
     double s_next;
@@ -372,23 +395,32 @@ __device__ void spline_shared(const double* __restrict__ x, int n, const double*
         const double r = (dxi * dxi * slm + (2.0 * d + dxi) * dxm * sli) / d;
         s_next = (r - all[n - 1] * dp) * iml[n - 1];
     }
-    // back substitution with one-row prefetch of DP and y
+    // back substitution
     double yr = Y(n - 1);
-    double dpi = DPs(n - 2), yl = Y(n - 2);
-    for (int i = n - 2; i >= 0; --i) {
-        double dpn = 0.0, yln = 0.0;
-        if (i > 0) { dpn = DPs(i - 1); yln = Y(i - 1); }
-        const double s_i = dpi - cpl[i] * s_next;
-        const double dx = xs[i + 1] - xs[i];
-        const double sl = (yr - yl) / dx;
-        const double tt = (s_i + s_next - 2.0 * sl) / dx;
-        OUT(i, 0, tt / dx);
-        OUT(i, 1, (sl - s_i) / dx - tt);
-        OUT(i, 2, s_i);
-        OUT(i, 3, yl);
-        s_next = s_i;
-        yr = yl;
-        dpi = dpn; yl = yln;
+    for (int i0 = n - 2; i0 >= 0; i0 -= PF) {
+        double dpb[PF], ylb[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int i = i0 - k;
+            dpb[k] = i >= 0 ? DPs(i) : 0.0;
+            ylb[k] = i >= 0 ? Y(i) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int i = i0 - k;
+            if (i < 0) break;
+            const double yl = ylb[k];
+            const double s_i = dpb[k] - cpl[i] * s_next;
+            const double dx = xs[i + 1] - xs[i];
+            const double sl = (yr - yl) / dx;
+            const double tt = (s_i + s_next - 2.0 * sl) / dx;
+            OUT(i, 0, tt / dx);
+            OUT(i, 1, (sl - s_i) / dx - tt);
+            OUT(i, 2, s_i);
+            OUT(i, 3, yl);
+            s_next = s_i;
+            yr = yl;
+        }
     }
 }
 
@@ -485,6 +517,12 @@ __global__ __launch_bounds__(64) void k_prep(
     int32_t* __restrict__ runs, Item* __restrict__ items, double* __restrict__ invcp,
     double* __restrict__ invdp, int32_t* __restrict__ err) {
     const int b = blockIdx.x;
+#ifdef EFD_EXP_PREP_ROLE
+    {
+        const int role = b == 0 ? 0 : (b < 1 + nb_amp ? 1 : 2);
+        if (role != EFD_EXP_PREP_ROLE) return;
+    }
+#endif
     if (b == 0) {
         traj_splines(t, phi_phi, phi_r, f_phi, f_r, nt, coefT, kslope, tscratch);
     } else if (b < 1 + nb_amp) {
@@ -1499,6 +1537,9 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
                            nb_amp, coefT, kslope, (double*)(ws + L.tscratch), coefA, runs, items,
                            invcp, invdp, &hdr->runs_overflow);
         HIP_TRY(hipGetLastError());
+#ifdef EFD_EXP_PREP_ROLE
+        return EFD_OK;   // timing experiment: the later stages would read partial data
+#endif
     }
     // K4: interval records
     {
