@@ -46,18 +46,22 @@
 
 namespace {
 
-constexpr int TILE = 256;           // threads per workgroup in k_modesum
+#ifndef EFD_TILE
+#define EFD_TILE 256
+#endif
+constexpr int TILE = EFD_TILE;      // threads per workgroup in k_modesum
+constexpr int NWAVE = TILE / 64;    // waves per workgroup
 #ifndef EFD_BPL
 #define EFD_BPL 2
 #endif
 constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
-constexpr int XCD_GROUP = 4;        // consecutive tiles per XCD in the k_modesum dispatch order
+constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
-constexpr int KEYCAP = 2048;        // record keys per tile pass held in LDS
-constexpr int SEGWIN = 1024;        // segments examined per window when building a tile list
-constexpr int NC = 32;              // interval records per LDS stage in k_modesum
+constexpr int KEYCAP = TILE >= 256 ? 2048 : 1024;  // record keys per tile pass held in LDS
+constexpr int SEGWIN = 4 * TILE;    // segments examined per window when building a tile list
+constexpr int NC = TILE / 8;        // interval records per LDS stage (two 16-B pieces/thread)
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
@@ -986,7 +990,10 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_re
 // Q-factor notes above) for lanes with `act` set. need_general is set for active lanes that
 // the general path must redo (t(g) overshot the record's knot interval, F' = 0, or |y| < 555 in
 // the uniform mode); zc is 0 for those and for inactive lanes. Everything is computed
-// unconditionally and masked once at the end (selects, no divergent branches).
+// unconditionally and masked once at the end (selects, no divergent branches). A wider fast
+// path (a wave-uniform 40-term branch for 18.4 <= |y| < 555) cut general-path calls 5x but
+// cost 4% overall through the hot loop's code generation, so it is not used: the general path
+// runs for ~1.5% of (record, wave) evaluations.
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs, double fk,
                                          double tfk, bool act, double& zr, double& zi,
@@ -1081,6 +1088,9 @@ __device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double 
 // Each record feeds BPL independent, branch-free evaluations per lane; lanes needing the
 // general path are masked and redone in a cold block.
 // ----------------------------------------------------------------------------------------
+#ifdef EFD_EXP_COUNT
+__device__ unsigned long long g_exp_count[4];   // record evals, cold-path evals, cold lanes, skips
+#endif
 template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) void k_modesum(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
@@ -1094,7 +1104,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
     __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
-    __shared__ int wcnt[4];
+    __shared__ int wcnt[NWAVE];
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
     // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
@@ -1177,7 +1187,8 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                         const unsigned long long below = bal & ((1ull << lane) - 1ull);
                         hits[before + __popcll(below)] = sgi;
                     }
-                    nhit += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+#pragma unroll
+                    for (int w = 0; w < NWAVE; ++w) nhit += wcnt[w];
                     __syncthreads();
                 }
                 win += SEGWIN;
@@ -1268,7 +1279,15 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                 const Item* it = stg + ii;
                 const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
                 const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
-                if (khi <= w_lo || klo >= w_hi) continue;     // misses this wave's chunk
+                if (khi <= w_lo || klo >= w_hi) {              // misses this wave's chunk
+#ifdef EFD_EXP_COUNT
+                    if (lane == 0) atomicAdd(&g_exp_count[3], 1ull);
+#endif
+                    continue;
+                }
+#ifdef EFD_EXP_COUNT
+                if (lane == 0) atomicAdd(&g_exp_count[0], 1ull);
+#endif
                 const double gs = s ? 1.0 : -1.0;
                 bool anyneed = false;
                 bool need[BPL];
@@ -1285,6 +1304,13 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                     anyneed = anyneed | need[i];
                 }
                 if (__builtin_expect(__any(anyneed), 0)) {     // cold: general path, some lanes
+#ifdef EFD_EXP_COUNT
+                    {
+                        const unsigned long long nl_ = __popcll(__ballot(need[0])) +
+                                                       (BPL > 1 ? __popcll(__ballot(need[BPL - 1])) : 0);
+                        if (lane == 0) { atomicAdd(&g_exp_count[1], 1ull); atomicAdd(&g_exp_count[2], nl_); }
+                    }
+#endif
                     const Item* git = items + (key >> 1);
                     const int h = git->h;
 #pragma unroll
@@ -1466,6 +1492,14 @@ __global__ void k_inner_final(const double2* __restrict__ part, int np, double s
 extern "C" {
 
 int efd_version(void) { return EFD_VERSION; }
+
+#ifdef EFD_EXP_COUNT
+int efd_exp_counters(unsigned long long* out) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 4));
+    return EFD_OK;
+}
+#endif
 
 int efd_last_error(char* buf, int len) {
     if (!buf || len <= 0) return EFD_ERR_ARG;
