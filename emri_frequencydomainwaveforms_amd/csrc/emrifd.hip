@@ -852,6 +852,29 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
     c = flip_sign_if(odd ? sr : cr, (iq + 1) & 2);
 }
 
+// sin/cos for the fast path: reduce by pi/128 against a 256-entry table of (sin, cos)(k pi/128)
+// held in LDS, then short Taylor polynomials on |r| <= pi/256 (truncation < 1e-20 relative)
+// and the angle-sum formula. ~17 FP64 operations instead of ~26 plus the quadrant logic of
+// sincos_big; the table read is one 16-B LDS access per value. Valid for |x| < 2^31 pi/128.
+constexpr int SCTAB = 256;
+__device__ __forceinline__ void sincos_tab(double x, const double2* __restrict__ tab, double& s,
+                                           double& c) {
+    constexpr double INV_STEP = 40.74366543152521;       // 128 / pi
+    constexpr double STEP_1 = 0.02454369260617026;       // pi/128, leading part
+    constexpr double STEP_2 = 9.567553118338697e-19;     // pi/128 - STEP_1
+    const double q = rint(x * INV_STEP);
+    double r = fma(-q, STEP_1, x);
+    r = fma(-q, STEP_2, r);
+    const double2 t = tab[(int)q & (SCTAB - 1)];          // (sin, cos)(q pi/128)
+    const double z = r * r;
+    const double sr = fma(r * z, fma(z, fma(z, -1.984126984126984e-04, 8.333333333333333e-03),
+                                     -1.6666666666666666e-01), r);
+    const double cr = fma(z, fma(z, fma(z, -1.388888888888889e-03, 4.1666666666666664e-02),
+                                 -0.5), 1.0);
+    s = fma(t.x, cr, t.y * sr);
+    c = fma(t.y, cr, -t.x * sr);
+}
+
 // 1/sqrt(x) for finite x > 0 to full double precision: the hardware estimate plus one
 // third-order correction (the OCML sequence without its special-value fix-up, which the
 // callers make unnecessary by masking x <= 0).
@@ -996,8 +1019,8 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_re
 // runs for ~1.5% of (record, wave) evaluations.
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs, double fk,
-                                         double tfk, bool act, double& zr, double& zi,
-                                         bool& need_general) {
+                                         double tfk, bool act, const double2* __restrict__ sct,
+                                         double& zr, double& zi, bool& need_general) {
     // g = gs * fk (gs = +-1, fk the lane's bin frequency, tfk = 2 pi fk)
     const double u = fma(gs, fk, -it->gx);
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
@@ -1026,7 +1049,7 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs,
         ar = nr;
     }
     double sn, cs;
-    sincos_big(psi, sn, cs);
+    sincos_tab(psi, sct, sn, cs);
     const double a = (act & good) ? amp : 0.0;
     zr = a * (ar * cs - ai * sn);
     zi = a * (ar * sn + ai * cs);
@@ -1092,7 +1115,11 @@ __device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double 
 __device__ unsigned long long g_exp_count[4];   // record evals, cold-path evals, cold lanes, skips
 #endif
 template <bool PAIRED, int CAUSTIC, int BPL>
+#ifdef EFD_EXP_WAVES_PER_EU
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_EXP_WAVES_PER_EU, 8))) void k_modesum(
+#else
 __global__ __launch_bounds__(TILE) void k_modesum(
+#endif
     const Item* __restrict__ items, const int4* __restrict__ ranges,
     const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
     const int32_t* __restrict__ nsegp, const double* __restrict__ freq, int64_t nf,
@@ -1105,6 +1132,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     __shared__ int part[TILE];
     __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
     __shared__ int wcnt[NWAVE];
+    __shared__ double2 sctab[SCTAB];   // (sin, cos)(k pi/128) for sincos_tab
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
     // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
@@ -1119,6 +1147,12 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int ni = nt - 1;
+    for (int k = tid; k < SCTAB; k += TILE) {
+        double sv, cv;
+        sincospi((double)k / (SCTAB / 2), &sv, &cv);
+        sctab[k] = make_double2(sv, cv);
+    }
+    __syncthreads();
 
     // ---- the tile's record list, built in LDS from the segment table (no global list, no
     // atomics). Segments are taken in windows of SEGWIN: (1) each thread tests SEGWIN/TILE
@@ -1299,10 +1333,13 @@ __global__ __launch_bounds__(TILE) void k_modesum(
 #ifdef EFD_EXP_NOCOMPUTE
                     zr[i] = act ? fk[i] * it->ar[0] : 0.0; zi[i] = gs * it->ai[1]; need[i] = false;
 #else
-                    spa_fast<CAUSTIC>(it, gs, fk[i], tfk[i], act, zr[i], zi[i], need[i]);
+                    spa_fast<CAUSTIC>(it, gs, fk[i], tfk[i], act, sctab, zr[i], zi[i], need[i]);
 #endif
                     anyneed = anyneed | need[i];
                 }
+#ifdef EFD_EXP_NOSLOW
+                anyneed = false;
+#endif
                 if (__builtin_expect(__any(anyneed), 0)) {     // cold: general path, some lanes
 #ifdef EFD_EXP_COUNT
                     {
