@@ -96,8 +96,8 @@ struct __attribute__((aligned(16))) Item {
     double ph[4];     // Phi_k(t) = m Phi_phi + n Phi_r
     double fd[3];     // F'(t)
     double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
-    double yp[2];     // -scale * Y+        (parent branch, f = -g)
-    double ym[2];     // -scale * Y-        (partner branch, f = +g)
+    double y[2][2];   // y[0] = -scale * Y+ (parent, f = -g); y[1] = conj(-scale * Y-) (partner,
+                      // f = +g; conjugated so that sub-branch s reads its own factor as y[s])
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
     int32_t flags;    // bit0: interval part of a run; bit1: has partner (m != 0)
     int32_t h;
@@ -674,11 +674,11 @@ __device__ unsigned long long build_item(
     // S = -h_nb(-f) * scale: fold the minus sign and the complex scale into Y
     {
         const double yr = ylm_p[2 * h], yi = ylm_p[2 * h + 1];
-        it.yp[0] = -(sc_re * yr - sc_im * yi);
-        it.yp[1] = -(sc_re * yi + sc_im * yr);
+        it.y[0][0] = -(sc_re * yr - sc_im * yi);
+        it.y[0][1] = -(sc_re * yi + sc_im * yr);
         const double zr = partner ? ylm_m[2 * h] : 0.0, zi = partner ? ylm_m[2 * h + 1] : 0.0;
-        it.ym[0] = -(sc_re * zr - sc_im * zi);
-        it.ym[1] = -(sc_re * zi + sc_im * zr);
+        it.y[1][0] = -(sc_re * zr - sc_im * zi);
+        it.y[1][1] = (sc_re * zi + sc_im * zr);   // conjugate of -scale * Y-
     }
     // g-interval of this record: [x_lo, x_hi), lower end open at the run's first knot
     const double Fj = knotF(f_phi, f_r, m, n, j), Fj1 = knotF(f_phi, f_r, m, n, j + 1);
@@ -852,25 +852,24 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
     c = flip_sign_if(odd ? sr : cr, (iq + 1) & 2);
 }
 
-// sin/cos for the fast path: reduce by pi/128 against a 256-entry table of (sin, cos)(k pi/128)
-// held in LDS, then short Taylor polynomials on |r| <= pi/256 (truncation < 1e-20 relative)
-// and the angle-sum formula. ~17 FP64 operations instead of ~26 plus the quadrant logic of
-// sincos_big; the table read is one 16-B LDS access per value. Valid for |x| < 2^31 pi/128.
-constexpr int SCTAB = 256;
-__device__ __forceinline__ void sincos_tab(double x, const double2* __restrict__ tab, double& s,
-                                           double& c) {
-    constexpr double INV_STEP = 40.74366543152521;       // 128 / pi
-    constexpr double STEP_1 = 0.02454369260617026;       // pi/128, leading part
-    constexpr double STEP_2 = 9.567553118338697e-19;     // pi/128 - STEP_1
+// sin/cos for the fast path: reduce by pi/256 against a 512-entry table of
+// (sin, cos)(k pi/256) held in LDS, then short Taylor polynomials on |r| <= pi/512 (sin to r^5,
+// cos to r^4: truncation < 1e-16 relative) and the angle-sum formula: ~14 FP64 operations
+// instead of ~26 plus the quadrant logic of sincos_big. `shift` (an integer number of table
+// steps) is added to the angle exactly, through the table index. Valid for |x| < 2^31 pi/256.
+constexpr int SCTAB = 512;
+__device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
+                                           double& s, double& c) {
+    constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
+    constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
+    constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
     const double q = rint(x * INV_STEP);
     double r = fma(-q, STEP_1, x);
     r = fma(-q, STEP_2, r);
-    const double2 t = tab[(int)q & (SCTAB - 1)];          // (sin, cos)(q pi/128)
+    const double2 t = tab[((int)q + shift) & (SCTAB - 1)];   // (sin, cos)((q + shift) pi/256)
     const double z = r * r;
-    const double sr = fma(r * z, fma(z, fma(z, -1.984126984126984e-04, 8.333333333333333e-03),
-                                     -1.6666666666666666e-01), r);
-    const double cr = fma(z, fma(z, fma(z, -1.388888888888889e-03, 4.1666666666666664e-02),
-                                 -0.5), 1.0);
+    const double sr = fma(r * z, fma(z, 8.333333333333333e-03, -1.6666666666666666e-01), r);
+    const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), 1.0);
     s = fma(t.x, cr, t.y * sr);
     c = fma(t.y, cr, -t.x * sr);
 }
@@ -1033,7 +1032,9 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs,
     const double afd = fabs(fd);
     good = good & (afd > 0.0);
     const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
-    const double psi = fma(gs * tfk, tt, -ph) + copysign(0.75 * PI, fd);
+    // psi = 2 pi g t - Phi + sgn(F') 3 pi/4; the 3 pi/4 (192 table steps) goes in as an index
+    const double psi0 = fma(gs * tfk, tt, -ph);
+    const int shift = fd > 0.0 ? 192 : -192;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
         // w = 3 F''^2 / (2 pi F'^3) = (fdd_scaled * |F'|^-3/2)^2 with the sign of F'
         const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
@@ -1049,7 +1050,7 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs,
         ar = nr;
     }
     double sn, cs;
-    sincos_tab(psi, sct, sn, cs);
+    sincos_tab(psi0, shift, sct, sn, cs);
     const double a = (act & good) ? amp : 0.0;
     zr = a * (ar * cs - ai * sn);
     zi = a * (ar * sn + ai * cs);
@@ -1149,7 +1150,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
     const int ni = nt - 1;
     for (int k = tid; k < SCTAB; k += TILE) {
         double sv, cv;
-        sincospi((double)k / (SCTAB / 2), &sv, &cv);
+        sincospi((double)k / (SCTAB / 2), &sv, &cv);   // (sin, cos)(k pi / 256)
         sctab[k] = make_double2(sv, cv);
     }
     __syncthreads();
@@ -1362,14 +1363,13 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                 }
                 // own bin: s = 0 -> Y+ z (parent, f = -g); s = 1 -> Y- conj(z) (partner, f = +g)
                 // mirror:  s = 0 -> Y- conj(z);                s = 1 -> Y+ z
-                // With Y- conj(z) = conj(conj(Y-) z), both are (Yo z) with the imaginary part's
-                // sign so: Yo = s ? conj(Y-) : Y+, so = s ? -1 : 1 (and Ym, -so for the
-                // mirror) -- four FMAs per accumulator, no selects per bin.
-                const double ypr = it->yp[0], ypi = it->yp[1];
-                const double ymr = it->ym[0], ymi = it->ym[1];
+                // With Y- conj(z) = conj(conj(Y-) z) and the record holding (Y+, conj(Y-)) as
+                // y[0], y[1]: own += Yo z with Yo = y[s], mirror += Ym z with Ym = y[1-s], the
+                // imaginary parts signed so = s ? -1 : 1 and -so. The factors come straight
+                // from LDS at an s-dependent offset: four FMAs per accumulator, no selects.
+                const double o1 = it->y[s][0], o2 = it->y[s][1];          // Yo = o1 + i o2
+                const double m1 = it->y[1 - s][0], m2 = it->y[1 - s][1];  // Ym = m1 + i m2
                 const double so = s ? -1.0 : 1.0;
-                const double o1 = s ? ymr : ypr, o2 = s ? -ymi : ypi;   // Yo = o1 + i o2
-                const double m1 = s ? ypr : ymr, m2 = s ? ypi : -ymi;   // Ym = m1 + i m2
                 const double o3 = so * o1, o4 = so * o2, m3 = -so * m1, m4 = -so * m2;
 #pragma unroll
                 for (int i = 0; i < BPL; ++i) {
