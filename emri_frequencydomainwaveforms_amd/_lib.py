@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum",
     "efd_modesum_status",
     "efd_modesum_contributions",
+    "efd_modesum_stats",
     "efd_polarizations",
     "efd_loglike",
     "efd_inner_product",
@@ -101,6 +102,9 @@ def load(path=None):
     lib.efd_modesum_status.argtypes = [vp, vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int
     lib.efd_modesum_contributions.argtypes = [vp, ctypes.POINTER(i64), vp]
+    lib.efd_modesum_stats.restype = ctypes.c_int
+    lib.efd_modesum_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                      ctypes.POINTER(i32), vp]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int

@@ -59,9 +59,15 @@ constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
-constexpr int KEYCAP = TILE >= 256 ? 2048 : 1024;  // record keys per tile pass held in LDS
-constexpr int SEGWIN = 4 * TILE;    // segments examined per window when building a tile list
-constexpr int NC = TILE / 8;        // interval records per LDS stage (two 16-B pieces/thread)
+#ifndef EFD_KEYCAP
+#define EFD_KEYCAP (EFD_TILE >= 256 ? 2048 : 1024)
+#endif
+#ifndef EFD_SEGWIN_F
+#define EFD_SEGWIN_F 4
+#endif
+constexpr int KEYCAP = EFD_KEYCAP;  // record keys per tile pass held in LDS
+constexpr int SEGWIN = EFD_SEGWIN_F * TILE;  // segments examined per window (tile list build)
+constexpr int MAX_K = 8192;         // harmonics per call (k_group sorts them in LDS)
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
@@ -85,35 +91,42 @@ int fail(int code, const std::string& msg) {
 // Data layouts in HBM
 // ----------------------------------------------------------------------------------------
 
-// One record per (harmonic h, forward knot interval j): everything the SPA needs on the
-// bins whose t(g) falls in [t_j, t_{j+1}). 256 B, staged through LDS by k_modesum.
+// One record per ((m, n) group g, forward knot interval j): everything the SPA needs on the
+// bins whose t(g) falls in [t_j, t_{j+1}). All harmonics (l, m, n) of one (m, n) share F, Phi,
+// t(f), F', F'', sin/cos and the K_{1/3} factor; only A_lmn Y differs, and the not-a-knot spline
+// is linear in its data, so the group carries the two combined amplitude splines
+//   Bp(t) = sum_l y0_l A_l(t),  Bm(t) = sum_l y1_l A_l(t)   (y0 = -scale Y+, y1 = conj(-scale Y-))
+// and one SPA evaluation serves every l. 288 B (18 pieces of 16 B), staged through LDS.
 struct __attribute__((aligned(16))) Item {
     double gx;        // left end of the inverse-spline interval (ascending F)
     double ic[4];     // t(g) = ((ic0 u + ic1) u + ic2) u + ic3, u = g - gx
     double tj, tj1;   // forward interval
-    double ar[4];     // Re A(t), w = t - tj (c0 highest power, scipy PPoly order)
-    double ai[4];     // Im A(t)
-    double ph[4];     // Phi_k(t) = m Phi_phi + n Phi_r
+    double ph[4];     // Phi_mn(t) = m Phi_phi + n Phi_r, w = t - tj (scipy PPoly order)
     double fd[3];     // F'(t)
     double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
-    double y[2][2];   // y[0] = -scale * Y+ (parent, f = -g); y[1] = conj(-scale * Y-) (partner,
-                      // f = +g; conjugated so that sub-branch s reads its own factor as y[s])
+    double b[2][2][4];  // b[0] = Bp (re, im cubics), b[1] = Bm: sub-branch s reads b[s] for its
+                        // own bin and b[1-s] for the mirror
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
-    int32_t flags;    // bit0: interval part of a run; bit1: has partner (m != 0)
-    int32_t h;
+    int32_t pad[2];
 };
-static_assert(sizeof(Item) == 256, "Item must be 256 B");
+static_assert(sizeof(Item) == 288, "Item must be 288 B");
+constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
+constexpr int NC = (2 * TILE) / PIECES;         // records per LDS stage (two pieces per thread)
 
 struct Header {
-    int64_t contributions;      // C of the last call (k_items)
+    int64_t contributions;      // C of the last call: (l, m, n) branch x bin pairs (k_items)
+    int64_t evaluations;        // SPA evaluations: (m, n) group branch x bin pairs
     int32_t runs_overflow;      // set by k_prep when a harmonic has > MAXRUNS monotonic runs
+    int32_t groups;             // G: distinct (m, n) of the call (k_group)
+    int32_t bad_mn;             // set by k_group when |m| > 255 or |n| > 1023
     int32_t pad0;
-    int64_t pad[6];             // 64 B
+    int64_t pad[4];             // 64 B
 };
+static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
-        seginfo, nseg, slotlh, slotinfo, slotcnt, total;
+        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, total;
     int64_t ntiles, nlanes;
 };
 
@@ -127,7 +140,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
     L.header = take(sizeof(Header));
-    L.coefA = take(sizeof(double) * ni * 4 * 2 * K);
+    L.coefA = take(sizeof(double) * ni * 4 * 4 * K);   // [ni][4][4K]: Bp re/im, Bm re/im
     L.coefT = take(sizeof(double) * ni * 4 * 8);
     L.kslope = take(sizeof(double) * nt * 2);
     L.tscratch = take(sizeof(double) * nt * 16);
@@ -142,6 +155,10 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.slotlh = take(sizeof(int2) * 2 * MAXRUNS * K);
     L.slotinfo = take(sizeof(int4) * 2 * MAXRUNS * K);
     L.slotcnt = take(sizeof(int32_t) * ((2 * MAXRUNS * K + 255) / 256));
+    L.gm = take(sizeof(int32_t) * K);
+    L.gn = take(sizeof(int32_t) * K);
+    L.gstart = take(sizeof(int32_t) * (K + 1));
+    L.gmem = take(sizeof(int32_t) * K);
     L.total = off;
     return L;
 }
@@ -254,6 +271,78 @@ __device__ __forceinline__ double dcubic(const double* c, double w) {
 }
 
 // ----------------------------------------------------------------------------------------
+// K0: (m, n) groups. One workgroup sorts the K harmonics by (m, n, h) in LDS (bitonic, 64-bit
+// keys) and writes the groups in (m, n) order with their members in ascending h:
+//   gm[g], gn[g]; members gmem[gstart[g] .. gstart[g+1]); G = hdr->groups.
+// The order is a function of (m, n) alone, so everything downstream is deterministic.
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ marr,
+                                                const int32_t* __restrict__ narr, int K,
+                                                int32_t* __restrict__ gm, int32_t* __restrict__ gn,
+                                                int32_t* __restrict__ gstart,
+                                                int32_t* __restrict__ gmem,
+                                                Header* __restrict__ hdr) {
+    __shared__ unsigned long long key[MAX_K];
+    __shared__ int part[1024];
+    const int tid = threadIdx.x;
+    int P = 1;
+    while (P < K) P <<= 1;
+    for (int i = tid; i < P; i += 1024) {
+        unsigned long long k = ~0ull;
+        if (i < K) {
+            const int m = marr[i], n = narr[i];
+            if (m < -256 || m > 255 || n < -1024 || n > 1023) atomicOr(&hdr->bad_mn, 1);
+            const unsigned gk = ((unsigned)(m + 256) & 511u) << 11 | ((unsigned)(n + 1024) & 2047u);
+            k = ((unsigned long long)gk << 32) | (unsigned)i;
+        }
+        key[i] = k;
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < P / 2; t += 1024) {
+                const int lo = 2 * t - (t & (stride - 1));   // index with bit `stride` clear
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long a = key[lo], b = key[hi];
+                if ((a > b) == up) { key[lo] = b; key[hi] = a; }
+            }
+            __syncthreads();
+        }
+    }
+    // group starts: position p starts a group if its (m, n) differs from p - 1; exclusive scan
+    // of the start flags over per-thread blocks of consecutive positions
+    const int per = (K + 1023) / 1024;
+    const int p0 = min(K, tid * per), p1 = min(K, p0 + per);
+    int mine = 0;
+    for (int p = p0; p < p1; ++p) mine += (p == 0 || (key[p] >> 32) != (key[p - 1] >> 32));
+    part[tid] = mine;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int g = part[tid] - mine;   // groups started before p0
+    for (int p = p0; p < p1; ++p) {
+        const unsigned long long k = key[p];
+        gmem[p] = (int32_t)(unsigned)(k & 0xffffffffu);
+        if (p == 0 || (k >> 32) != (key[p - 1] >> 32)) {
+            const unsigned gk = (unsigned)(k >> 32);
+            gm[g] = (int32_t)(gk >> 11) - 256;
+            gn[g] = (int32_t)(gk & 2047u) - 1024;
+            gstart[g] = p;
+            ++g;
+        }
+    }
+    if (tid == 1023) {
+        gstart[part[1023]] = K;
+        hdr->groups = part[1023];
+    }
+}
+
+// ----------------------------------------------------------------------------------------
 // K1: trajectory splines (one wave; lanes 0..3 the knot data, then lanes 4..5 the slopes)
 // coefT layout: [interval][coef c][q], q: 0 Phi_phi, 1 Phi_r, 2 f_phi, 3 f_r, 4 f_phi', 5 f_r'
 // ----------------------------------------------------------------------------------------
@@ -310,11 +399,15 @@ __device__ void traj_splines(const double* __restrict__ t, const double* __restr
 }
 
 // ----------------------------------------------------------------------------------------
-// K2: shared-knot splines of the amplitudes, one lane per interpolant (Re/Im of each harmonic).
-// y is knot-major [n][ninterp] (FEW's teuk_modes[N_t][K] complex layout), coef [n-1][4][ninterp].
+// K2: shared-knot splines, one lane per interpolant q < count; knot values YF(i, q); coef is
+// [n-1][4][stride] (stride >= count). For the mode sum the interpolants are the four real parts
+// of the group amplitudes (Bp re, Bp im, Bm re, Bm im of group q/4), summed over the group's
+// harmonics as they are read (FEW's teuk_modes[N_t][K] complex layout underneath).
 // ----------------------------------------------------------------------------------------
-__device__ void spline_shared(const double* __restrict__ x, int n, const double* __restrict__ y,
-                              int ninterp, double* coef, int64_t scratch_stride, int block) {
+template <class YF>
+__device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int count, int stride,
+                              double* coef, int64_t scratch_stride, int block) {
+    const int ninterp = stride;
     // The not-a-knot matrix depends only on the shared knots: one thread factors it into LDS
     // (cp_i, 1/m_i, a_i of the Thomas sweep), then every lane runs the two division-free
     // recurrences for its right-hand side. DP(i) lives in the c1 slot of interval i of the
@@ -342,8 +435,8 @@ __device__ void spline_shared(const double* __restrict__ x, int n, const double*
     }
     __syncthreads();
     const int q = block * blockDim.x + threadIdx.x;
-    if (q >= ninterp) return;
-    auto Y = [&](int i) { return y[(size_t)i * ninterp + q]; };
+    if (q >= count) return;
+    auto Y = [&](int i) { return yf(i, q); };
     auto OUT = [&](int i, int c, double v) { coef[((size_t)i * 4 + c) * ninterp + q] = v; };
     if (n < 4) {
         double* cpbuf = coef;
@@ -429,7 +522,7 @@ __device__ void spline_shared(const double* __restrict__ x, int n, const double*
 }
 
 // ----------------------------------------------------------------------------------------
-// K3: inverse splines t(F) per monotonic run, one lane per harmonic
+// K3: inverse splines t(F) per monotonic run, one lane per (m, n) group h
 // runs[h][r] = (ja, jb, sign, 0): forward intervals [ja, jb), F increasing (+1)/decreasing (-1)
 // Item.gx / Item.ic are filled for the intervals of each run.
 // ----------------------------------------------------------------------------------------
@@ -441,7 +534,7 @@ __device__ __forceinline__ double knotF(const double* f_phi, const double* f_r, 
 
 __device__ void inverse_splines(const double* __restrict__ t, const double* __restrict__ f_phi,
                                   const double* __restrict__ f_r, const int32_t* __restrict__ marr,
-                                  const int32_t* __restrict__ narr, int nt, int K,
+                                  const int32_t* __restrict__ narr, int nt, int K, int G,
                                   int32_t* __restrict__ runs, Item* __restrict__ items,
                                   double* __restrict__ cpbuf, double* __restrict__ dpbuf,
                                   int32_t* __restrict__ err, int block) {
@@ -455,8 +548,8 @@ __device__ void inverse_splines(const double* __restrict__ t, const double* __re
         frs[i] = f_r[i];
     }
     __syncthreads();
-    const int h = block * blockDim.x + threadIdx.x;
-    if (h >= K) return;
+    const int h = block * blockDim.x + threadIdx.x;   // (m, n) group
+    if (h >= G) return;
     const int m = marr[h], n = narr[h];
     const int ni = nt - 1;
     Item* it = items + (size_t)h * ni;
@@ -515,11 +608,14 @@ __device__ void inverse_splines(const double* __restrict__ t, const double* __re
 __global__ __launch_bounds__(64) void k_prep(
     const double* __restrict__ t, const double* __restrict__ phi_phi,
     const double* __restrict__ phi_r, const double* __restrict__ f_phi,
-    const double* __restrict__ f_r, const double* __restrict__ amp, const int32_t* __restrict__ m,
-    const int32_t* __restrict__ n, int nt, int K, int nb_amp, double* __restrict__ coefT,
-    double* __restrict__ kslope, double* __restrict__ tscratch, double* coefA,
-    int32_t* __restrict__ runs, Item* __restrict__ items, double* __restrict__ invcp,
-    double* __restrict__ invdp, int32_t* __restrict__ err) {
+    const double* __restrict__ f_r, const double* __restrict__ amp,
+    const double* __restrict__ ylm_p, const double* __restrict__ ylm_m, double sc_re,
+    double sc_im, const int32_t* __restrict__ gm, const int32_t* __restrict__ gn,
+    const int32_t* __restrict__ gstart, const int32_t* __restrict__ gmem, int nt, int K,
+    int nb_amp, double* __restrict__ coefT, double* __restrict__ kslope,
+    double* __restrict__ tscratch, double* coefA, int32_t* __restrict__ runs,
+    Item* __restrict__ items, double* __restrict__ invcp, double* __restrict__ invdp,
+    Header* __restrict__ hdr) {
     const int b = blockIdx.x;
 #ifdef EFD_EXP_PREP_ROLE
     {
@@ -530,16 +626,43 @@ __global__ __launch_bounds__(64) void k_prep(
     if (b == 0) {
         traj_splines(t, phi_phi, phi_r, f_phi, f_r, nt, coefT, kslope, tscratch);
     } else if (b < 1 + nb_amp) {
-        spline_shared(t, nt, amp, 2 * K, coefA, (int64_t)4 * 2 * K, b - 1);
+        const int G = hdr->groups;
+        // y0 = -scale Y+, y1 = conj(-scale Y-) (partner only for m != 0): S = -h_nb(-f) scale
+        auto yf = [&](int i, int q) {
+            const int g = q >> 2, comp = q & 3;
+            const int pa = gstart[g], pb = gstart[g + 1];
+            const bool partner = gm[g] != 0;
+            double acc = 0.0;
+            for (int p = pa; p < pb; ++p) {
+                const int h = gmem[p];
+                const double Ar = amp[((size_t)i * K + h) * 2], Ai = amp[((size_t)i * K + h) * 2 + 1];
+                double yr, yi;
+                if (comp < 2) {
+                    const double vr = ylm_p[2 * h], vi = ylm_p[2 * h + 1];
+                    yr = -(sc_re * vr - sc_im * vi);
+                    yi = -(sc_re * vi + sc_im * vr);
+                } else {
+                    const double vr = partner ? ylm_m[2 * h] : 0.0;
+                    const double vi = partner ? ylm_m[2 * h + 1] : 0.0;
+                    yr = -(sc_re * vr - sc_im * vi);
+                    yi = (sc_re * vi + sc_im * vr);
+                }
+                acc += (comp & 1) ? (Ar * yi + Ai * yr) : (Ar * yr - Ai * yi);
+            }
+            return acc;
+        };
+        spline_shared(t, nt, yf, 4 * G, 4 * K, coefA, (int64_t)4 * 4 * K, b - 1);
     } else {
-        inverse_splines(t, f_phi, f_r, m, n, nt, K, runs, items, invcp, invdp, err, b - 1 - nb_amp);
+        inverse_splines(t, f_phi, f_r, gm, gn, nt, K, hdr->groups, runs, items, invcp, invdp,
+                        &hdr->runs_overflow, b - 1 - nb_amp);
     }
 }
 
 __global__ __launch_bounds__(64) void k_spline_shared(const double* __restrict__ x, int n,
                                                       const double* __restrict__ y, int ninterp,
                                                       double* coef, int64_t scratch_stride) {
-    spline_shared(x, n, y, ninterp, coef, scratch_stride, blockIdx.x);
+    auto yf = [&](int i, int q) { return y[(size_t)i * ninterp + q]; };
+    spline_shared(x, n, yf, ninterp, ninterp, coef, scratch_stride, blockIdx.x);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -586,73 +709,85 @@ __device__ int64_t grid_bound(const double* __restrict__ f, int64_t nf, double v
     return lo;
 }
 
-__device__ unsigned long long build_item(
+__device__ void build_item(
     const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
-    const int32_t* __restrict__ marr, const int32_t* __restrict__ narr,
-    const double* __restrict__ ylm_p, const double* __restrict__ ylm_m, int ni, int K,
+    const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int ni, int K,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
-    int64_t nl, int64_t nl1, double sc_re, double sc_im, Item* __restrict__ items,
-    int4* __restrict__ ranges, int h, int j);
+    int64_t nl, int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges, int h, int j,
+    unsigned long long& evals);
 
+// K4: one thread per (group g, knot interval j). Counts both the SPA evaluations the kernel
+// makes (per group) and the reference formulation's contributions C (per (l, m, n) harmonic:
+// the group's evaluations times its member count).
 __global__ void k_items(const double* __restrict__ t, const double* __restrict__ f_phi,
-                        const double* __restrict__ f_r, const int32_t* __restrict__ marr,
-                        const int32_t* __restrict__ narr, const double* __restrict__ ylm_p,
-                        const double* __restrict__ ylm_m, int nt, int K,
-                        const double* __restrict__ coefA, const double* __restrict__ coefT,
-                        const int32_t* __restrict__ runs, const double* __restrict__ freq,
-                        int64_t nf, int paired, int64_t nl, int64_t nl1, double sc_re,
-                        double sc_im, Item* __restrict__ items, int4* __restrict__ ranges,
+                        const double* __restrict__ f_r, const int32_t* __restrict__ gm,
+                        const int32_t* __restrict__ gn, const int32_t* __restrict__ gstart,
+                        int nt, int K, const double* __restrict__ coefA,
+                        const double* __restrict__ coefT, const int32_t* __restrict__ runs,
+                        const double* __restrict__ freq, int64_t nf, int paired, int64_t nl,
+                        int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges,
                         Header* __restrict__ hdr) {
     const int ni = nt - 1;
+    const int G = hdr->groups;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    __shared__ unsigned long long red[4];
-    unsigned long long contrib = 0;
-    if (gid < (int64_t)ni * K) contrib = build_item(t, f_phi, f_r, marr, narr, ylm_p, ylm_m, ni, K,
-                                                     coefA, coefT, runs, freq, nf, paired, nl,
-                                                     nl1, sc_re, sc_im, items, ranges,
-                                                     (int)(gid % K), (int)(gid / K));
-    for (int o = 32; o > 0; o >>= 1) contrib += __shfl_xor(contrib, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = contrib;
+    __shared__ unsigned long long red[2][4];
+    unsigned long long ev = 0, contrib = 0;
+    if (gid < (int64_t)ni * G) {
+        const int g = (int)(gid % G), j = (int)(gid / G);
+        build_item(t, f_phi, f_r, gm, gn, ni, K, coefA, coefT, runs, freq, nf, paired, nl, nl1,
+                   items, ranges, g, j, ev);
+        contrib = ev * (unsigned long long)(gstart[g + 1] - gstart[g]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        ev += __shfl_xor(ev, o);
+        contrib += __shfl_xor(contrib, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = contrib;
+        red[1][threadIdx.x >> 6] = ev;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long v = red[0] + red[1] + red[2] + red[3];
-        if (v) atomicAdd((unsigned long long*)&hdr->contributions, v);
+        const unsigned long long c = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        const unsigned long long e = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        if (c) atomicAdd((unsigned long long*)&hdr->contributions, c);
+        if (e) atomicAdd((unsigned long long*)&hdr->evaluations, e);
     }
 }
 
-// One interval record; returns its contribution count and bumps the per-tile counters.
-__device__ unsigned long long build_item(
+// One interval record of group h; `evals` = its (branch x bin) evaluation count.
+__device__ void build_item(
     const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
-    const int32_t* __restrict__ marr, const int32_t* __restrict__ narr,
-    const double* __restrict__ ylm_p, const double* __restrict__ ylm_m, int ni, int K,
+    const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int ni, int K,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
-    int64_t nl, int64_t nl1, double sc_re, double sc_im, Item* __restrict__ items,
-    int4* __restrict__ ranges, int h, int j) {
+    int64_t nl, int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges, int h, int j,
+    unsigned long long& evals) {
     Item& it = items[(size_t)h * ni + j];
-    const int m = marr[h], n = narr[h];
+    const int m = gm[h], n = gn[h];
     const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
     int run = -1;
     for (int r = 0; r < MAXRUNS; ++r) {
         if (rr[4 * r + 2] != 0 && j >= rr[4 * r] && j < rr[4 * r + 1]) { run = r; break; }
     }
     const int partner = (m != 0) ? 1 : 0;
-    it.h = h;
+    evals = 0;
     if (run < 0) {  // flat interval (F_{j+1} == F_j): no support; place empty ranges at 0
-        it.flags = 0;
         it.klo[0] = it.khi[0] = it.klo[1] = it.khi[1] = 0;
         ranges[(size_t)h * ni + j] = make_int4(0, 0, 0, 0);
-        return 0;
+        return;
     }
     const int a = rr[4 * run], sg = rr[4 * run + 2];
-    it.flags = 1 | (partner << 1);
     it.tj = t[j];
     it.tj1 = t[j + 1];
     const double dm = (double)m, dn = (double)n;
     for (int c = 0; c < 4; ++c) {
-        it.ar[c] = coefA[((size_t)j * 4 + c) * 2 * K + 2 * h];
-        it.ai[c] = coefA[((size_t)j * 4 + c) * 2 * K + 2 * h + 1];
+        const double* ca = coefA + ((size_t)j * 4 + c) * 4 * K + 4 * h;
+        it.b[0][0][c] = ca[0];   // Bp re
+        it.b[0][1][c] = ca[1];   // Bp im
+        it.b[1][0][c] = ca[2];   // Bm re
+        it.b[1][1][c] = ca[3];   // Bm im
         const double* ct = coefT + ((size_t)j * 4 + c) * 8;
         it.ph[c] = dm * ct[0] + dn * ct[1];
     }
@@ -670,15 +805,6 @@ __device__ unsigned long long build_item(
         it.fdd[0] = SQRT_3_2PI * (3.0 * G0);
         it.fdd[1] = SQRT_3_2PI * (2.0 * G1);
         it.fdd[2] = SQRT_3_2PI * G2;
-    }
-    // S = -h_nb(-f) * scale: fold the minus sign and the complex scale into Y
-    {
-        const double yr = ylm_p[2 * h], yi = ylm_p[2 * h + 1];
-        it.y[0][0] = -(sc_re * yr - sc_im * yi);
-        it.y[0][1] = -(sc_re * yi + sc_im * yr);
-        const double zr = partner ? ylm_m[2 * h] : 0.0, zi = partner ? ylm_m[2 * h + 1] : 0.0;
-        it.y[1][0] = -(sc_re * zr - sc_im * zi);
-        it.y[1][1] = (sc_re * zi + sc_im * zr);   // conjugate of -scale * Y-
     }
     // g-interval of this record: [x_lo, x_hi), lower end open at the run's first knot
     const double Fj = knotF(f_phi, f_r, m, n, j), Fj1 = knotF(f_phi, f_r, m, n, j + 1);
@@ -709,13 +835,13 @@ __device__ unsigned long long build_item(
     it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
     it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
     ranges[(size_t)h * ni + j] = make_int4((int)lo0, (int)hi0, (int)lo1, (int)hi1);
-    // contributions C (harmonic branch x bin evaluations) for the roofline
+    // branch x bin evaluations (on a paired grid one lane serves both the branch and its partner)
     const int mult = paired ? 1 + partner : 1;
-    return (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
+    evals = (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
 }
 
 // ----------------------------------------------------------------------------------------
-// K5: segment table. A segment is (harmonic, monotonic run, sub-branch s) with a non-empty lane
+// K5: segment table. A segment is (group, monotonic run, sub-branch s) with a non-empty lane
 // range; its interval records are consecutive (h * ni + j, j in [ja, jb)) and, walked in lane
 // order (j += dir), cover consecutive, disjoint lane ranges. K5a: one thread per (h, run, s)
 // slot writes the slot's segment (or an empty marker) into a dense table plus a per-block count;
@@ -726,6 +852,7 @@ __device__ unsigned long long build_item(
 __global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict__ runs,
                                                        const int4* __restrict__ ranges, int nt,
                                                        int K, int lim0, int lim1,
+                                                       const Header* __restrict__ hdr,
                                                        int2* __restrict__ slot_lh,
                                                        int4* __restrict__ slot_info,
                                                        int32_t* __restrict__ blockcnt) {
@@ -733,12 +860,13 @@ __global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict
     __shared__ int wc[4];
     bool valid = false;
     if (i < K * MAXRUNS * 2) {
+        const int G = hdr->groups;
         const int h = i / (2 * MAXRUNS), r = (i >> 1) % MAXRUNS, sb = i & 1;
         const int ni = nt - 1;
         int2 lh = make_int2(0, 0);
         int4 info = make_int4(0, 0, 0, 0);
         const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS + 4 * r;
-        if (rr[2] != 0) {
+        if (h < G && rr[2] != 0) {
             const int ja = rr[0], jb = rr[1], n = jb - ja;
             const int dir = (sb == 0) ? -rr[2] : rr[2];   // s = 0 walks g downward in lane order
             const int lim = sb ? lim1 : lim0;
@@ -908,7 +1036,27 @@ __constant__ double KC[20] = {
     1.9570621786581614e+22, -4.854832179436167e+24, 1.3621079545263217e+27,
     -4.2915604492858035e+29, 1.5087738952527293e+32};
 
-// (R + i I) for |y| < 555: asymptotic with up to 40 terms down to |y| = 18.4, below that the
+// Fast-path series length: FAST_J terms of each of R and I/w, exact (truncation < 1e-17) for
+// |y| >= FAST_Y (kfactor_slow's bands: J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48).
+#ifndef EFD_FAST_J
+#define EFD_FAST_J 4
+#endif
+constexpr int FAST_J = EFD_FAST_J;
+constexpr double FAST_Y = FAST_J <= 3 ? 555.0 : FAST_J == 4 ? 153.0 : FAST_J == 5 ? 75.0 : 48.0;
+static_assert(FAST_J >= 3 && FAST_J <= 6, "fast-path series: 3..6 terms");
+__device__ __forceinline__ void kseries_fast(double ww, double& R, double& I) {
+    const double uu = ww * ww;
+    double r = KB[FAST_J - 1], im = KC[FAST_J - 1];
+#pragma unroll
+    for (int j = FAST_J - 2; j >= 0; --j) {
+        r = fma(r, uu, KB[j]);
+        im = fma(im, uu, KC[j]);
+    }
+    R = r;
+    I = ww * im;
+}
+
+// (R + i I) for |y| < FAST_Y: asymptotic with up to 40 terms down to |y| = 18.4, below that the
 // ascending series K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3}) divided by Q_spa.
 __device__ __noinline__ void kfactor_slow(double fd, double fdd, double& R, double& I) {
     const double y = TWO_PI * fd * fd * fd / (3.0 * fdd * fdd);
@@ -964,10 +1112,11 @@ __device__ __noinline__ void kfactor_slow(double fd, double fdd, double& R, doub
     I = (qi * sr - qr * si) * afd;
 }
 
-// Generic (slow-path) evaluation of the harmonic's forward splines at t when t(g) overshoots
-// the record's interval: search the knot and gather the cubic pieces directly.
+// Generic (slow-path) evaluation of group h's forward splines at t when t(g) overshoots the
+// record's interval: search the knot and gather the cubic pieces directly.
 struct FwdEval {
-    double ar, ai, ph, fd, fdd;
+    double b[4];   // Bp re, Bp im, Bm re, Bm im
+    double ph, fd, fdd;
 };
 __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restrict__ t, int nt,
                                                 int h, int K, int m, int n,
@@ -988,12 +1137,11 @@ __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restr
     auto cub = [&](double c0, double c1, double c2, double c3) {
         return fma(fma(fma(c0, w, c1), w, c2), w, c3);
     };
-    const double* ca = coefA + (size_t)j * 4 * 2 * K + 2 * h;
+    const double* ca = coefA + (size_t)j * 4 * 4 * K + 4 * h;
     const double* ct = coefT + (size_t)j * 32;
     const double dm = (double)m, dn = (double)n;
     FwdEval e;
-    e.ar = cub(ca[0], ca[2 * K], ca[4 * K], ca[6 * K]);
-    e.ai = cub(ca[1], ca[2 * K + 1], ca[4 * K + 1], ca[6 * K + 1]);
+    for (int q = 0; q < 4; ++q) e.b[q] = cub(ca[q], ca[4 * K + q], ca[8 * K + q], ca[12 * K + q]);
     e.ph = cub(dm * ct[0] + dn * ct[1], dm * ct[8] + dn * ct[9], dm * ct[16] + dn * ct[17],
                dm * ct[24] + dn * ct[25]);
     const double F0 = dm * ct[2] + dn * ct[3], F1 = dm * ct[10] + dn * ct[11],
@@ -1007,99 +1155,138 @@ __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restr
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Branch-free SPA evaluation of interval record `it` at g on the fast path: returns
-// zc = A Q e^{i(2 pi g t - Phi)} (the mirror-convention term before Y and scale; see the
-// Q-factor notes above) for lanes with `act` set. need_general is set for active lanes that
-// the general path must redo (t(g) overshot the record's knot interval, F' = 0, or |y| < 555 in
-// the uniform mode); zc is 0 for those and for inactive lanes. Everything is computed
-// unconditionally and masked once at the end (selects, no divergent branches). A wider fast
-// path (a wave-uniform 40-term branch for 18.4 <= |y| < 555) cut general-path calls 5x but
-// cost 4% overall through the hot loop's code generation, so it is not used: the general path
-// runs for ~1.5% of (record, wave) evaluations.
-template <int CAUSTIC>
-__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double gs, double fk,
-                                         double tfk, bool act, const double2* __restrict__ sct,
-                                         double& zr, double& zi, bool& need_general) {
-    // g = gs * fk (gs = +-1, fk the lane's bin frequency, tfk = 2 pi fk)
-    const double u = fma(gs, fk, -it->gx);
+__device__ __forceinline__ double cubic(const double* __restrict__ c, double w) {
+    return fma(fma(fma(c[0], w, c[1]), w, c[2]), w, c[3]);
+}
+
+// Branch-free SPA evaluation of interval record `it` on sub-branch S (g = -f for S = 0, +f for
+// S = 1) at the lane's bin: returns the group-independent factor
+//   W = Q e^{i(2 pi g t - Phi)}   (Q-factor notes above; arg Q_spa folded into the phase)
+// and w = t - t_j for the amplitude cubics, for lanes with `act` set. need_general is set for
+// active lanes the general path must redo (t(g) overshot the record's knot interval, F' = 0, or
+// |y| < FAST_Y in the uniform mode); W is 0 for those and for inactive lanes. Everything is
+// computed unconditionally and masked once (selects, no divergent branches).
+template <int S, int CAUSTIC>
+__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk, double tfk,
+                                         bool act, const double2* __restrict__ sct, double& wr,
+                                         double& wi, double& w, bool& need_general) {
+    // g = +-fk (tfk = 2 pi fk): the sign is a source modifier, free
+    const double u = (S ? fk : -fk) - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
-    const double w = tt - it->tj;
+    w = tt - it->tj;
     bool good = (tt >= it->tj) & (tt < it->tj1);
-    double ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
-    double ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
     const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
     good = good & (afd > 0.0);
     const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
     // psi = 2 pi g t - Phi + sgn(F') 3 pi/4; the 3 pi/4 (192 table steps) goes in as an index
-    const double psi0 = fma(gs * tfk, tt, -ph);
+    const double psi0 = fma(S ? tfk : -tfk, tt, -ph);
     const int shift = fd > 0.0 ? 192 : -192;
+    double R = 1.0, I = 0.0;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
         // w = 3 F''^2 / (2 pi F'^3) = (fdd_scaled * |F'|^-3/2)^2 with the sign of F'
         const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
         const double a3 = amp * amp * amp;
         const double t3 = fdds * a3;
         const double ww = copysign(t3 * t3, fd);
-        good = good & (fabs(ww) * 555.0 <= 1.0);
-        const double uu = ww * ww;
-        const double R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
-        const double I = ww * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
-        const double nr = ar * R - ai * I;
-        ai = ar * I + ai * R;
-        ar = nr;
+        good = good & (fabs(ww) * FAST_Y <= 1.0);
+        kseries_fast(ww, R, I);
     }
+    // W = 0 unless this lane finishes here (the general path adds the others' terms)
+    const double a = (act & good) ? amp : 0.0;
+    R *= a;
+    I *= a;
     double sn, cs;
     sincos_tab(psi0, shift, sct, sn, cs);
-    const double a = (act & good) ? amp : 0.0;
-    zr = a * (ar * cs - ai * sn);
-    zi = a * (ar * sn + ai * cs);
+    wr = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, cs, -I * sn) : R * cs;
+    wi = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, sn, I * cs) : R * sn;
     need_general = act & !good;
 }
 
+#ifdef EFD_EXP_COUNT
+// record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
+// FAST_Y, |y| < 18.4
+__device__ unsigned long long g_exp_count[16];  // [8..15]: |y| bands of kfactor_slow's J
+#endif
+
 // General (cold) path: scipy interval selection for t(g) and the full K_{1/3} evaluation.
+// Returns W and both group amplitudes at t(g).
+struct ColdEval {
+    double wr, wi, b[4];
+};
 template <int CAUSTIC>
-__device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double g,
-                                            const double* __restrict__ t, int nt, int h, int K,
-                                            int m, int n, const double* __restrict__ coefA,
-                                            const double* __restrict__ coefT) {
+__device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double g, int h,
+                                             const double* __restrict__ t, int nt, int K,
+                                             const int32_t* __restrict__ gm,
+                                             const int32_t* __restrict__ gn,
+                                             const double* __restrict__ coefA,
+                                             const double* __restrict__ coefT) {
     const double u = g - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
-    double ar, ai, ph, fd, fdd;
+    double ph, fd, fdd;
+    ColdEval c;
     if (tt >= it->tj && tt < it->tj1) {
         const double w = tt - it->tj;
-        ar = fma(fma(fma(it->ar[0], w, it->ar[1]), w, it->ar[2]), w, it->ar[3]);
-        ai = fma(fma(fma(it->ai[0], w, it->ai[1]), w, it->ai[2]), w, it->ai[3]);
+        for (int q = 0; q < 4; ++q) c.b[q] = cubic(it->b[q >> 1][q & 1], w);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
         fdd = INV_SQRT_3_2PI * fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
     } else {  // t(g) overshot the record's knot interval: evaluate like scipy
-        const FwdEval fe = forward_generic(tt, t, nt, h, K, m, n, coefA, coefT);
-        ar = fe.ar; ai = fe.ai; ph = fe.ph; fd = fe.fd; fdd = fe.fdd;
+#ifdef EFD_EXP_COUNT
+        atomicAdd(&g_exp_count[4], 1ull);
+#endif
+        const FwdEval fe = forward_generic(tt, t, nt, h, K, gm[h], gn[h], coefA, coefT);
+        for (int q = 0; q < 4; ++q) c.b[q] = fe.b[q];
+        ph = fe.ph; fd = fe.fd; fdd = fe.fdd;
     }
     const double amp = fd != 0.0 ? rsqrt(fabs(fd)) : 0.0;
     const double psi = fma(TWO_PI * g, tt, -ph) + (fd > 0.0 ? 0.75 * PI : -0.75 * PI);
+    double R = 1.0, I = 0.0;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM && fd != 0.0 && fdd != 0.0) {
         const double a2 = amp * amp;
         const double a6 = a2 * a2 * a2;
         const double ww = (fd > 0.0 ? 1.0 : -1.0) * (3.0 / TWO_PI) * fdd * fdd * a6;
-        double R, I;
-        if (fabs(ww) * 555.0 <= 1.0) {
-            const double uu = ww * ww;
-            R = fma(fma(KB[2], uu, KB[1]), uu, KB[0]);
-            I = ww * fma(fma(KC[2], uu, KC[1]), uu, KC[0]);
+        if (fabs(ww) * FAST_Y <= 1.0) {
+            kseries_fast(ww, R, I);
         } else {
+#ifdef EFD_EXP_COUNT
+            atomicAdd(&g_exp_count[fabs(ww) * 18.4 <= 1.0 ? 5 : 6], 1ull);
+            {
+                const double ay = 1.0 / fabs(ww);
+                const int band = ay >= 153.0 ? 8 : ay >= 75.0 ? 9 : ay >= 48.0 ? 10 : ay >= 29.4 ? 11
+                               : ay >= 23.1 ? 12 : ay >= 20.3 ? 13 : ay >= 18.4 ? 14 : 15;
+                atomicAdd(&g_exp_count[band], 1ull);
+            }
+#endif
             kfactor_slow(fd, fdd, R, I);
         }
-        const double nr = ar * R - ai * I;
-        ai = ar * I + ai * R;
-        ar = nr;
     }
     double sn, cs;
     sincos_big(psi, sn, cs);
-    // returned by value: references into the caller's register arrays would force them into
-    // scratch memory
-    return make_double2(amp * (ar * cs - ai * sn), amp * (ar * sn + ai * cs));
+    c.wr = amp * (R * cs - I * sn);
+    c.wi = amp * (R * sn + I * cs);
+    return c;
+}
+
+// Accumulation of one evaluation into the lane's two bins. X is the own bin's group amplitude
+// (b[S]), Z the mirror's (b[1-S]):
+//   S = 0: own += X W,        mirror += conj(Z W)   (parent at f = -g, partner at the mirror)
+//   S = 1: own += conj(X W),  mirror += Z W
+template <int S, bool PAIRED>
+__device__ __forceinline__ void accumulate(double wr, double wi, double xr, double xi, double zr,
+                                           double zi, double& own_r, double& own_i,
+                                           double& mir_r, double& mir_i) {
+    own_r = fma(xr, wr, own_r);
+    own_r = fma(-xi, wi, own_r);
+    own_i = fma(S ? -xr : xr, wi, own_i);
+    own_i = fma(S ? -xi : xi, wr, own_i);
+    if (PAIRED) {
+        mir_r = fma(zr, wr, mir_r);
+        mir_r = fma(-zi, wi, mir_r);
+        mir_i = fma(S ? zr : -zr, wi, mir_i);
+        mir_i = fma(S ? zi : -zi, wr, mir_i);
+    }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1109,24 +1296,24 @@ __device__ __noinline__ double2 spa_general(const Item* __restrict__ it, double 
 // summation order -> bitwise reproducible), then streamed through a double-buffered LDS stage:
 // the whole workgroup gathers the next NC records with coalesced 16-B loads while the waves
 // evaluate the current NC from LDS (broadcast reads; no dependent global latency in the loop).
-// Each record feeds BPL independent, branch-free evaluations per lane; lanes needing the
-// general path are masked and redone in a cold block.
+// Each record feeds BPL independent, branch-free evaluations per lane (one per (m, n) group:
+// every l of the group at once); lanes needing the general path get W = 0 there and add their
+// term in a cold block. The sub-branch S of a record is wave-uniform: each S has its own copy of
+// the evaluation (compile-time signs and LDS offsets).
 // ----------------------------------------------------------------------------------------
-#ifdef EFD_EXP_COUNT
-__device__ unsigned long long g_exp_count[4];   // record evals, cold-path evals, cold lanes, skips
-#endif
 template <bool PAIRED, int CAUSTIC, int BPL>
-#ifdef EFD_EXP_WAVES_PER_EU
-__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_EXP_WAVES_PER_EU, 8))) void k_modesum(
-#else
-__global__ __launch_bounds__(TILE) void k_modesum(
+// 3 waves per SIMD (<= 168 VGPRs): the LDS footprint allows 3 workgroups per CU anyway, and
+// the compiler's unconstrained choice (180 VGPRs, 2 waves) ran 1.33 ms against 1.12 ms
+#ifndef EFD_WAVES_PER_EU
+#define EFD_WAVES_PER_EU 3
 #endif
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8))) void k_modesum(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
     const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
     const int32_t* __restrict__ nsegp, const double* __restrict__ freq, int64_t nf,
-    int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ marr,
-    const int32_t* __restrict__ narr, const double* __restrict__ t,
-    const double* __restrict__ coefA, const double* __restrict__ coefT, int accumulate,
+    int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,
+    const int32_t* __restrict__ gn, const double* __restrict__ t,
+    const double* __restrict__ coefA, const double* __restrict__ coefT, int accumulate_out,
     double* __restrict__ out) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
@@ -1177,21 +1364,24 @@ __global__ __launch_bounds__(TILE) void k_modesum(
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
 
-    // staging: a record is 16 pieces of 16 B; NC records = 16 NC pieces, two per thread.
+    // staging: a record is PIECES pieces of 16 B; NC records take at most two pieces per thread.
     // (Plain registers, no lambda-captured arrays: those were demoted to scratch memory.)
-    static_assert(16 * NC == 2 * TILE, "staging assumes two 16-B pieces per thread");
+    static_assert(PIECES * NC <= 2 * TILE, "staging assumes at most two 16-B pieces per thread");
     const int pc0 = tid, pc1 = tid + TILE;
+    const int r0 = pc0 / PIECES, q0 = pc0 % PIECES, r1 = pc1 / PIECES, q1 = pc1 % PIECES;
     uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
 #define EFD_FETCH(c)                                                                          \
     do {                                                                                      \
-        const int e0_ = (c) * NC + (pc0 >> 4), e1_ = (c) * NC + (pc1 >> 4);                   \
-        if (e0_ < cnt) pre0 = reinterpret_cast<const uint4*>(items + (keys[e0_] >> 1))[pc0 & 15]; \
-        if (e1_ < cnt) pre1 = reinterpret_cast<const uint4*>(items + (keys[e1_] >> 1))[pc1 & 15]; \
+        const int e0_ = (c) * NC + r0, e1_ = (c) * NC + r1;                                   \
+        if (r0 < NC && e0_ < cnt)                                                             \
+            pre0 = reinterpret_cast<const uint4*>(items + (keys[e0_] >> 1))[q0];              \
+        if (r1 < NC && e1_ < cnt)                                                             \
+            pre1 = reinterpret_cast<const uint4*>(items + (keys[e1_] >> 1))[q1];              \
     } while (0)
 #define EFD_STORE(buf)                                                                        \
     do {                                                                                      \
-        reinterpret_cast<uint4*>(&stage[(buf)][pc0 >> 4])[pc0 & 15] = pre0;                   \
-        reinterpret_cast<uint4*>(&stage[(buf)][pc1 >> 4])[pc1 & 15] = pre1;                   \
+        if (r0 < NC) reinterpret_cast<uint4*>(&stage[(buf)][r0])[q0] = pre0;                  \
+        if (r1 < NC) reinterpret_cast<uint4*>(&stage[(buf)][r1])[q1] = pre1;                  \
     } while (0)
 
     int win = 0;        // next segment window
@@ -1309,7 +1499,7 @@ __global__ __launch_bounds__(TILE) void k_modesum(
             for (int ii = 0; ii < nin; ++ii) {
                 const uint32_t key = rfl(keys[c * NC + ii]);
                 // S = 0: g = -f (parent at the own bin, partner at the mirror); S = 1: g = +f
-                // (partner at the own bin, parent at the mirror). Y- is zero for m = 0 harmonics.
+                // (partner at the own bin, parent at the mirror). Bm is zero for m = 0 groups.
                 const int s = (int)(key & 1);
                 const Item* it = stg + ii;
                 const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
@@ -1323,67 +1513,54 @@ __global__ __launch_bounds__(TILE) void k_modesum(
 #ifdef EFD_EXP_COUNT
                 if (lane == 0) atomicAdd(&g_exp_count[0], 1ull);
 #endif
-                const double gs = s ? 1.0 : -1.0;
                 bool anyneed = false;
                 bool need[BPL];
-                double zr[BPL], zi[BPL];
-#pragma unroll
-                for (int i = 0; i < BPL; ++i) {
-                    const int32_t k = w_lo + 64 * i + lane;
-                    const bool act = (k >= klo) & (k < khi);
-#ifdef EFD_EXP_NOCOMPUTE
-                    zr[i] = act ? fk[i] * it->ar[0] : 0.0; zi[i] = gs * it->ai[1]; need[i] = false;
-#else
-                    spa_fast<CAUSTIC>(it, gs, fk[i], tfk[i], act, sctab, zr[i], zi[i], need[i]);
-#endif
-                    anyneed = anyneed | need[i];
-                }
-#ifdef EFD_EXP_NOSLOW
-                anyneed = false;
-#endif
-                if (__builtin_expect(__any(anyneed), 0)) {     // cold: general path, some lanes
-#ifdef EFD_EXP_COUNT
-                    {
-                        const unsigned long long nl_ = __popcll(__ballot(need[0])) +
-                                                       (BPL > 1 ? __popcll(__ballot(need[BPL - 1])) : 0);
-                        if (lane == 0) { atomicAdd(&g_exp_count[1], 1ull); atomicAdd(&g_exp_count[2], nl_); }
-                    }
-#endif
-                    const Item* git = items + (key >> 1);
-                    const int h = git->h;
+                auto body = [&](auto Sc) {
+                    constexpr int S = decltype(Sc)::value;
+                    const double* xo = &it->b[S][0][0];       // own bin: b[S] (re 0..3, im 4..7)
+                    const double* xm = &it->b[1 - S][0][0];   // mirror: b[1-S]
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
-                        if (need[i]) {
-                            const double2 zg = spa_general<CAUSTIC>(git, gs * fk[i], t, nt, h, K,
-                                                                    marr[h], narr[h], coefA, coefT);
-                            zr[i] = zg.x;
-                            zi[i] = zg.y;
+                        const int32_t k = w_lo + 64 * i + lane;
+                        const bool act = (k >= klo) & (k < khi);
+                        double wr, wi, w;
+                        spa_fast<S, CAUSTIC>(it, fk[i], tfk[i], act, sctab, wr, wi, w, need[i]);
+                        anyneed = anyneed | need[i];
+                        const double xr = cubic(xo, w), xi = cubic(xo + 4, w);
+                        const double zr = PAIRED ? cubic(xm, w) : 0.0;
+                        const double zi = PAIRED ? cubic(xm + 4, w) : 0.0;
+                        accumulate<S, PAIRED>(wr, wi, xr, xi, zr, zi, own_r[i], own_i[i],
+                                              mir_r[i], mir_i[i]);
+                    }
+#ifdef EFD_EXP_NOSLOW
+                    anyneed = false;
+#endif
+                    if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
+#ifdef EFD_EXP_COUNT
+                        {
+                            const unsigned long long nl_ = __popcll(__ballot(need[0])) +
+                                (BPL > 1 ? __popcll(__ballot(need[BPL - 1])) : 0);
+                            if (lane == 0) {
+                                atomicAdd(&g_exp_count[1], 1ull);
+                                atomicAdd(&g_exp_count[2], nl_);
+                            }
+                        }
+#endif
+                        const int hg = (int)((key >> 1) / (uint32_t)ni);   // the record's group
+#pragma unroll
+                        for (int i = 0; i < BPL; ++i) {
+                            if (need[i]) {
+                                const ColdEval ce = spa_general<CAUSTIC>(
+                                    it, S ? fk[i] : -fk[i], hg, t, nt, K, gm, gn, coefA, coefT);
+                                accumulate<S, PAIRED>(ce.wr, ce.wi, ce.b[2 * S], ce.b[2 * S + 1],
+                                                      ce.b[2 - 2 * S], ce.b[3 - 2 * S], own_r[i],
+                                                      own_i[i], mir_r[i], mir_i[i]);
+                            }
                         }
                     }
-                }
-                // own bin: s = 0 -> Y+ z (parent, f = -g); s = 1 -> Y- conj(z) (partner, f = +g)
-                // mirror:  s = 0 -> Y- conj(z);                s = 1 -> Y+ z
-                // With Y- conj(z) = conj(conj(Y-) z) and the record holding (Y+, conj(Y-)) as
-                // y[0], y[1]: own += Yo z with Yo = y[s], mirror += Ym z with Ym = y[1-s], the
-                // imaginary parts signed so = s ? -1 : 1 and -so. The factors come straight
-                // from LDS at an s-dependent offset: four FMAs per accumulator, no selects.
-                const double o1 = it->y[s][0], o2 = it->y[s][1];          // Yo = o1 + i o2
-                const double m1 = it->y[1 - s][0], m2 = it->y[1 - s][1];  // Ym = m1 + i m2
-                const double so = s ? -1.0 : 1.0;
-                const double o3 = so * o1, o4 = so * o2, m3 = -so * m1, m4 = -so * m2;
-#pragma unroll
-                for (int i = 0; i < BPL; ++i) {
-                    own_r[i] = fma(o1, zr[i], own_r[i]);
-                    own_r[i] = fma(-o2, zi[i], own_r[i]);
-                    own_i[i] = fma(o3, zi[i], own_i[i]);
-                    own_i[i] = fma(o4, zr[i], own_i[i]);
-                    if (PAIRED) {
-                        mir_r[i] = fma(m1, zr[i], mir_r[i]);
-                        mir_r[i] = fma(-m2, zi[i], mir_r[i]);
-                        mir_i[i] = fma(m3, zi[i], mir_i[i]);
-                        mir_i[i] = fma(m4, zr[i], mir_i[i]);
-                    }
-                }
+                };
+                if (s == 0) body(std::integral_constant<int, 0>{});
+                else body(std::integral_constant<int, 1>{});
             }
             // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
             // barrier that closed it; the barrier below publishes the new stage for chunk c+1
@@ -1408,12 +1585,12 @@ __global__ __launch_bounds__(TILE) void k_modesum(
                 oi += mir_i[i];
             } else {
                 double2 vm = make_double2(mir_r[i], mir_i[i]);
-                if (accumulate) { const double2 p = o[km]; vm.x += p.x; vm.y += p.y; }
+                if (accumulate_out) { const double2 p = o[km]; vm.x += p.x; vm.y += p.y; }
                 o[km] = vm;
             }
         }
         double2 v = make_double2(orr, oi);
-        if (accumulate) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
+        if (accumulate_out) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
         o[k] = v;
     }
 }
@@ -1533,7 +1710,7 @@ int efd_version(void) { return EFD_VERSION; }
 #ifdef EFD_EXP_COUNT
 int efd_exp_counters(unsigned long long* out) {
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 4));
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 16));
     return EFD_OK;
 }
 #endif
@@ -1557,7 +1734,7 @@ int efd_spline_build(const double* x, int n, const double* y, int ninterp, doubl
 }
 
 size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf) {
-    if (nt < 2 || nt > MAX_NT || K <= 0 || nf <= 0) return 0;
+    if (nt < 2 || nt > MAX_NT || K <= 0 || K > MAX_K || nf <= 0) return 0;
     return make_layout(nt, K, nf, 0).total;  // unpaired has the most tiles
 }
 
@@ -1567,7 +1744,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         !a->n || !a->ylm_p || !a->ylm_m || !a->freq || !a->out)
         return fail(EFD_ERR_ARG, "efd_modesum: NULL array");
     if (a->nt < 2 || a->nt > MAX_NT) return fail(EFD_ERR_ARG, "efd_modesum: nt out of range");
-    if (a->K <= 0) return fail(EFD_ERR_ARG, "efd_modesum: K must be positive");
+    if (a->K <= 0 || a->K > MAX_K) return fail(EFD_ERR_ARG, "efd_modesum: K out of range [1, 8192]");
     if (a->nf <= 0 || a->nf >= (int64_t)INT32_MAX)
         return fail(EFD_ERR_ARG, "efd_modesum: nf out of range");
     if (a->caustic != EFD_CAUSTIC_SPA && a->caustic != EFD_CAUSTIC_UNIFORM)
@@ -1591,6 +1768,10 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     int2* seglh = (int2*)(ws + L.seglh);
     int4* seginfo = (int4*)(ws + L.seginfo);
     int32_t* nseg = (int32_t*)(ws + L.nseg);
+    int32_t* gm = (int32_t*)(ws + L.gm);
+    int32_t* gn = (int32_t*)(ws + L.gn);
+    int32_t* gstart = (int32_t*)(ws + L.gstart);
+    int32_t* gmem = (int32_t*)(ws + L.gmem);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
@@ -1599,14 +1780,20 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
 
     HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
 
-    // K1-K3: trajectory splines, amplitude splines, inverse splines (one fused launch)
+    // K0: (m, n) groups
+    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
+                       hdr);
+    HIP_TRY(hipGetLastError());
+    // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
+    // grids sized for G = K, blocks past the device-side G return at once)
     {
-        const int nb_amp = (2 * K + 63) / 64;
+        const int nb_amp = (4 * K + 63) / 64;
         const int nb_inv = (K + 63) / 64;
         hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp + nb_inv), dim3(64), sizeof(double) * 7 * nt, st,
-                           a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, a->amp, a->m, a->n, nt, K,
+                           a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, a->amp, a->ylm_p,
+                           a->ylm_m, a->scale_re, a->scale_im, gm, gn, gstart, gmem, nt, K,
                            nb_amp, coefT, kslope, (double*)(ws + L.tscratch), coefA, runs, items,
-                           invcp, invdp, &hdr->runs_overflow);
+                           invcp, invdp, hdr);
         HIP_TRY(hipGetLastError());
 #ifdef EFD_EXP_PREP_ROLE
         return EFD_OK;   // timing experiment: the later stages would read partial data
@@ -1618,9 +1805,8 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         const int threads = 256;
         const int64_t blocks = (total + threads - 1) / threads;
         hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(threads), 0, st, a->t, a->f_phi,
-                           a->f_r, a->m, a->n, a->ylm_p, a->ylm_m, nt, K, coefA, coefT, runs,
-                           a->freq, nf, paired, nl, nl1, a->scale_re, a->scale_im, items, ranges,
-                           hdr);
+                           a->f_r, gm, gn, gstart, nt, K, coefA, coefT, runs, a->freq, nf, paired,
+                           nl, nl1, items, ranges, hdr);
         HIP_TRY(hipGetLastError());
     }
     // K5: segment table
@@ -1631,8 +1817,8 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         const int nblk = (nslot + 255) / 256;
         int32_t* blockcnt = (int32_t*)(ws + L.slotcnt);
         hipLaunchKernelGGL(k_segment_slots, dim3(nblk), dim3(256), 0, st, runs, ranges, nt, K,
-                           (int)(paired ? nl : nf), (int)(paired ? nl1 : nf), slot_lh, slot_info,
-                           blockcnt);
+                           (int)(paired ? nl : nf), (int)(paired ? nl1 : nf), hdr, slot_lh,
+                           slot_info, blockcnt);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_segment_compact, dim3(nblk), dim3(256), 0, st, slot_lh, slot_info,
                            blockcnt, nslot, seglh, seginfo, nseg);
@@ -1646,7 +1832,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh, seginfo,  \
-                       nseg, a->freq, nf, nl, L.ntiles, nt, K, a->m, a->n, a->t, coefA, coefT,    \
+                       nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA, coefT,        \
                        acc, a->out)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
@@ -1669,6 +1855,8 @@ int efd_modesum_status(const void* workspace, void* stream) {
     HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
     if (h.runs_overflow != 0)
         return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
+    if (h.bad_mn != 0)
+        return fail(EFD_ERR_ARG, "efd_modesum: |m| > 255 or |n| > 1023");
     return EFD_OK;
 }
 
@@ -1678,6 +1866,18 @@ int efd_modesum_contributions(const void* workspace, int64_t* contributions, voi
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
     *contributions = h.contributions;
+    return EFD_OK;
+}
+
+int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* evaluations,
+                      int32_t* groups, void* stream) {
+    if (!workspace) return fail(EFD_ERR_ARG, "NULL argument");
+    Header h{};
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
+    if (contributions) *contributions = h.contributions;
+    if (evaluations) *evaluations = h.evaluations;
+    if (groups) *groups = h.groups;
     return EFD_OK;
 }
 

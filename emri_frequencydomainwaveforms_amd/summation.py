@@ -141,6 +141,17 @@ class ModeSumEngine:
                    "efd_modesum_contributions", self.lib)
         return int(c.value)
 
+    def stats(self, stream=None):
+        """(contributions C, SPA evaluations, (m, n) groups) of the last launch."""
+        import ctypes
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        c, e, g = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+        _lib.check(self.lib.efd_modesum_stats(self._ws.data_ptr(), ctypes.byref(c),
+                                              ctypes.byref(e), ctypes.byref(g), st),
+                   "efd_modesum_stats", self.lib)
+        return int(c.value), int(e.value), int(g.value)
+
     def run(self, inp, freq, out=None, grid_symmetric=None, scale=1.0 + 0.0j, accumulate=False,
             check=True):
         """Launch on the current stream; with check=True synchronise and surface device errors."""

@@ -72,11 +72,11 @@ typedef struct efd_modesum_args {
     int32_t nt;
     /* harmonics (device) */
     const double* amp;        /* complex [nt][K]: Teukolsky amplitude A_k(t_i) (FEW layout)  */
-    const int32_t* m;         /* [K] m >= 0; m > 0 adds the -m partner branch                */
-    const int32_t* n;         /* [K]                                                          */
+    const int32_t* m;         /* [K] 0 <= m <= 255; m > 0 adds the -m partner branch          */
+    const int32_t* n;         /* [K] |n| <= 1023                                              */
     const double* ylm_p;      /* complex [K]: Y_lm                                            */
     const double* ylm_m;      /* complex [K]: (-1)^l Y_{l,-m} (ignored for m = 0)             */
-    int32_t K;
+    int32_t K;                /* 1 <= K <= 8192                                               */
     /* frequency grid (device), ascending */
     const double* freq;       /* [nf]                                                         */
     int64_t nf;
@@ -97,7 +97,8 @@ typedef struct efd_modesum_args {
 size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf);
 
 /*
- * Full FD mode sum: spline build -> per-harmonic t(f) inverse splines -> interval records ->
+ * Full FD mode sum: (m, n) grouping -> spline build (trajectory; group amplitudes
+ * sum_l Y A_lmn) -> per-group t(f) inverse splines -> interval records ->
  * segment table -> SPA evaluation with output-stationary accumulation (each tile of frequency
  * bins builds its own record list in LDS). Asynchronous, allocation-free, no host sync, no
  * atomics on the spectrum; bitwise reproducible.
@@ -108,9 +109,16 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
  * this workspace (a harmonic with more than 8 monotonic frequency runs -> EFD_ERR_ARG). */
 int efd_modesum_status(const void* workspace, void* stream);
 
-/* Contributions C (harmonic branch x bin pairs) evaluated by the last efd_modesum on this
- * workspace (for the roofline); synchronises `stream`. */
+/* Contributions C (harmonic branch x bin pairs, the reference's per-(l, m, n) formulation) of
+ * the last efd_modesum on this workspace (for the roofline); synchronises `stream`. */
 int efd_modesum_contributions(const void* workspace, int64_t* contributions, void* stream);
+
+/* Statistics of the last efd_modesum on this workspace; synchronises `stream`. contributions as
+ * above; evaluations = SPA evaluations actually made (one per (m, n) group branch x bin: every
+ * l of a group shares t(f), the phase and the K_{1/3} factor); groups = distinct (m, n).
+ * NULL outputs are skipped. */
+int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* evaluations,
+                      int32_t* groups, void* stream);
 
 /*
  * h+ = (S(f) + conj(S_flip))/2, hx = i (S(f) - conj(S_flip))/2 with S_flip the array reversed

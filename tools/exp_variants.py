@@ -1,0 +1,120 @@
+"""Kernel experiments: build libemrifd.so variants here (CPU), time them on the GPU box.
+
+    python tools/exp_variants.py build NAME[:-DFLAG[=V][,-DFLAG2...]] ...   # here, hipcc only
+    python tools/exp_variants.py run NAME ...                              # on the GPU box
+
+`build` writes exp/libemrifd_<NAME>.so (git-ignored, travels with gpurun). `run` loads each
+variant in its own child process, runs config 2's full device pipeline, and prints one JSON line
+per variant: k_modesum ms (HIP events, mean of 5 launches), the spectrum's max deviation from
+the in-tree library's (relative to max|S|), and the EFD_EXP_COUNT counters when compiled in.
+The variant named "base" is the in-tree library.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXP = os.path.join(ROOT, "exp")
+SRC = os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc", "emrifd.hip")
+sys.path.insert(0, ROOT)
+
+
+def lib_path(name):
+    if name == "base":
+        return os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "libemrifd.so")
+    return os.path.join(EXP, f"libemrifd_{name}.so")
+
+
+def build(specs):
+    os.makedirs(EXP, exist_ok=True)
+    procs = []
+    for spec in specs:
+        name, _, flags = spec.partition(":")
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               *[f for f in flags.split(",") if f], "-o", lib_path(name), SRC]
+        print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+    if any(p.wait() != 0 for p in procs):
+        sys.exit("variant build failed")
+
+
+def child(name, ref_path):
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    os.environ["EFD_LIB"] = lib_path(name)
+    import bench
+    from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine
+
+    caustic = os.environ.get("EXP_CAUSTIC", "uniform")
+    w = bench.build_workload()
+    inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
+                                 w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"])
+    freq = torch.as_tensor(w["freq"], device="cuda")
+    S = torch.empty(len(w["freq"]), dtype=torch.complex128, device="cuda")
+    eng = ModeSumEngine(caustic=caustic)
+    eng.run(inp, freq, out=S, grid_symmetric=True, scale=w["prefactor"])
+    lib = eng.lib
+    has_cnt = hasattr(lib, "efd_exp_counters")
+    st = torch.cuda.current_stream().cuda_stream
+    fS = torch.view_as_real(S)
+    ms = []
+    for _ in range(6):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        b.record()
+        eng.launch(inp, freq, fS, True, w["prefactor"], stream=st,
+                   prof_events=(a.cuda_event, b.cuda_event))
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+    out = {"variant": name, "kernel_ms": float(np.mean(ms[1:])), "min_ms": float(min(ms[1:])),
+           "ok": bool(eng.status(st))}
+    Sh = S.cpu().numpy()
+    if ref_path and os.path.exists(ref_path):
+        R = np.load(ref_path)
+        out["max_rel_dev_vs_base"] = float(np.abs(Sh - R).max() / np.abs(R).max())
+    elif name == "base" and ref_path:
+        np.save(ref_path, Sh)
+    if has_cnt:
+        cnt = (ctypes.c_ulonglong * 16)()
+        lib.efd_exp_counters(cnt)
+        runs = 7  # the counters accumulate over every launch above
+        out["counters_per_launch"] = {k: cnt[i] / runs for i, k in enumerate(
+            ("record_evals", "cold_evals", "cold_lanes", "skips", "lanes_overshoot",
+             "lanes_y_mid", "lanes_y_small", "unused", "y_ge153", "y_ge75", "y_ge48",
+             "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18"))}
+    print("EXPRESULT " + json.dumps(out), flush=True)
+
+
+def run(names):
+    import tempfile
+    ref = os.path.join(tempfile.gettempdir(), f"exp_base_S_{os.getpid()}.npy")
+    if "base" in names:
+        names = ["base"] + [n for n in names if n != "base"]
+    for name in names:
+        r = subprocess.run([sys.executable, __file__, "child", name, ref], capture_output=True,
+                           text=True, timeout=300)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("EXPRESULT ")]
+        if r.returncode != 0 or not lines:
+            print(json.dumps({"variant": name, "error": r.returncode,
+                              "stderr": r.stderr[-2000:]}), flush=True)
+            if r.returncode < 0 or r.returncode in (124, 134, 137, 139):
+                sys.exit(1)   # a crash: start nothing more on the GPU
+            continue
+        print(lines[-1][len("EXPRESULT "):], flush=True)
+
+
+if __name__ == "__main__":
+    cmd, rest = sys.argv[1], sys.argv[2:]
+    if cmd == "build":
+        build(rest)
+    elif cmd == "run":
+        run(rest)
+    elif cmd == "child":
+        child(rest[0], rest[1] if len(rest) > 1 else None)
+    else:
+        sys.exit(__doc__)
