@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "FD waveforms/sec (2 yr, dt=10 s, ~3000 modes) at 1/2/4/8 GPUs; mode-sum HBM GB/s"
 HBM_PEAK_GBS = 8000.0
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 peak (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
 
 
 def build_workload(T=2.0, dt=10.0, eps=1e-5, M=1e6, mu=10.0, e0=0.35, theta=np.pi / 3,
@@ -206,7 +207,7 @@ def main():
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in sevs]))
     else:
         kern_ms = kern_ms_overlapped
-    C = eng.contributions(lanes[0]["stream"].cuda_stream)
+    C, n_eval, n_groups = eng.stats(lanes[0]["stream"].cuda_stream)
 
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -220,13 +221,22 @@ def main():
         b_alg = 32.0 * C + 32.0 * n_interp * nt + 16.0 * nf
         achieved = b_alg / (kern_ms * 1e-3) / 1e9
         traffic = None
+        fp64 = None
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof):
             try:
                 pj = json.load(open(prof))
                 if pj.get("workload") == "config2" and pj.get("caustic") == args.caustic:
                     traffic = pj.get("hbm_bytes_per_launch")
-            except (ValueError, OSError):
+                    f = pj.get("fp64")
+                    if f:
+                        tf = f["flops_per_launch"] / (kern_ms * 1e-3) / 1e12
+                        fp64 = {"achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": tf / FP64_VALU_PEAK_TFLOPS,
+                                "valu_busy": f["valu_busy"],
+                                "source": "FP64 VALU lane ops per launch from the committed "
+                                          "rocprofv3 PMC pass / this run's kernel_ms"}
+            except (ValueError, OSError, KeyError):
                 traffic = None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -250,7 +260,8 @@ def main():
             "data": "synthetic (stand-in trajectory/amplitudes; FEW data absent offline)",
             "config": {"workload": "config2: M=1e6 mu=10 e0=0.35 Tobs=2yr dt=10s eps=1e-5 "
                                    f"caustic={args.caustic}",
-                       "harmonics": K, "N_t": nt, "N_f": nf, "contributions": C,
+                       "harmonics": K, "mn_groups": n_groups, "N_t": nt, "N_f": nf,
+                       "contributions": C, "spa_evaluations": n_eval,
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
                        "streams_per_gpu": len(lanes)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -261,7 +272,8 @@ def main():
                                            f"HIP events, {args.roofline_launches} back-to-back "
                                            "launches on one stream after the timed region; "
                                            f"overlapped in-region: {kern_ms_overlapped:.3f} ms"),
-                         "contributions_per_s": C / (kern_ms * 1e-3)},
+                         "contributions_per_s": C / (kern_ms * 1e-3),
+                         "fp64_valu": fp64},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

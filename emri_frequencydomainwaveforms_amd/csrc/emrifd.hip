@@ -126,7 +126,7 @@ static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
-        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, total;
+        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, total;
     int64_t ntiles, nlanes;
 };
 
@@ -159,6 +159,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.gn = take(sizeof(int32_t) * K);
     L.gstart = take(sizeof(int32_t) * (K + 1));
     L.gmem = take(sizeof(int32_t) * K);
+    L.gamp = take(sizeof(double) * nt * 4 * K);
     L.total = off;
     return L;
 }
@@ -340,6 +341,41 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ marr
         gstart[part[1023]] = K;
         hdr->groups = part[1023];
     }
+}
+
+// K0b: group amplitudes at the knots, one thread per (knot i, group g):
+//   Bp = sum_l y0_l A_l(t_i),  Bm = sum_l y1_l A_l(t_i),  y0 = -scale Y+,  y1 = conj(-scale Y-)
+// (y1 = 0 for m = 0: no partner), summed in ascending h. gamp is [nt][4K]: (Bp re, Bp im,
+// Bm re, Bm im) of group g at 4g. S = -h_nb(-f) * scale: the minus sign and scale live here.
+__global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ amp,
+                                                   const double* __restrict__ ylm_p,
+                                                   const double* __restrict__ ylm_m, double sc_re,
+                                                   double sc_im, const int32_t* __restrict__ gm,
+                                                   const int32_t* __restrict__ gstart,
+                                                   const int32_t* __restrict__ gmem, int nt, int K,
+                                                   const Header* __restrict__ hdr,
+                                                   double* __restrict__ gamp) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (g >= hdr->groups || i >= nt) return;
+    const bool partner = gm[g] != 0;
+    double bpr = 0.0, bpi = 0.0, bmr = 0.0, bmi = 0.0;
+    for (int p = gstart[g], pe = gstart[g + 1]; p < pe; ++p) {
+        const int h = gmem[p];
+        const double ar = amp[((size_t)i * K + h) * 2], ai = amp[((size_t)i * K + h) * 2 + 1];
+        const double vr = ylm_p[2 * h], vi = ylm_p[2 * h + 1];
+        const double y0r = -(sc_re * vr - sc_im * vi), y0i = -(sc_re * vi + sc_im * vr);
+        bpr += ar * y0r - ai * y0i;
+        bpi += ar * y0i + ai * y0r;
+        if (partner) {
+            const double ur = ylm_m[2 * h], ui = ylm_m[2 * h + 1];
+            const double y1r = -(sc_re * ur - sc_im * ui), y1i = (sc_re * ui + sc_im * ur);
+            bmr += ar * y1r - ai * y1i;
+            bmi += ar * y1i + ai * y1r;
+        }
+    }
+    double* o = gamp + (size_t)i * 4 * K + 4 * g;
+    o[0] = bpr; o[1] = bpi; o[2] = bmr; o[3] = bmi;
 }
 
 // ----------------------------------------------------------------------------------------
@@ -608,10 +644,9 @@ __device__ void inverse_splines(const double* __restrict__ t, const double* __re
 __global__ __launch_bounds__(64) void k_prep(
     const double* __restrict__ t, const double* __restrict__ phi_phi,
     const double* __restrict__ phi_r, const double* __restrict__ f_phi,
-    const double* __restrict__ f_r, const double* __restrict__ amp,
-    const double* __restrict__ ylm_p, const double* __restrict__ ylm_m, double sc_re,
-    double sc_im, const int32_t* __restrict__ gm, const int32_t* __restrict__ gn,
-    const int32_t* __restrict__ gstart, const int32_t* __restrict__ gmem, int nt, int K,
+    const double* __restrict__ f_r, const double* __restrict__ gamp,
+    const int32_t* __restrict__ gm,
+    const int32_t* __restrict__ gn, int nt, int K,
     int nb_amp, double* __restrict__ coefT, double* __restrict__ kslope,
     double* __restrict__ tscratch, double* coefA, int32_t* __restrict__ runs,
     Item* __restrict__ items, double* __restrict__ invcp, double* __restrict__ invdp,
@@ -627,30 +662,7 @@ __global__ __launch_bounds__(64) void k_prep(
         traj_splines(t, phi_phi, phi_r, f_phi, f_r, nt, coefT, kslope, tscratch);
     } else if (b < 1 + nb_amp) {
         const int G = hdr->groups;
-        // y0 = -scale Y+, y1 = conj(-scale Y-) (partner only for m != 0): S = -h_nb(-f) scale
-        auto yf = [&](int i, int q) {
-            const int g = q >> 2, comp = q & 3;
-            const int pa = gstart[g], pb = gstart[g + 1];
-            const bool partner = gm[g] != 0;
-            double acc = 0.0;
-            for (int p = pa; p < pb; ++p) {
-                const int h = gmem[p];
-                const double Ar = amp[((size_t)i * K + h) * 2], Ai = amp[((size_t)i * K + h) * 2 + 1];
-                double yr, yi;
-                if (comp < 2) {
-                    const double vr = ylm_p[2 * h], vi = ylm_p[2 * h + 1];
-                    yr = -(sc_re * vr - sc_im * vi);
-                    yi = -(sc_re * vi + sc_im * vr);
-                } else {
-                    const double vr = partner ? ylm_m[2 * h] : 0.0;
-                    const double vi = partner ? ylm_m[2 * h + 1] : 0.0;
-                    yr = -(sc_re * vr - sc_im * vi);
-                    yi = (sc_re * vi + sc_im * vr);
-                }
-                acc += (comp & 1) ? (Ar * yi + Ai * yr) : (Ar * yr - Ai * yi);
-            }
-            return acc;
-        };
+        auto yf = [&](int i, int q) { return gamp[(size_t)i * 4 * K + q]; };
         spline_shared(t, nt, yf, 4 * G, 4 * K, coefA, (int64_t)4 * 4 * K, b - 1);
     } else {
         inverse_splines(t, f_phi, f_r, gm, gn, nt, K, hdr->groups, runs, items, invcp, invdp,
@@ -1772,6 +1784,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     int32_t* gn = (int32_t*)(ws + L.gn);
     int32_t* gstart = (int32_t*)(ws + L.gstart);
     int32_t* gmem = (int32_t*)(ws + L.gmem);
+    double* gamp = (double*)(ws + L.gamp);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
@@ -1784,14 +1797,16 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
                        hdr);
     HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
+                       a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
+    HIP_TRY(hipGetLastError());
     // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
     // grids sized for G = K, blocks past the device-side G return at once)
     {
         const int nb_amp = (4 * K + 63) / 64;
         const int nb_inv = (K + 63) / 64;
         hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp + nb_inv), dim3(64), sizeof(double) * 7 * nt, st,
-                           a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, a->amp, a->ylm_p,
-                           a->ylm_m, a->scale_re, a->scale_im, gm, gn, gstart, gmem, nt, K,
+                           a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, gamp, gm, gn, nt, K,
                            nb_amp, coefT, kslope, (double*)(ws + L.tscratch), coefA, runs, items,
                            invcp, invdp, hdr);
         HIP_TRY(hipGetLastError());

@@ -43,11 +43,30 @@ def main(tag):
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
     pmc = {}
     ndisp = {}
-    for p in ("pmc_fetch", "pmc_write", "pmc_sq"):
-        vals, n = per_dispatch(os.path.join(src, p, "run_counter_collection.csv"))
+    for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_valu"):
+        f = os.path.join(src, p, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        vals, n = per_dispatch(f)
         pmc.update(vals)
         ndisp[p] = n
     hbm = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
+    fp64 = None
+    if "SQ_INSTS_VALU_FMA_F64" in pmc:
+        # FP64 lane operations per launch (an FMA counts 2 FLOP), scaled by the measured lane
+        # utilisation of VALU instructions; VALU busy = SQ_ACTIVE_INST_VALU / CUs / GPU cycles
+        # (rocprofv3's VALUBusy; GRBM_GUI_ACTIVE is summed over the 8 XCDs here)
+        util = pmc["SQ_THREAD_CYCLES_VALU"] / (64.0 * pmc["SQ_ACTIVE_INST_VALU"])
+        flops = 64.0 * util * (2.0 * pmc["SQ_INSTS_VALU_FMA_F64"] + pmc["SQ_INSTS_VALU_MUL_F64"]
+                               + pmc["SQ_INSTS_VALU_ADD_F64"] + pmc["SQ_INSTS_VALU_TRANS_F64"])
+        gpu_cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
+        fp64 = {"flops_per_launch": flops, "lane_utilisation": util,
+                "valu_busy": pmc["SQ_ACTIVE_INST_VALU"] / 256.0 / gpu_cycles,
+                "fp64_share_of_valu_insts": (pmc["SQ_INSTS_VALU_FMA_F64"]
+                                             + pmc["SQ_INSTS_VALU_MUL_F64"]
+                                             + pmc["SQ_INSTS_VALU_ADD_F64"]
+                                             + pmc["SQ_INSTS_VALU_TRANS_F64"])
+                / pmc["SQ_INSTS_VALU"]}
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
         if "k_modesum" in r["Name"]:
@@ -55,13 +74,13 @@ def main(tag):
     bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
     summary = {"tag": tag, "kernel": "k_modesum", "workload": "config2",
                "caustic": "uniform", "counters_per_launch": pmc, "dispatches": ndisp,
-               "hbm_bytes_per_launch": hbm,
+               "hbm_bytes_per_launch": hbm, "fp64": fp64,
                "hbm_formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (kB; gfx950 FETCH_SIZE x2)",
                "rocprof_avg_ms": stats.get("avg_ns", 0.0) / 1e6,
                "bench_event_ms": bench["roofline"]["kernel_ms"]}
     json.dump(summary, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"workload": "config2", "caustic": "uniform", "kernel": "k_modesum",
-               "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc.json"},
+               "hbm_bytes_per_launch": hbm, "fp64": fp64, "source": f"profiles/{tag}_pmc.json"},
               open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
