@@ -102,9 +102,10 @@ def load(path=None):
     lib.efd_modesum_status.argtypes = [vp, vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int
     lib.efd_modesum_contributions.argtypes = [vp, ctypes.POINTER(i64), vp]
-    lib.efd_modesum_stats.restype = ctypes.c_int
-    lib.efd_modesum_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
-                                      ctypes.POINTER(i32), vp]
+    if hasattr(lib, "efd_modesum_stats"):   # absent only in pre-grouping experiment builds
+        lib.efd_modesum_stats.restype = ctypes.c_int
+        lib.efd_modesum_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                          ctypes.POINTER(i32), vp]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int

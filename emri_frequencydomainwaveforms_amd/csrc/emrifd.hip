@@ -1003,10 +1003,15 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
     constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
     constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
-    const double q = rint(x * INV_STEP);
+    // q = nearest integer to x / step via the 1.5 * 2^52 shifter: its low word is q itself
+    // (two's complement), so neither rint nor a float->int conversion is needed
+    constexpr double SHIFTER = 6755399441055744.0;
+    const double qs = fma(x, INV_STEP, SHIFTER);
+    const double q = qs - SHIFTER;
     double r = fma(-q, STEP_1, x);
     r = fma(-q, STEP_2, r);
-    const double2 t = tab[((int)q + shift) & (SCTAB - 1)];   // (sin, cos)((q + shift) pi/256)
+    const int qi = __double2loint(qs);
+    const double2 t = tab[(qi + shift) & (SCTAB - 1)];   // (sin, cos)((q + shift) pi/256)
     const double z = r * r;
     const double sr = fma(r * z, fma(z, 8.333333333333333e-03, -1.6666666666666666e-01), r);
     const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), 1.0);
@@ -1068,6 +1073,35 @@ __device__ __forceinline__ void kseries_fast(double ww, double& R, double& I) {
     I = ww * im;
 }
 
+// Ascending-series coefficients of kfactor_slow, c+-_k = 1 / (k! Gamma(k + 1 +- 1/3)) (the
+// recurrence c_k = c_(k-1) / (k (k +- 1/3)) evaluated once, in double), and the Horner degree
+// for |y| < i + 1 (next term < 1e-19 of the leading one); |y| < 18.4 needs at most 41.
+__constant__ double ASC_P[42] = {
+    1.1198465217221856, 0.8398848912916392, 0.1799753338482084, 0.01799753338482084,
+    0.001038319233739664, 3.89369712652374e-05, 1.024657138558879e-06, 1.9960853348549593e-08,
+    2.9941280022824386e-10, 3.564438097955284e-12, 3.449456223827694e-14, 2.766943495048952e-16,
+    1.869556415573616e-18, 1.0785902397540092e-20, 5.375034417378783e-23, 2.336971485816862e-25,
+    8.942492930421667e-28, 3.0347826686951365e-30, 9.196311117257989e-33, 2.5035329720303054e-35,
+    6.156228619746653e-38, 1.3741581740505923e-40, 2.796794112721694e-43, 5.211417601344772e-46,
+    8.923660276275295e-49, 1.4089989909908362e-51, 2.0579342614277064e-54, 2.788528809522637e-57,
+    3.514952280910888e-60, 4.13199719542816e-63, 4.540656258712264e-66, 4.674663272524637e-69,
+    4.5180379566926256e-72, 4.1073072333569326e-75, 3.5185384637552244e-78, 2.8451793507454644e-81,
+    2.175213570906318e-84, 1.5747202492082417e-87, 1.0810436493420424e-90, 7.047220660639129e-94,
+    4.368111979734997e-97, 2.577564110779896e-100};
+__constant__ double ASC_M[42] = {
+    0.7384881116216483, 1.1077321674324723, 0.3323196502297417, 0.04153995627871771,
+    0.0028322697462762076, 0.00012138298912612317, 3.5700879154742108e-06, 7.65018839030188e-08,
+    1.2473133245057413e-09, 1.5991196468022326e-11, 1.6542617035885167e-13, 1.4098821337402132e-15,
+    1.007058666957295e-17, 6.115740892453209e-20, 3.1963802573797266e-22, 1.4529001169907847e-24,
+    5.796144083739833e-27, 2.045697911908176e-29, 6.433012301598037e-32, 1.8138192579693712e-34,
+    4.611404893142469e-37, 1.0625356896641634e-39, 2.2290958524423007e-42, 4.2757593077537736e-45,
+    7.527745260129883e-48, 1.2207154475886294e-50, 1.8292439274554885e-53, 2.540616565910401e-56,
+    3.279625515374872e-59, 3.945018663241626e-62, 4.432605239597333e-65, 4.662628232395511e-68,
+    4.6012778609166224e-71, 4.2683468097556795e-74, 3.728899367870425e-77, 3.073268709783318e-80,
+    2.393511456217537e-83, 1.7642590586370054e-86, 1.2325983176318156e-89, 8.173728896762703e-93,
+    5.151509808884057e-96, 3.089670017323505e-99};
+__constant__ int ASC_DEG[19] = {10, 12, 15, 17, 19, 21, 22, 24, 26, 27, 29, 30, 32, 34, 35, 37, 38, 40, 41};
+
 // (R + i I) for |y| < FAST_Y: asymptotic with up to 40 terms down to |y| = 18.4, below that the
 // ascending series K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3}) divided by Q_spa.
 __device__ __noinline__ void kfactor_slow(double fd, double fdd, double& R, double& I) {
@@ -1088,19 +1122,15 @@ __device__ __noinline__ void kfactor_slow(double fd, double fdd, double& R, doub
         I = w * im;
         return;
     }
-    // ascending series for K_{1/3}(z), z = -i y; K~ = K e^{z}
+    // ascending series for K_{1/3}(z), z = -i y; K~ = K e^{z}: sp, sm = sum_k c+-_k q^k,
+    // q = -y^2/4, by Horner to the degree |y| needs (no divisions, no convergence test)
     const double sgn = y > 0 ? 1.0 : -1.0;
-    constexpr double nu = 1.0 / 3.0;
-    constexpr double G_P = 0.89297951156924921122;  // Gamma(4/3)
-    constexpr double G_M = 1.35411793942640041695;  // Gamma(2/3)
     const double q = -0.25 * y * y;
-    double tp = 1.0 / G_P, tm = 1.0 / G_M, sp = tp, sm = tm;
-    for (int k = 1; k < 200; ++k) {
-        tp *= q / (k * (k + nu));
-        tm *= q / (k * (k - nu));
-        sp += tp;
-        sm += tm;
-        if (fabs(tp) < 1e-18 * fabs(sp) && fabs(tm) < 1e-18 * fabs(sm)) break;
+    const int deg = ASC_DEG[min(18, (int)ay)];
+    double sp = ASC_P[deg], sm = ASC_M[deg];
+    for (int k = deg - 1; k >= 0; --k) {
+        sp = fma(sp, q, ASC_P[k]);
+        sm = fma(sm, q, ASC_M[k]);
     }
     const double zp = cbrt(0.5 * ay);     // (|y|/2)^{1/3}
     const double zm = 1.0 / zp;
@@ -1131,20 +1161,14 @@ struct FwdEval {
     double ph, fd, fdd;
 };
 __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restrict__ t, int nt,
-                                                int h, int K, int m, int n,
+                                                int jhint, int h, int K, int m, int n,
                                                 const double* __restrict__ coefA,
                                                 const double* __restrict__ coefT) {
-    // scipy: interval i with t_i <= tt < t_{i+1}, clamped to [0, nt-2] (extrapolation)
-    int lo = 0, hi = nt - 1;
-    if (tt >= t[nt - 1]) lo = nt - 2;
-    else if (tt <= t[0]) lo = 0;
-    else {
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (t[mid] <= tt) lo = mid; else hi = mid;
-        }
-    }
-    const int j = lo;
+    // scipy: interval i with t_i <= tt < t_{i+1}, clamped to [0, nt-2] (extrapolation). t(g)
+    // overshoots the record's interval jhint by little, so walk from there (1-2 loads).
+    int j = jhint;
+    while (j > 0 && tt < t[j]) --j;
+    while (j < nt - 2 && tt >= t[j + 1]) ++j;
     const double w = tt - t[j];
     auto cub = [&](double c0, double c1, double c2, double c3) {
         return fma(fma(fma(c0, w, c1), w, c2), w, c3);
@@ -1202,7 +1226,7 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
         const double a3 = amp * amp * amp;
         const double t3 = fdds * a3;
         const double ww = copysign(t3 * t3, fd);
-        good = good & (fabs(ww) * FAST_Y <= 1.0);
+        good = good & (fabs(ww) <= 1.0 / FAST_Y);
         kseries_fast(ww, R, I);
     }
     // W = 0 unless this lane finishes here (the general path adds the others' terms)
@@ -1228,7 +1252,7 @@ struct ColdEval {
     double wr, wi, b[4];
 };
 template <int CAUSTIC>
-__device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double g, int h,
+__device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double g, int h, int jrec,
                                              const double* __restrict__ t, int nt, int K,
                                              const int32_t* __restrict__ gm,
                                              const int32_t* __restrict__ gn,
@@ -1248,7 +1272,7 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
 #ifdef EFD_EXP_COUNT
         atomicAdd(&g_exp_count[4], 1ull);
 #endif
-        const FwdEval fe = forward_generic(tt, t, nt, h, K, gm[h], gn[h], coefA, coefT);
+        const FwdEval fe = forward_generic(tt, t, nt, jrec, h, K, gm[h], gn[h], coefA, coefT);
         for (int q = 0; q < 4; ++q) c.b[q] = fe.b[q];
         ph = fe.ph; fd = fe.fd; fdd = fe.fdd;
     }
@@ -1559,11 +1583,12 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                         }
 #endif
                         const int hg = (int)((key >> 1) / (uint32_t)ni);   // the record's group
+                        const int jr = (int)((key >> 1) - (uint32_t)hg * (uint32_t)ni);   // interval
 #pragma unroll
                         for (int i = 0; i < BPL; ++i) {
                             if (need[i]) {
                                 const ColdEval ce = spa_general<CAUSTIC>(
-                                    it, S ? fk[i] : -fk[i], hg, t, nt, K, gm, gn, coefA, coefT);
+                                    it, S ? fk[i] : -fk[i], hg, jr, t, nt, K, gm, gn, coefA, coefT);
                                 accumulate<S, PAIRED>(ce.wr, ce.wi, ce.b[2 * S], ce.b[2 * S + 1],
                                                       ce.b[2 - 2 * S], ce.b[3 - 2 * S], own_r[i],
                                                       own_i[i], mir_r[i], mir_i[i]);
