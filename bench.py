@@ -11,16 +11,16 @@ emri_pe.py:623-635), Tobs = 2 yr, dt = 10 s (N_f = 6,311,631 two-sided bins), ep
 trajectory, amplitudes, Ylm; host stand-ins, NOT FEW physics) are resident in HBM before timing.
 One step = one full FD waveform on the device: spline build -> inverse splines -> interval
 records -> tile lists -> mode sum -> h+/hx over f >= 0 (the Likelihood path, emri_pe.py:241).
-Waveforms alternate over --streams (default 2) independent pipelines, so one waveform's
-latency-bound spline kernels and its mode sum's ramp-up overlap the previous mode sum's tail.
+With --pipeline overlap (default) waveform i+1's preparation (grouping, splines, records:
+latency-bound kernels on few CUs; efd_modesum_prepare) runs on a second stream beside waveform
+i's mode sum (efd_modesum_sum), and the sum writes h+/hx itself (fused polarisations).
 
 Multi-GPU: one process per GPU; each rank generates its own waveforms (the walker batch of
 emri_pe.py shards with no data-path exchange: weak scaling); value = all ranks' waveforms / the
 max over ranks of the timed region.
 
 roofline: the mode-sum kernel (k_modesum) timed with HIP events recorded on its own stream
-around that kernel only (with --streams > 1, in a serial pass of back-to-back launches right
-after the timed region, since overlapped launches share the GPU); achieved = B_alg / t with B_alg = 32 C + 32 n_interp N_t + 16 N_f
+around each launch of that kernel in the timed region; achieved = B_alg / t with B_alg = 32 C + 32 n_interp N_t + 16 N_f
 (32 B per SPA contribution of the reference's scatter formulation),
 peak 8.0 TB/s (MI355X_MICROARCH.md). traffic: HBM bytes per launch from the committed rocprofv3
 PMC pass (profiles/), or null.
@@ -112,10 +112,9 @@ def main():
     ap.add_argument("--eps", type=float, default=1e-5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="independent waveform pipelines in flight (HIP streams)")
-    ap.add_argument("--roofline-launches", type=int, default=5,
-                    help="serial k_modesum launches timed for the roofline when streams > 1")
+    ap.add_argument("--pipeline", default="overlap", choices=["overlap", "serial"],
+                    help="overlap: prepare(i+1) on a second stream beside sum(i), fused h+/hx; "
+                         "serial: one stream, efd_modesum + efd_polarizations")
     args = ap.parse_args()
 
     import torch
@@ -138,41 +137,51 @@ def main():
     freq = torch.as_tensor(w["freq"], device=dev)
     nf = int(freq.numel())
     k0 = int(np.searchsorted(w["freq"], 0.0))
-    # waveforms alternate over `streams` independent pipelines (own workspace, output and HIP
-    # stream): waveform i+1's latency-bound spline/record kernels and the head of its mode sum
-    # run while waveform i's mode sum drains, instead of leaving CUs idle in between
-    lanes = []
-    for _ in range(max(1, args.streams)):
-        S = torch.empty(nf, dtype=torch.complex128, device=dev)
+    overlap = args.pipeline == "overlap"
+    # Two slots (workspace + h+/hx outputs). "overlap": waveform i+1's preparation (grouping,
+    # splines, records: latency-bound kernels on few CUs) runs on the prep stream while waveform
+    # i's mode sum runs on the sum stream; the sum writes h+/hx directly (fused polarisations).
+    # "serial": one stream, efd_modesum then efd_polarizations (the unfused path).
+    slots = []
+    for _ in range(2 if overlap else 1):
         hp = torch.empty(nf - k0, dtype=torch.complex128, device=dev)
-        eng = ModeSumEngine(caustic=args.caustic)
-        s = torch.cuda.Stream(dev)
-        with torch.cuda.stream(s):
-            eng.run(inp, freq, out=S, grid_symmetric=True, scale=w["prefactor"])  # workspace
-        lanes.append(dict(eng=eng, stream=s, fS=torch.view_as_real(S),
-                          fhp=torch.view_as_real(hp),
-                          fhc=torch.view_as_real(torch.empty_like(hp))))
-    torch.cuda.synchronize()
-    eng = lanes[0]["eng"]
-    lib = eng.lib
+        slots.append(dict(eng=ModeSumEngine(caustic=args.caustic), fhp=torch.view_as_real(hp),
+                          fhc=torch.view_as_real(torch.empty_like(hp)),
+                          fS=None if overlap else torch.view_as_real(
+                              torch.empty(nf, dtype=torch.complex128, device=dev)),
+                          prep_done=torch.cuda.Event(), sum_done=None))
+    s_prep = torch.cuda.Stream(dev)
+    s_sum = torch.cuda.Stream(dev) if overlap else s_prep
+    lib = slots[0]["eng"].lib
+
+    def step(i, ev=None):
+        sl = slots[i % len(slots)]
+        eng = sl["eng"]
+        pe = (ev[0].cuda_event, ev[1].cuda_event) if ev is not None else (None, None)
+        if overlap:
+            if sl["sum_done"] is not None:        # the slot's previous sum has read its workspace
+                s_prep.wait_event(sl["sum_done"])
+            eng.launch(inp, freq, None, True, w["prefactor"], stream=s_prep.cuda_stream,
+                       phase="prepare")
+            sl["prep_done"].record(s_prep)
+            s_sum.wait_event(sl["prep_done"])
+            eng.launch(inp, freq, None, True, w["prefactor"], stream=s_sum.cuda_stream,
+                       prof_events=pe, hp=sl["fhp"], hc=sl["fhc"], k0=k0, phase="sum")
+            done = torch.cuda.Event()
+            done.record(s_sum)
+            sl["sum_done"] = done
+        else:
+            st = s_prep.cuda_stream
+            eng.launch(inp, freq, sl["fS"], True, w["prefactor"], stream=st, prof_events=pe)
+            _lib.check(lib.efd_polarizations(sl["fS"].data_ptr(), nf, k0, sl["fhp"].data_ptr(),
+                                             sl["fhc"].data_ptr(), st), "efd_polarizations", lib)
 
     evs = []
     for i in range(args.steps):
-        s = lanes[i % len(lanes)]["stream"]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s)
-        b.record(s)
+        a.record(s_sum)   # creates the events; the library re-records them around k_modesum
+        b.record(s_sum)
         evs.append((a, b))
-    torch.cuda.synchronize()
-
-    def step(i, ev=None):
-        ln = lanes[i % len(lanes)]
-        st = ln["stream"].cuda_stream
-        pe = (ev[0].cuda_event, ev[1].cuda_event) if ev is not None else (None, None)
-        ln["eng"].launch(inp, freq, ln["fS"], True, w["prefactor"], stream=st, prof_events=pe)
-        _lib.check(lib.efd_polarizations(ln["fS"].data_ptr(), nf, k0, ln["fhp"].data_ptr(),
-                                         ln["fhc"].data_ptr(), st), "efd_polarizations", lib)
-
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -186,28 +195,13 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    if not all(ln["eng"].status(ln["stream"].cuda_stream) for ln in lanes):
-        raise RuntimeError(f"efd_modesum reported a device error: {_lib.last_error(lib)}")
-    kern_ms_overlapped = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    # roofline timing: with several pipelines in flight, two mode-sum kernels share the GPU and
-    # each one's start-to-end time covers both; the per-launch duration of the kernel itself is
-    # measured right after the timed region on one stream, back to back (same inputs)
-    if len(lanes) > 1:
-        ln = lanes[0]
-        sevs = []
-        for i in range(args.roofline_launches):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(ln["stream"])   # creates the events; the library re-records them
-            b.record(ln["stream"])   # around the kernel
-            ln["eng"].launch(inp, freq, ln["fS"], True, w["prefactor"],
-                             stream=ln["stream"].cuda_stream,
-                             prof_events=(a.cuda_event, b.cuda_event))
-            sevs.append((a, b))
-        torch.cuda.synchronize()
-        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in sevs]))
-    else:
-        kern_ms = kern_ms_overlapped
-    C, n_eval, n_groups = eng.stats(lanes[0]["stream"].cuda_stream)
+    for sl in slots:
+        if not sl["eng"].status(s_sum.cuda_stream):
+            raise RuntimeError(f"efd_modesum reported a device error: {_lib.last_error(lib)}")
+    # per-launch k_modesum duration, live over the timed region (HIP events on the sum stream;
+    # with the overlap pipeline the next waveform's preparation kernels share the GPU with it)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    C, n_eval, n_groups = slots[0]["eng"].stats(s_sum.cuda_stream)
 
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -263,15 +257,12 @@ def main():
                        "harmonics": K, "mn_groups": n_groups, "N_t": nt, "N_f": nf,
                        "contributions": C, "spa_evaluations": n_eval,
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
-                       "streams_per_gpu": len(lanes)},
+                       "pipeline": args.pipeline},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_modesum", "kernel_ms": kern_ms,
-                         "kernel_timing": ("HIP events around each launch in the timed region"
-                                           if len(lanes) == 1 else
-                                           f"HIP events, {args.roofline_launches} back-to-back "
-                                           "launches on one stream after the timed region; "
-                                           f"overlapped in-region: {kern_ms_overlapped:.3f} ms"),
+                         "kernel_timing": "HIP events around each k_modesum launch in the timed "
+                                          "region (sum stream), mean",
                          "contributions_per_s": C / (kern_ms * 1e-3),
                          "fp64_valu": fp64},
             "cpu_baseline": cpu,

@@ -26,6 +26,8 @@ EXPORTED_SYMBOLS = (
     "efd_spline_build",
     "efd_modesum_workspace_bytes",
     "efd_modesum",
+    "efd_modesum_prepare",
+    "efd_modesum_sum",
     "efd_modesum_status",
     "efd_modesum_contributions",
     "efd_modesum_stats",
@@ -61,6 +63,9 @@ class ModesumArgs(ctypes.Structure):
         ("out", ctypes.c_void_p),
         ("prof_begin", ctypes.c_void_p),
         ("prof_end", ctypes.c_void_p),
+        ("hp", ctypes.c_void_p),
+        ("hc", ctypes.c_void_p),
+        ("k0", ctypes.c_int64),
     ]
 
 
@@ -98,6 +103,10 @@ def load(path=None):
     lib.efd_modesum_workspace_bytes.argtypes = [i32, i32, i64]
     lib.efd_modesum.restype = ctypes.c_int
     lib.efd_modesum.argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
+    for name in ("efd_modesum_prepare", "efd_modesum_sum"):
+        if hasattr(lib, name):   # absent only in older experiment builds
+            getattr(lib, name).restype = ctypes.c_int
+            getattr(lib, name).argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
     lib.efd_modesum_status.argtypes = [vp, vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int

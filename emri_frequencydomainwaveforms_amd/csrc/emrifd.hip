@@ -1350,7 +1350,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,
     const int32_t* __restrict__ gn, const double* __restrict__ t,
     const double* __restrict__ coefA, const double* __restrict__ coefT, int accumulate_out,
-    double* __restrict__ out) {
+    double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -1609,26 +1609,50 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
 #undef EFD_FETCH
 #undef EFD_STORE
 
+    // S is written when out != NULL; on a symmetric grid h+ and hx of bins [k0, nf) are written
+    // straight from the registers when hp != NULL (the lane holds S(k) and S(nf-1-k), the two
+    // halves of efd_polarizations' flip), so the likelihood path never stores S
     double2* o = reinterpret_cast<double2*>(out);
+    double2* php = reinterpret_cast<double2*>(hp);
+    double2* phc = reinterpret_cast<double2*>(hc);
 #pragma unroll
     for (int i = 0; i < BPL; ++i) {
         const int64_t k = w_lo + 64 * i + lane;
         if (k >= nlanes) continue;
-        double orr = own_r[i], oi = own_i[i];
-        if (PAIRED) {
-            const int64_t km = nf - 1 - k;
-            if (km == k) {
-                orr += mir_r[i];
-                oi += mir_i[i];
-            } else {
-                double2 vm = make_double2(mir_r[i], mir_i[i]);
+        const int64_t km = PAIRED ? nf - 1 - k : k;
+        double2 sk = make_double2(own_r[i], own_i[i]);
+        double2 sm = make_double2(mir_r[i], mir_i[i]);
+        if (PAIRED && km == k) {
+            sk.x += sm.x;
+            sk.y += sm.y;
+            sm = sk;
+        }
+        if (o) {
+            if (PAIRED && km != k) {
+                double2 vm = sm;
                 if (accumulate_out) { const double2 p = o[km]; vm.x += p.x; vm.y += p.y; }
                 o[km] = vm;
             }
+            double2 v = sk;
+            if (accumulate_out) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
+            o[k] = v;
         }
-        double2 v = make_double2(orr, oi);
-        if (accumulate_out) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
-        o[k] = v;
+        if (PAIRED && php) {
+            // h+ = (a + conj b)/2, hx = i (a - conj b)/2 with a = S(j), b = S(nf-1-j)
+            auto put = [&](int64_t j, double2 a, double2 b) {
+                if (j < k0) return;
+                double2 vp = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+                double2 vc = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+                if (accumulate_out) {
+                    const double2 pp = php[j - k0], pc = phc[j - k0];
+                    vp.x += pp.x; vp.y += pp.y; vc.x += pc.x; vc.y += pc.y;
+                }
+                php[j - k0] = vp;
+                phc[j - k0] = vc;
+            };
+            put(km, sm, sk);
+            if (km != k) put(k, sk, sm);
+        }
     }
 }
 
@@ -1775,11 +1799,19 @@ size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf) {
     return make_layout(nt, K, nf, 0).total;  // unpaired has the most tiles
 }
 
-int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream) {
+// phase: 1 = prepare (K0-K5), 2 = sum (K8), 3 = both
+static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                        void* stream, int phase) {
     if (!a || !workspace) return fail(EFD_ERR_ARG, "efd_modesum: NULL argument");
     if (!a->t || !a->phi_phi || !a->phi_r || !a->f_phi || !a->f_r || !a->amp || !a->m ||
-        !a->n || !a->ylm_p || !a->ylm_m || !a->freq || !a->out)
+        !a->n || !a->ylm_p || !a->ylm_m || !a->freq)
         return fail(EFD_ERR_ARG, "efd_modesum: NULL array");
+    const bool pol = a->hp != nullptr || a->hc != nullptr;
+    if (pol && (!a->hp || !a->hc || !a->grid_symmetric || a->k0 < 0 || a->k0 > a->nf))
+        return fail(EFD_ERR_ARG, "efd_modesum: hp/hc need both pointers, a symmetric grid and "
+                                 "0 <= k0 <= nf");
+    if ((phase & 2) && !a->out && !pol)
+        return fail(EFD_ERR_ARG, "efd_modesum: no output (out or hp/hc)");
     if (a->nt < 2 || a->nt > MAX_NT) return fail(EFD_ERR_ARG, "efd_modesum: nt out of range");
     if (a->K <= 0 || a->K > MAX_K) return fail(EFD_ERR_ARG, "efd_modesum: K out of range [1, 8192]");
     if (a->nf <= 0 || a->nf >= (int64_t)INT32_MAX)
@@ -1816,6 +1848,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
     const int64_t nl = L.nlanes;
     const int64_t nl1 = paired ? ((nf % 2) ? nl - 1 : nl) : nf;
 
+    if (phase & 1) {
     HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
 
     // K0: (m, n) groups
@@ -1864,8 +1897,9 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
                            blockcnt, nslot, seglh, seginfo, nseg);
     }
     HIP_TRY(hipGetLastError());
+    }  // phase 1
     // K8: mode sum
-    {
+    if (phase & 2) {
         const int64_t gq = 8 * XCD_GROUP;
         const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
         const int acc = a->accumulate ? 1 : 0;
@@ -1873,7 +1907,7 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh, seginfo,  \
                        nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA, coefT,        \
-                       acc, a->out)
+                       acc, a->out, a->hp, a->hc, a->k0)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
             else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
@@ -1886,6 +1920,20 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
         if (a->prof_end) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_end, st));
     }
     return EFD_OK;
+}
+
+int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream) {
+    return modesum_impl(a, workspace, workspace_bytes, stream, 3);
+}
+
+int efd_modesum_prepare(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+    return modesum_impl(a, workspace, workspace_bytes, stream, 1);
+}
+
+int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                    void* stream) {
+    return modesum_impl(a, workspace, workspace_bytes, stream, 2);
 }
 
 int efd_modesum_status(const void* workspace, void* stream) {

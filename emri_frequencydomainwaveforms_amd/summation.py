@@ -108,11 +108,18 @@ class ModeSumEngine:
         return self._ws
 
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
-               stream=None, prof_events=(None, None)):
-        """Asynchronous launch; returns the workspace (check with `status`)."""
+               stream=None, prof_events=(None, None), hp=None, hc=None, k0=0, phase="all"):
+        """Asynchronous launch; returns the workspace (check with `status`).
+
+        out: float64 view of the complex spectrum, or None when only the fused polarisations
+        hp/hc (float64 views of complex [nf - k0], symmetric grids) are wanted. phase: "all"
+        (efd_modesum), "prepare" or "sum" (efd_modesum_prepare / _sum, for overlapping one
+        waveform's preparation with the previous one's sum on another stream).
+        """
         torch = _torch()
         nf = int(freq.numel())
         ws = self._workspace(inp.nt, inp.K, nf, freq.device)
+        ptr = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
         a = _lib.ModesumArgs(
             t=inp.t.data_ptr(), phi_phi=inp.phi_phi.data_ptr(), phi_r=inp.phi_r.data_ptr(),
             f_phi=inp.f_phi.data_ptr(), f_r=inp.f_r.data_ptr(), nt=inp.nt,
@@ -121,9 +128,12 @@ class ModeSumEngine:
             freq=freq.data_ptr(), nf=nf, grid_symmetric=1 if grid_symmetric else 0,
             scale_re=float(np.real(scale)), scale_im=float(np.imag(scale)),
             caustic=CAUSTIC_MODES[self.caustic], accumulate=1 if accumulate else 0,
-            out=out.data_ptr(), prof_begin=prof_events[0], prof_end=prof_events[1])
+            out=ptr(out), prof_begin=prof_events[0], prof_end=prof_events[1],
+            hp=ptr(hp), hc=ptr(hc), k0=int(k0))
         st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
-        _lib.check(self.lib.efd_modesum(a, ws.data_ptr(), ws.numel(), st), "efd_modesum", self.lib)
+        fn = {"all": "efd_modesum", "prepare": "efd_modesum_prepare",
+              "sum": "efd_modesum_sum"}[phase]
+        _lib.check(getattr(self.lib, fn)(a, ws.data_ptr(), ws.numel(), st), fn, self.lib)
         return ws
 
     def status(self, stream=None):

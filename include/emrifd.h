@@ -84,12 +84,19 @@ typedef struct efd_modesum_args {
     /* scaling: S *= scale (complex), e.g. mu MRSUN_SI/(dist Gpc) * e^{-2 i psi_pol}           */
     double scale_re, scale_im;
     int32_t caustic;          /* EFD_CAUSTIC_*                                                */
-    int32_t accumulate;       /* 1: out += S, 0: out = S                                      */
-    double* out;              /* complex [nf] (device): FEW 'fd' spectrum S = h+ - i hx       */
+    int32_t accumulate;       /* 1: outputs += new values, 0: outputs = new values            */
+    double* out;              /* complex [nf] (device): FEW 'fd' spectrum S = h+ - i hx, or
+                               * NULL when only hp/hc are wanted                               */
     /* optional hipEvent_t pair recorded on `stream` around the mode-sum kernel alone (K8), for
      * roofline timing; NULL = not recorded */
     void* prof_begin;
     void* prof_end;
+    /* optional fused polarisations (symmetric grids only): complex [nf - k0] each, written as
+     * efd_polarizations(S, nf, k0, hp, hc) would, from the registers that hold S (no S round
+     * trip through HBM). NULL = not written. */
+    double* hp;
+    double* hc;
+    int64_t k0;
 } efd_modesum_args;
 
 /* Bytes of device workspace efd_modesum needs for (nt, K, nf), valid for either grid kind;
@@ -104,6 +111,18 @@ size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf);
  * atomics on the spectrum; bitwise reproducible.
  */
 int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * The same call in two phases on possibly different streams (the caller orders them, e.g. with
+ * an event): _prepare runs everything up to the tile lists' segment table (grouping, splines,
+ * inverse splines, interval records; latency-bound, few CUs), _sum the mode-sum kernel (reads
+ * freq, writes out / hp / hc). With two workspaces, waveform i+1's prepare overlaps waveform
+ * i's sum. efd_modesum == _prepare then _sum on one stream.
+ */
+int efd_modesum_prepare(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                        void* stream);
+int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                    void* stream);
 
 /* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
  * this workspace (a harmonic with more than 8 monotonic frequency runs -> EFD_ERR_ARG). */

@@ -205,3 +205,40 @@ def test_loglike_matches_numpy():
     _lib.check(lib.efd_loglike(torch.view_as_real(H).data_ptr(), torch.view_as_real(D).data_ptr(),
                                W.data_ptr(), 2, nbin, out.data_ptr(), scr.data_ptr(), st), "ll")
     assert abs(out.item() - ref) <= 1e-12 * abs(ref)
+
+
+def test_fused_polarizations_and_two_phase_api(multimode):
+    """efd_modesum_prepare + efd_modesum_sum with hp/hc == efd_modesum then efd_polarizations,
+    bitwise, for k0 at f = 0 (mask_positive) and k0 = 0 (full grid), plus accumulate."""
+    import ctypes
+    from emri_frequencydomainwaveforms_amd import _lib
+    d = multimode
+    inp = DeviceInputs.from_host(d["t"], np.asarray(d["amp"]).T, d["phi_phi"], d["phi_r"],
+                                 d["f_phi"], d["f_r"], d["m"], d["n"], d["ylm_p"], d["ylm_m"])
+    freq = torch.as_tensor(d["freq"], device="cuda")
+    nf = len(d["freq"])
+    eng = ModeSumEngine()
+    S = eng.run(inp, freq, grid_symmetric=True, scale=d["prefactor"])
+    st = torch.cuda.current_stream().cuda_stream
+    for k0 in (int(np.searchsorted(d["freq"], 0.0)), 0):
+        rp = torch.empty(nf - k0, dtype=torch.complex128, device="cuda")
+        rc = torch.empty_like(rp)
+        _lib.check(eng.lib.efd_polarizations(torch.view_as_real(S).data_ptr(), nf, k0,
+                                             torch.view_as_real(rp).data_ptr(),
+                                             torch.view_as_real(rc).data_ptr(),
+                                             ctypes.c_void_p(st)), "pol")
+        hp = torch.full_like(rp, np.nan)
+        hc = torch.full_like(rp, np.nan)
+        eng.launch(inp, freq, None, True, d["prefactor"], phase="prepare")
+        eng.launch(inp, freq, None, True, d["prefactor"], phase="sum",
+                   hp=torch.view_as_real(hp), hc=torch.view_as_real(hc), k0=k0)
+        assert eng.status()
+        assert torch.equal(hp, rp) and torch.equal(hc, rc)
+        eng.launch(inp, freq, None, True, d["prefactor"], accumulate=True,
+                   hp=torch.view_as_real(hp), hc=torch.view_as_real(hc), k0=k0)
+        assert eng.status()
+        assert torch.allclose(hp, 2 * rp, rtol=1e-15, atol=0) and torch.allclose(hc, 2 * rc,
+                                                                                rtol=1e-15, atol=0)
+    with pytest.raises(_lib.EFDError):   # fused outputs need a symmetric grid
+        eng.launch(inp, freq, None, False, d["prefactor"], hp=torch.view_as_real(hp),
+                   hc=torch.view_as_real(hc), k0=0)

@@ -15,9 +15,9 @@ tail -1 $O/pytest_gpu.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 2; }
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
-# one pipeline: the profiled per-launch k_modesum durations are then the same quantity the
-# bench line reports (with --streams 2, in-flight launches overlap and each spans both)
-B="$R/bench.py --no-cpu-baseline --steps 10 --warmup 2 --streams 1"
+# the same command as the bench line (overlap pipeline): one k_modesum launch per waveform on
+# the sum stream, so the profiled per-launch durations are the quantity the bench reports
+B="$R/bench.py --no-cpu-baseline --steps 10 --warmup 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $B > $O/trace.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_modesum --output-format csv -d $O/pmc_fetch -o run -- python $B > $O/pmc_fetch.log 2>&1 || exit 4
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_modesum --output-format csv -d $O/pmc_write -o run -- python $B > $O/pmc_write.log 2>&1 || exit 5
