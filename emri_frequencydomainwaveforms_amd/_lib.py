@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_status",
     "efd_modesum_contributions",
     "efd_modesum_stats",
+    "efd_td_workspace_bytes",
+    "efd_td_modesum",
     "efd_polarizations",
     "efd_loglike",
     "efd_inner_product",
@@ -66,6 +68,35 @@ class ModesumArgs(ctypes.Structure):
         ("hp", ctypes.c_void_p),
         ("hc", ctypes.c_void_p),
         ("k0", ctypes.c_int64),
+    ]
+
+
+class TdArgs(ctypes.Structure):
+    """Mirror of `efd_td_args` (include/emrifd.h)."""
+
+    _fields_ = [
+        ("t", ctypes.c_void_p),
+        ("phi_phi", ctypes.c_void_p),
+        ("phi_r", ctypes.c_void_p),
+        ("f_phi", ctypes.c_void_p),
+        ("f_r", ctypes.c_void_p),
+        ("nt", ctypes.c_int32),
+        ("amp", ctypes.c_void_p),
+        ("m", ctypes.c_void_p),
+        ("n", ctypes.c_void_p),
+        ("ylm_p", ctypes.c_void_p),
+        ("ylm_m", ctypes.c_void_p),
+        ("K", ctypes.c_int32),
+        ("dt", ctypes.c_double),
+        ("nsamples", ctypes.c_int64),
+        ("scale_re", ctypes.c_double),
+        ("scale_im", ctypes.c_double),
+        ("accumulate", ctypes.c_int32),
+        ("out", ctypes.c_void_p),
+        ("hp", ctypes.c_void_p),
+        ("hc", ctypes.c_void_p),
+        ("prof_begin", ctypes.c_void_p),
+        ("prof_end", ctypes.c_void_p),
     ]
 
 
@@ -115,6 +146,11 @@ def load(path=None):
         lib.efd_modesum_stats.restype = ctypes.c_int
         lib.efd_modesum_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
                                           ctypes.POINTER(i32), vp]
+    if hasattr(lib, "efd_td_modesum"):   # absent only in older experiment builds
+        lib.efd_td_workspace_bytes.restype = sz
+        lib.efd_td_workspace_bytes.argtypes = [i32, i32]
+        lib.efd_td_modesum.restype = ctypes.c_int
+        lib.efd_td_modesum.argtypes = [ctypes.POINTER(TdArgs), vp, sz, vp]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int

@@ -73,6 +73,18 @@ constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
 constexpr double INV_SQRT_3_2PI = 1.44720250911653531871; // sqrt(2 pi / 3)
 
+// Fast-path series length: FAST_J terms of each of R and I/w, exact (truncation < 1e-17) for
+// |y| >= FAST_Y (kfactor_slow's bands: J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48).
+#ifndef EFD_FAST_J
+#define EFD_FAST_J 4
+#endif
+constexpr int FAST_J = EFD_FAST_J;
+constexpr double FAST_Y = FAST_J <= 3 ? 555.0 : FAST_J == 4 ? 153.0 : FAST_J == 5 ? 75.0 : 48.0;
+static_assert(FAST_J >= 3 && FAST_J <= 6, "fast-path series: 3..6 terms");
+// Truncation after J terms is KB[J] w^(2J) < 1e-17 for |y| >= JSER_Y[J]; k_items picks the
+// smallest J whose bound holds on the whole interval (a lower bound of |y| there).
+__constant__ double JSER_Y[7] = {0.0, 6.0e7, 8.7e3, 570.0, 153.0, 75.0, 48.0};
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -100,14 +112,15 @@ int fail(int code, const std::string& msg) {
 struct __attribute__((aligned(16))) Item {
     double gx;        // left end of the inverse-spline interval (ascending F)
     double ic[4];     // t(g) = ((ic0 u + ic1) u + ic2) u + ic3, u = g - gx
-    double tj, tj1;   // forward interval
+    double tj, dtj;   // forward interval [tj, tj + dtj)
     double ph[4];     // Phi_mn(t) = m Phi_phi + n Phi_r, w = t - tj (scipy PPoly order)
     double fd[3];     // F'(t)
     double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
     double b[2][2][4];  // b[0] = Bp (re, im cubics), b[1] = Bm: sub-branch s reads b[s] for its
                         // own bin and b[1-s] for the mirror
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
-    int32_t pad[2];
+    int32_t jser;     // K_{1/3} series terms the fast path needs on this interval (1..FAST_J)
+    int32_t pad;
 };
 static_assert(sizeof(Item) == 288, "Item must be 288 B");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
@@ -792,7 +805,7 @@ __device__ void build_item(
     }
     const int a = rr[4 * run], sg = rr[4 * run + 2];
     it.tj = t[j];
-    it.tj1 = t[j + 1];
+    it.dtj = t[j + 1] - t[j];
     const double dm = (double)m, dn = (double)n;
     for (int c = 0; c < 4; ++c) {
         const double* ca = coefA + ((size_t)j * 4 + c) * 4 * K + 4 * h;
@@ -817,6 +830,33 @@ __device__ void build_item(
         it.fdd[0] = SQRT_3_2PI * (3.0 * G0);
         it.fdd[1] = SQRT_3_2PI * (2.0 * G1);
         it.fdd[2] = SQRT_3_2PI * G2;
+        // lower bound of |y| = 2 pi |F'|^3 / (3 F''^2) over w in [0, dtj]: min |F'| and max |F''|
+        // of the two quadratics from their end points and vertices (F' changing sign -> 0)
+        const double dt = it.dtj;
+        auto qv = [](double a, double b, double c, double x) { return (a * x + b) * x + c; };
+        const double fa = it.fd[2], fb = qv(it.fd[0], it.fd[1], it.fd[2], dt);
+        double fdmin = fmin(fabs(fa), fabs(fb));
+        if ((fa > 0.0) != (fb > 0.0) || fa == 0.0 || fb == 0.0) fdmin = 0.0;
+        if (it.fd[0] != 0.0) {
+            const double xv = -it.fd[1] / (2.0 * it.fd[0]);
+            if (xv > 0.0 && xv < dt) {
+                const double fv = qv(it.fd[0], it.fd[1], it.fd[2], xv);
+                if ((fv > 0.0) != (fa > 0.0)) fdmin = 0.0;
+                fdmin = fmin(fdmin, fabs(fv));
+            }
+        }
+        double gmax = fmax(fabs(G2), fabs(qv(3.0 * G0, 2.0 * G1, G2, dt)));
+        if (G0 != 0.0) {
+            const double xv = -(2.0 * G1) / (6.0 * G0);
+            if (xv > 0.0 && xv < dt) gmax = fmax(gmax, fabs(qv(3.0 * G0, 2.0 * G1, G2, xv)));
+        }
+        // 10% margin for the rounding of both bounds and of the kernel's own evaluation
+        const double ymin = gmax > 0.0 ? TWO_PI * fdmin * fdmin * fdmin / (3.0 * gmax * gmax) / 1.1
+                                       : INFINITY;
+        int J = FAST_J;
+        for (int jj = 1; jj < FAST_J; ++jj)
+            if (ymin >= JSER_Y[jj]) { J = jj; break; }
+        it.jser = J;
     }
     // g-interval of this record: [x_lo, x_hi), lower end open at the run's first knot
     const double Fj = knotF(f_phi, f_r, m, n, j), Fj1 = knotF(f_phi, f_r, m, n, j + 1);
@@ -1053,24 +1093,27 @@ __constant__ double KC[20] = {
     1.9570621786581614e+22, -4.854832179436167e+24, 1.3621079545263217e+27,
     -4.2915604492858035e+29, 1.5087738952527293e+32};
 
-// Fast-path series length: FAST_J terms of each of R and I/w, exact (truncation < 1e-17) for
-// |y| >= FAST_Y (kfactor_slow's bands: J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48).
-#ifndef EFD_FAST_J
-#define EFD_FAST_J 4
-#endif
-constexpr int FAST_J = EFD_FAST_J;
-constexpr double FAST_Y = FAST_J <= 3 ? 555.0 : FAST_J == 4 ? 153.0 : FAST_J == 5 ? 75.0 : 48.0;
-static_assert(FAST_J >= 3 && FAST_J <= 6, "fast-path series: 3..6 terms");
-__device__ __forceinline__ void kseries_fast(double ww, double& R, double& I) {
+
+
+template <int J>
+__device__ __forceinline__ void kseries(double ww, double& R, double& I) {
+    if (J == 1) {
+        R = 1.0;
+        I = ww * KC[0];
+        return;
+    }
     const double uu = ww * ww;
-    double r = KB[FAST_J - 1], im = KC[FAST_J - 1];
+    double r = KB[J - 1], im = KC[J - 1];
 #pragma unroll
-    for (int j = FAST_J - 2; j >= 0; --j) {
+    for (int j = J - 2; j >= 0; --j) {
         r = fma(r, uu, KB[j]);
         im = fma(im, uu, KC[j]);
     }
     R = r;
     I = ww * im;
+}
+__device__ __forceinline__ void kseries_fast(double ww, double& R, double& I) {
+    kseries<FAST_J>(ww, R, I);
 }
 
 // Ascending-series coefficients of kfactor_slow, c+-_k = 1 / (k! Gamma(k + 1 +- 1/3)) (the
@@ -1202,7 +1245,7 @@ __device__ __forceinline__ double cubic(const double* __restrict__ c, double w) 
 // active lanes the general path must redo (t(g) overshot the record's knot interval, F' = 0, or
 // |y| < FAST_Y in the uniform mode); W is 0 for those and for inactive lanes. Everything is
 // computed unconditionally and masked once (selects, no divergent branches).
-template <int S, int CAUSTIC>
+template <int S, int CAUSTIC, int J>
 __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk, double tfk,
                                          bool act, const double2* __restrict__ sct, double& wr,
                                          double& wi, double& w, bool& need_general) {
@@ -1210,7 +1253,9 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
     const double u = (S ? fk : -fk) - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     w = tt - it->tj;
-    bool good = (tt >= it->tj) & (tt < it->tj1);
+    // 0 <= w < dtj as one unsigned compare of the bit patterns (negative w and NaN fail)
+    bool good = (unsigned long long)__double_as_longlong(w) <
+                (unsigned long long)__double_as_longlong(it->dtj);
     const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
@@ -1226,8 +1271,9 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
         const double a3 = amp * amp * amp;
         const double t3 = fdds * a3;
         const double ww = copysign(t3 * t3, fd);
-        good = good & (fabs(ww) <= 1.0 / FAST_Y);
-        kseries_fast(ww, R, I);
+        // J < FAST_J: the record's |y| bound covers every in-interval lane, no per-lane test
+        if (J == FAST_J) good = good & (fabs(ww) <= 1.0 / FAST_Y);
+        kseries<J>(ww, R, I);
     }
     // W = 0 unless this lane finishes here (the general path adds the others' terms)
     const double a = (act & good) ? amp : 0.0;
@@ -1240,10 +1286,12 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
     need_general = act & !good;
 }
 
-#ifdef EFD_EXP_COUNT
+#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK)
 // record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
 // FAST_Y, |y| < 18.4
 __device__ unsigned long long g_exp_count[16];  // [8..15]: |y| bands of kfactor_slow's J
+__device__ unsigned int g_exp_tile[16384];       // record evaluations per tile (first 16384)
+__device__ unsigned long long g_exp_tclk[16384];  // wall clock (s_memrealtime) per tile
 #endif
 
 // General (cold) path: scipy interval selection for t(g) and the full K_{1/3} evaluation.
@@ -1262,8 +1310,9 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     double ph, fd, fdd;
     ColdEval c;
-    if (tt >= it->tj && tt < it->tj1) {
-        const double w = tt - it->tj;
+    const double wl = tt - it->tj;
+    if (wl >= 0.0 && wl < it->dtj) {
+        const double w = wl;
         for (int q = 0; q < 4; ++q) c.b[q] = cubic(it->b[q >> 1][q & 1], w);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
@@ -1355,7 +1404,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
     __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
-    __shared__ int wcnt[NWAVE];
+    __shared__ int wcnt[(SEGWIN / TILE) * NWAVE];
     __shared__ double2 sctab[SCTAB];   // (sin, cos)(k pi/128) for sincos_tab
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
@@ -1368,6 +1417,9 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
     const int64_t tile = (int64_t)gridDim.x - 1 - lin;
     if (tile >= ntiles) return;
+#ifdef EFD_EXP_TCLK
+    const unsigned long long t_start = wall_clock64();
+#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int ni = nt - 1;
@@ -1430,27 +1482,39 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
         while (nkeys < KEYCAP) {
             if (wdone == wtotal) {                 // need a new window of segments
                 if (win >= nseg) break;
-                // (1) overlap test + ordered compaction
-                nhit = 0;
-                for (int row = 0; row < SEGWIN / TILE; ++row) {
+                // (1) overlap test + ordered compaction: every thread tests its SEGWIN/TILE
+                // segments, one barrier publishes the per-(row, wave) counts
+                constexpr int ROWS = SEGWIN / TILE;
+                unsigned long long bal[ROWS];
+#pragma unroll
+                for (int row = 0; row < ROWS; ++row) {
                     const int sgi = win + row * TILE + tid;
                     bool hit = false;
                     if (sgi < nseg) {
                         const int2 lh = seglh[sgi];
                         hit = lh.y > tlo && lh.x < thi;
                     }
-                    const unsigned long long bal = __ballot(hit);
-                    if (lane == 0) wcnt[wave] = __popcll(bal);
-                    __syncthreads();
+                    bal[row] = __ballot(hit);
+                    if (lane == 0) wcnt[row * NWAVE + wave] = __popcll(bal[row]);
+                }
+                __syncthreads();
+                nhit = 0;
+#pragma unroll
+                for (int row = 0; row < ROWS; ++row) {
                     int before = nhit;
-                    for (int w = 0; w < wave; ++w) before += wcnt[w];
-                    if (hit) {
-                        const unsigned long long below = bal & ((1ull << lane) - 1ull);
-                        hits[before + __popcll(below)] = sgi;
+                    for (int w = 0; w < wave; ++w) before += wcnt[row * NWAVE + w];
+                    if ((bal[row] >> lane) & 1ull) {
+                        const unsigned long long below = bal[row] & ((1ull << lane) - 1ull);
+                        hits[before + __popcll(below)] = win + row * TILE + tid;
                     }
 #pragma unroll
-                    for (int w = 0; w < NWAVE; ++w) nhit += wcnt[w];
-                    __syncthreads();
+                    for (int w = 0; w < NWAVE; ++w) nhit += wcnt[row * NWAVE + w];
+                }
+                __syncthreads();
+                if (nhit == 0) {                   // nothing of this window reaches the tile
+                    win += SEGWIN;
+                    wtotal = wdone = 0;
+                    continue;
                 }
                 win += SEGWIN;
                 // (2) bisect each hit segment for its records reaching into the tile
@@ -1474,22 +1538,29 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                     hcnt[i] = lo - p0;
                 }
                 __syncthreads();
-                // (3) exclusive scan of the counts (serial per thread over a block of hits)
+                // (3) exclusive scan of the counts (serial per thread over a block of hits,
+                // then a wave scan and one barrier for the wave totals)
                 const int hper = (nhit + TILE - 1) / TILE;
                 const int h0 = min(nhit, tid * hper), h1 = min(nhit, h0 + hper);
                 int mine = 0;
                 for (int i = h0; i < h1; ++i) mine += hcnt[i];
-                part[tid] = mine;
-                __syncthreads();
-                for (int o = 1; o < TILE; o <<= 1) {
-                    const int v = tid >= o ? part[tid - o] : 0;
-                    __syncthreads();
-                    part[tid] += v;
-                    __syncthreads();
+                int incl = mine;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
                 }
-                int run_off = part[tid] - mine;
+                if (lane == 63) part[wave] = incl;
+                __syncthreads();
+                int woff = 0, wsum = 0;
+#pragma unroll
+                for (int w = 0; w < NWAVE; ++w) {
+                    woff += w < wave ? part[w] : 0;
+                    wsum += part[w];
+                }
+                int run_off = woff + incl - mine;
                 for (int i = h0; i < h1; ++i) { hoff[i] = run_off; run_off += hcnt[i]; }
-                wtotal = part[TILE - 1];
+                wtotal = wsum;
                 wdone = 0;
                 __syncthreads();
                 continue;
@@ -1547,12 +1618,16 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                     continue;
                 }
 #ifdef EFD_EXP_COUNT
-                if (lane == 0) atomicAdd(&g_exp_count[0], 1ull);
+                if (lane == 0) {
+                    atomicAdd(&g_exp_count[0], 1ull);
+                    if (tile < 16384) atomicAdd(&g_exp_tile[tile], 1u);
+                }
 #endif
                 bool anyneed = false;
                 bool need[BPL];
-                auto body = [&](auto Sc) {
+                auto body = [&](auto Sc, auto Jc) {
                     constexpr int S = decltype(Sc)::value;
+                    constexpr int J = decltype(Jc)::value;
                     const double* xo = &it->b[S][0][0];       // own bin: b[S] (re 0..3, im 4..7)
                     const double* xm = &it->b[1 - S][0][0];   // mirror: b[1-S]
 #pragma unroll
@@ -1560,7 +1635,18 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                         const int32_t k = w_lo + 64 * i + lane;
                         const bool act = (k >= klo) & (k < khi);
                         double wr, wi, w;
-                        spa_fast<S, CAUSTIC>(it, fk[i], tfk[i], act, sctab, wr, wi, w, need[i]);
+                        spa_fast<S, CAUSTIC, J>(it, fk[i], tfk[i], act, sctab, wr, wi, w, need[i]);
+#ifdef EFD_EXP_DOUBLE   // timing experiment: the fast path's marginal cost (evaluated twice)
+                        {
+                            double wr2, wi2, w2;
+                            bool n2;
+                            spa_fast<S, CAUSTIC, J>(it, fk[i] * (1.0 + 1e-17 * wr), tfk[i], act,
+                                                 sctab, wr2, wi2, w2, n2);
+                            wr = 0.5 * (wr + wr2);
+                            wi = 0.5 * (wi + wi2);
+                            w = 0.5 * (w + w2);
+                        }
+#endif
                         anyneed = anyneed | need[i];
                         const double xr = cubic(xo, w), xi = cubic(xo + 4, w);
                         const double zr = PAIRED ? cubic(xm, w) : 0.0;
@@ -1596,8 +1682,23 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                         }
                     }
                 };
-                if (s == 0) body(std::integral_constant<int, 0>{});
-                else body(std::integral_constant<int, 1>{});
+                // wave-uniform dispatch on (S, series length J of the record)
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                auto by_j = [&](auto Sc) {
+                    if (CAUSTIC != EFD_CAUSTIC_UNIFORM) {
+                        body(Sc, std::integral_constant<int, FAST_J>{});
+                        return;
+                    }
+                    switch ((int)rfl((uint32_t)it->jser)) {
+                        case 1: body(Sc, std::integral_constant<int, 1>{}); break;
+                        case 2: body(Sc, std::integral_constant<int, 2>{}); break;
+                        case 3: body(Sc, std::integral_constant<int, 3>{}); break;
+                        default: body(Sc, std::integral_constant<int, FAST_J>{}); break;
+                    }
+                };
+                if (s == 0) by_j(I0{});
+                else by_j(I1{});
             }
             // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
             // barrier that closed it; the barrier below publishes the new stage for chunk c+1
@@ -1653,6 +1754,154 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
             put(km, sm, sk);
             if (km != k) put(k, sk, sm);
         }
+    }
+#ifdef EFD_EXP_TCLK
+    if (threadIdx.x == 0 && tile < 16384)
+        g_exp_tclk[tile] = ((t_start & 0xffffffffull) << 32) | ((wall_clock64() - t_start) & 0xffffffffull);
+#endif
+}
+
+// ----------------------------------------------------------------------------------------
+// K9: TD mode sum (FEW's InterpolatedModeSum [FEW-ext]; the reference's comparison path,
+// check_mode_by_mode.py:85-99, 254-264). Sample-stationary: each
+// thread owns TD_SPL samples t_i = i dt (strided by the block, so loads and stores coalesce).
+// The (m, n) groups of k_group are walked in descending (m, n) order and, per m, summed by
+// Horner's rule in z = e^{-i Phi_r}:
+//   h(t) = - sum_m [ b_m P_m + conj(b_m Q_m) ],   b_m = e^{-i (m Phi_phi + n0 Phi_r)},
+//   P_m = sum_n Bp_mn(t) z^(n - n0),  Q_m = sum_n Bm_mn(t) z^(n - n0),  n0 = min n of m,
+// so a group costs its four amplitude cubics and two complex multiply-adds (20 FP64 FMAs); a
+// sample pays one sin/cos for z and one per distinct m. Bp, Bm are k_group_amp's group
+// amplitudes (they carry -scale Y+ and conj(-scale Y-): hence the leading minus, and the
+// partner term conj(Bm e^{-i Phi}) = scale Y- conj(A) e^{+i Phi}). A gap in n multiplies by z
+// once more per missing n. The knot interval is wave-uniform except in the few waves that
+// straddle a knot; those read the amplitude coefficients per lane.
+// ----------------------------------------------------------------------------------------
+constexpr int TD_THREADS = 256;
+constexpr int TD_SPL = 4;   // samples per thread
+
+// scipy's interval choice: i with t_i <= x < t_{i+1}, clamped to [0, nt - 2]
+__device__ __forceinline__ int knot_interval(const double* __restrict__ t, int nt, double x) {
+    int lo = 0, hi = nt - 1;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (t[mid] <= x) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(TD_THREADS) void k_td_modesum(
+    const double* __restrict__ t, int nt, const double* __restrict__ coefT,
+    const double* __restrict__ coefA, const int32_t* __restrict__ gm,
+    const int32_t* __restrict__ gn, int K, const Header* __restrict__ hdr, double dt,
+    int64_t ns, int accumulate_out, double* __restrict__ out, double* __restrict__ hp,
+    double* __restrict__ hc) {
+    const int64_t s_base = (int64_t)blockIdx.x * (TD_THREADS * TD_SPL) + threadIdx.x;
+    const double t_end = t[nt - 1];
+    const int G = hdr->groups;
+    double w[TD_SPL], pphi[TD_SPL], pr[TD_SPL], zr[TD_SPL], zi[TD_SPL];
+    int jj[TD_SPL];
+    bool valid[TD_SPL];
+    bool any_valid = false;
+#pragma unroll
+    for (int i = 0; i < TD_SPL; ++i) {
+        const int64_t s = s_base + (int64_t)i * TD_THREADS;
+        const double ts = (double)s * dt;
+        valid[i] = s < ns && ts <= t_end;
+        any_valid |= valid[i];
+        // samples past the end share the last interval, keeping the wave uniform there
+        jj[i] = valid[i] ? knot_interval(t, nt, ts) : nt - 2;
+        w[i] = valid[i] ? ts - t[jj[i]] : 0.0;
+        const double* ct = coefT + (size_t)jj[i] * 32;
+        pphi[i] = fma(fma(fma(ct[0], w[i], ct[8]), w[i], ct[16]), w[i], ct[24]);
+        pr[i] = fma(fma(fma(ct[1], w[i], ct[9]), w[i], ct[17]), w[i], ct[25]);
+        double sn, cs;
+        sincos_big(pr[i], sn, cs);
+        zr[i] = cs;
+        zi[i] = -sn;
+    }
+    double Hr[TD_SPL], Hi[TD_SPL];
+#pragma unroll
+    for (int i = 0; i < TD_SPL; ++i) Hr[i] = Hi[i] = 0.0;
+
+    if (__any(any_valid) && G > 0) {
+        const int j0 = (int)rfl((uint32_t)jj[0]);
+        bool same = true;
+#pragma unroll
+        for (int i = 0; i < TD_SPL; ++i) same &= jj[i] == j0;
+        const size_t row = (size_t)4 * 4 * K;   // doubles per interval of coefA
+        auto run = [&](auto UNI) {
+            constexpr bool U = decltype(UNI)::value;
+            double Pr[TD_SPL], Pi[TD_SPL], Qr[TD_SPL], Qi[TD_SPL];
+#pragma unroll
+            for (int i = 0; i < TD_SPL; ++i) Pr[i] = Pi[i] = Qr[i] = Qi[i] = 0.0;
+            auto flush = [&](int m, int n0) {
+#pragma unroll
+                for (int i = 0; i < TD_SPL; ++i) {
+                    double sn, cs;
+                    sincos_big(fma((double)m, pphi[i], (double)n0 * pr[i]), sn, cs);
+                    const double br = cs, bi = -sn;   // b = e^{-i (m Phi_phi + n0 Phi_r)}
+                    // b P + conj(b Q)
+                    Hr[i] += (br * Pr[i] - bi * Pi[i]) + (br * Qr[i] - bi * Qi[i]);
+                    Hi[i] += (br * Pi[i] + bi * Pr[i]) - (br * Qi[i] + bi * Qr[i]);
+                    Pr[i] = Pi[i] = Qr[i] = Qi[i] = 0.0;
+                }
+            };
+            int cur_m = gm[G - 1], nprev = gn[G - 1];
+            for (int g = G - 1; g >= 0; --g) {
+                const int m = gm[g], n = gn[g];
+                int d = nprev - n;
+                if (m != cur_m) {
+                    flush(cur_m, nprev);
+                    cur_m = m;
+                    d = 1;   // P = Q = 0: the Horner step below reduces to P = Bp
+                }
+                nprev = n;
+                for (; d > 1; --d) {   // missing n between two groups of this m
+#pragma unroll
+                    for (int i = 0; i < TD_SPL; ++i) {
+                        const double a = Pr[i], b = Qr[i];
+                        Pr[i] = fma(a, zr[i], -Pi[i] * zi[i]);
+                        Pi[i] = fma(a, zi[i], Pi[i] * zr[i]);
+                        Qr[i] = fma(b, zr[i], -Qi[i] * zi[i]);
+                        Qi[i] = fma(b, zi[i], Qi[i] * zr[i]);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < TD_SPL; ++i) {
+                    const double* ca = coefA + (size_t)(U ? j0 : jj[i]) * row + 4 * g;
+                    const double wi = w[i];
+                    const double bpr = fma(fma(fma(ca[0], wi, ca[4 * K]), wi, ca[8 * K]), wi, ca[12 * K]);
+                    const double bpi = fma(fma(fma(ca[1], wi, ca[4 * K + 1]), wi, ca[8 * K + 1]), wi, ca[12 * K + 1]);
+                    const double bmr = fma(fma(fma(ca[2], wi, ca[4 * K + 2]), wi, ca[8 * K + 2]), wi, ca[12 * K + 2]);
+                    const double bmi = fma(fma(fma(ca[3], wi, ca[4 * K + 3]), wi, ca[8 * K + 3]), wi, ca[12 * K + 3]);
+                    // P = P z + Bp, Q = Q z + Bm
+                    const double a = Pr[i], b = Qr[i];
+                    Pr[i] = fma(a, zr[i], fma(-Pi[i], zi[i], bpr));
+                    Pi[i] = fma(a, zi[i], fma(Pi[i], zr[i], bpi));
+                    Qr[i] = fma(b, zr[i], fma(-Qi[i], zi[i], bmr));
+                    Qi[i] = fma(b, zi[i], fma(Qi[i], zr[i], bmi));
+                }
+            }
+            flush(cur_m, nprev);
+        };
+        if (__all(same)) run(std::integral_constant<bool, true>{});
+        else run(std::integral_constant<bool, false>{});
+    }
+
+    double2* o = reinterpret_cast<double2*>(out);
+#pragma unroll
+    for (int i = 0; i < TD_SPL; ++i) {
+        const int64_t s = s_base + (int64_t)i * TD_THREADS;
+        if (s >= ns) continue;
+        // h = h+ - i hx = -H (zero past the trajectory's end: pad_output)
+        double vr = valid[i] ? -Hr[i] : 0.0, vi = valid[i] ? -Hi[i] : 0.0;
+        if (o) {
+            double2 v = make_double2(vr, vi);
+            if (accumulate_out) { const double2 p = o[s]; v.x += p.x; v.y += p.y; }
+            o[s] = v;
+        }
+        if (hp) hp[s] = accumulate_out ? hp[s] + vr : vr;
+        if (hc) hc[s] = accumulate_out ? hc[s] - vi : -vi;
     }
 }
 
@@ -1768,10 +2017,16 @@ extern "C" {
 
 int efd_version(void) { return EFD_VERSION; }
 
-#ifdef EFD_EXP_COUNT
+#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK)
 int efd_exp_counters(unsigned long long* out) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 16));
+    return EFD_OK;
+}
+int efd_exp_tiles(unsigned int* out, unsigned long long* clk) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_tile), sizeof(unsigned int) * 16384));
+    HIP_TRY(hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_exp_tclk), sizeof(unsigned long long) * 16384));
     return EFD_OK;
 }
 #endif
@@ -1966,6 +2221,90 @@ int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* ev
     if (contributions) *contributions = h.contributions;
     if (evaluations) *evaluations = h.evaluations;
     if (groups) *groups = h.groups;
+    return EFD_OK;
+}
+
+// TD workspace: the FD layout's grouping and spline buffers only (no records, no tile lists)
+struct TdLayout {
+    size_t header, coefA, coefT, kslope, tscratch, gm, gn, gstart, gmem, gamp, total;
+};
+static TdLayout make_td_layout(int32_t nt, int32_t K) {
+    TdLayout L{};
+    const int64_t ni = nt - 1;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
+    L.header = take(sizeof(Header));
+    L.coefA = take(sizeof(double) * ni * 4 * 4 * K);
+    L.coefT = take(sizeof(double) * ni * 4 * 8);
+    L.kslope = take(sizeof(double) * nt * 2);
+    L.tscratch = take(sizeof(double) * nt * 16);
+    L.gm = take(sizeof(int32_t) * K);
+    L.gn = take(sizeof(int32_t) * K);
+    L.gstart = take(sizeof(int32_t) * (K + 1));
+    L.gmem = take(sizeof(int32_t) * K);
+    L.gamp = take(sizeof(double) * nt * 4 * K);
+    L.total = off;
+    return L;
+}
+
+size_t efd_td_workspace_bytes(int32_t nt, int32_t K) {
+    if (nt < 2 || nt > MAX_NT || K <= 0 || K > MAX_K) return 0;
+    return make_td_layout(nt, K).total;
+}
+
+int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!a || !workspace) return fail(EFD_ERR_ARG, "efd_td_modesum: NULL argument");
+    if (!a->t || !a->phi_phi || !a->phi_r || !a->f_phi || !a->f_r || !a->amp || !a->m ||
+        !a->n || !a->ylm_p || !a->ylm_m)
+        return fail(EFD_ERR_ARG, "efd_td_modesum: NULL array");
+    if (!a->out && !a->hp && !a->hc)
+        return fail(EFD_ERR_ARG, "efd_td_modesum: no output (out, hp or hc)");
+    if (a->nt < 2 || a->nt > MAX_NT) return fail(EFD_ERR_ARG, "efd_td_modesum: nt out of range");
+    if (a->K <= 0 || a->K > MAX_K)
+        return fail(EFD_ERR_ARG, "efd_td_modesum: K out of range [1, 8192]");
+    if (a->nsamples <= 0 || a->nsamples > ((int64_t)1 << 40))
+        return fail(EFD_ERR_ARG, "efd_td_modesum: nsamples out of range");
+    if (!(a->dt > 0.0)) return fail(EFD_ERR_ARG, "efd_td_modesum: dt must be > 0");
+    const TdLayout L = make_td_layout(a->nt, a->K);
+    if (workspace_bytes < L.total)
+        return fail(EFD_ERR_WORKSPACE,
+                    "efd_td_modesum: workspace too small (see efd_td_workspace_bytes)");
+    hipStream_t st = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    Header* hdr = (Header*)(ws + L.header);
+    double* coefA = (double*)(ws + L.coefA);
+    double* coefT = (double*)(ws + L.coefT);
+    int32_t* gm = (int32_t*)(ws + L.gm);
+    int32_t* gn = (int32_t*)(ws + L.gn);
+    int32_t* gstart = (int32_t*)(ws + L.gstart);
+    int32_t* gmem = (int32_t*)(ws + L.gmem);
+    double* gamp = (double*)(ws + L.gamp);
+    const int nt = a->nt, K = a->K;
+
+    HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
+    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
+                       hdr);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
+                       a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
+    HIP_TRY(hipGetLastError());
+    // k_prep's first two roles only (trajectory splines, group amplitude splines): the grid
+    // stops before the inverse-spline blocks, which the TD sum does not need
+    const int nb_amp = (4 * K + 63) / 64;
+    hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp), dim3(64), sizeof(double) * 7 * nt, st, a->t,
+                       a->phi_phi, a->phi_r, a->f_phi, a->f_r, gamp, gm, gn, nt, K, nb_amp, coefT,
+                       (double*)(ws + L.kslope), (double*)(ws + L.tscratch), coefA,
+                       (int32_t*)nullptr, (Item*)nullptr, (double*)nullptr, (double*)nullptr, hdr);
+    HIP_TRY(hipGetLastError());
+    const int64_t per_block = (int64_t)TD_THREADS * TD_SPL;
+    const int64_t nblk = (a->nsamples + per_block - 1) / per_block;
+    if (nblk > 0x7fffffffLL) return fail(EFD_ERR_ARG, "efd_td_modesum: too many samples");
+    if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
+    hipLaunchKernelGGL(k_td_modesum, dim3((unsigned)nblk), dim3(TD_THREADS), 0, st, a->t, nt,
+                       coefT, coefA, gm, gn, K, hdr, a->dt, a->nsamples, a->accumulate ? 1 : 0,
+                       a->out, a->hp, a->hc);
+    HIP_TRY(hipGetLastError());
+    if (a->prof_end) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_end, st));
     return EFD_OK;
 }
 

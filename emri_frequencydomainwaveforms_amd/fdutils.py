@@ -5,6 +5,9 @@
     get_fd_windowed(signal, window, window_in_fd=False)            :66-101
     get_fd_waveform_fromFD(waveform_generator, positive_frequency_mask, dt,
                            non_zero_mask=None, window=None, window_in_fd=False)   :105-139
+    get_fft_td_windowed(signal, window, dt)                        :49-64
+    get_fd_waveform_fromTD(waveform_generator, positive_frequency_mask, dt,
+                           non_zero_mask=None, window=None)        :142-178
 
 get_sensitivity interpolates the drivers' PSD table (LISA_Alloc_Sh.txt, shipped here as a data
 file) with a not-a-knot cubic spline, as the reference does with scipy's CubicSpline (:4-5); it
@@ -21,6 +24,10 @@ positive-frequency mask -> optional zeroing outside non_zero_mask. With no windo
 being the f >= 0 suffix of a sorted grid (the drivers' case, emri_pe.py:239-241), `fill` writes
 h+ and hx straight into the rows of a caller's [2][N] buffer (no intermediate copies); the
 Likelihood uses that.
+
+get_fd_waveform_fromTD is the reference's comparison template: the TD generator's [h+, hx]
+(efd_td_modesum on the device), times the window, through rocFFT (torch.fft), shifted and scaled
+by dt, then masked like the FD template.
 """
 
 import os
@@ -128,3 +135,41 @@ class get_fd_waveform_fromFD:
         """
         self.waveform_generator.fill_channels(out, *args, k0=self._suffix_k0, **kwargs)
         return out
+
+
+def get_fft_td_windowed(signal, window, dt):
+    """[fftshift(fft(h+ w)) dt, fftshift(fft(hx w)) dt] on the device (FDutils.py:49-64)."""
+    torch = require_gpu()
+    out = []
+    for x in (signal[0], signal[1]):
+        x = torch.as_tensor(x, device=torch.device("cuda", torch.cuda.current_device()))
+        if window is not None:
+            x = x * torch.as_tensor(window, device=x.device)
+        out.append(torch.fft.fftshift(torch.fft.fft(x.to(torch.complex128))) * dt)
+    return out
+
+
+class get_fd_waveform_fromTD:
+    """DFT of the TD template [ch1, ch2] over the positive frequencies (FDutils.py:142-178)."""
+
+    def __init__(self, waveform_generator, positive_frequency_mask, dt, non_zero_mask=None,
+                 window=None):
+        torch = require_gpu()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.waveform_generator = waveform_generator
+        self.positive_frequency_mask = torch.as_tensor(positive_frequency_mask, device=dev)
+        self.dt = dt
+        self.non_zero_mask = (None if non_zero_mask is None
+                              else torch.as_tensor(non_zero_mask, device=dev))
+        # the reference's default window is ones_like(mask) (:165-166): the identity
+        self.window = None if window is None else torch.as_tensor(window, device=dev)
+
+    def __call__(self, *args, **kwargs):
+        chans = self.waveform_generator(*args, **kwargs)
+        p, c = get_fft_td_windowed(chans, self.window, self.dt)
+        ch1 = p[self.positive_frequency_mask]
+        ch2 = c[self.positive_frequency_mask]
+        if self.non_zero_mask is not None:
+            ch1[~self.non_zero_mask] = 0.0
+            ch2[~self.non_zero_mask] = 0.0
+        return [ch1, ch2]

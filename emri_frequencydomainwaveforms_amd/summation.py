@@ -177,6 +177,103 @@ class ModeSumEngine:
         return out
 
 
+def td_length(T, dt, odd_len=True):
+    """Samples of FEW's padded TD output: the length of the FD grid for the same (T, dt)."""
+    N = int(T * YRSID_SI / dt) + 1
+    if odd_len and N % 2 == 0:
+        N += 1
+    return N
+
+
+class TDEngine:
+    """Owns the workspace of efd_td_modesum (time-domain mode sum) and launches it."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        if not hasattr(self.lib, "efd_td_modesum"):
+            raise _lib.EFDError("libemrifd.so lacks efd_td_modesum: rebuild it")
+        self._ws = None
+
+    def _workspace(self, nt, K, device):
+        torch = _torch()
+        nbytes = int(self.lib.efd_td_workspace_bytes(nt, K))
+        if nbytes == 0:
+            raise _lib.EFDError("efd_td_workspace_bytes rejected the shape")
+        if self._ws is None or self._ws.numel() < nbytes or self._ws.device != device:
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def launch(self, inp, dt, nsamples, out=None, hp=None, hc=None, scale=1.0 + 0.0j,
+               accumulate=False, stream=None, prof_events=(None, None)):
+        """Asynchronous launch. out: float64 view of complex [nsamples] (h = h+ - i hx);
+        hp / hc: real float64 [nsamples]; any of them may be None (not all)."""
+        torch = _torch()
+        dev = inp.t.device
+        ws = self._workspace(inp.nt, inp.K, dev)
+        ptr = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
+        a = _lib.TdArgs(
+            t=inp.t.data_ptr(), phi_phi=inp.phi_phi.data_ptr(), phi_r=inp.phi_r.data_ptr(),
+            f_phi=inp.f_phi.data_ptr(), f_r=inp.f_r.data_ptr(), nt=inp.nt,
+            amp=inp.amp.data_ptr(), m=inp.m.data_ptr(), n=inp.n.data_ptr(),
+            ylm_p=inp.ylm_p.data_ptr(), ylm_m=inp.ylm_m.data_ptr(), K=inp.K,
+            dt=float(dt), nsamples=int(nsamples), scale_re=float(np.real(scale)),
+            scale_im=float(np.imag(scale)), accumulate=1 if accumulate else 0, out=ptr(out),
+            hp=ptr(hp), hc=ptr(hc), prof_begin=prof_events[0], prof_end=prof_events[1])
+        st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(self.lib.efd_td_modesum(a, ws.data_ptr(), ws.numel(), st), "efd_td_modesum",
+                   self.lib)
+        return ws
+
+    def status(self, stream=None):
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        return self.lib.efd_modesum_status(self._ws.data_ptr(), st) == _lib.EFD_OK
+
+    def run(self, inp, dt, nsamples, scale=1.0 + 0.0j, check=True):
+        """Complex h = h+ - i hx (torch complex128 [nsamples] on the GPU)."""
+        torch = _torch()
+        h = torch.empty(int(nsamples), dtype=torch.complex128, device=inp.t.device)
+        self.launch(inp, dt, nsamples, out=torch.view_as_real(h), scale=scale)
+        if check and not self.status():
+            raise _lib.EFDError(f"efd_td_modesum: {_lib.last_error(self.lib)}")
+        return h
+
+
+class TDInterpolatedModeSum:
+    """FEW-compatible TD summation module (`InterpolatedModeSum` [FEW-ext]): the comparison
+    waveform of the reference (td_gen, check_mode_by_mode.py:85-99; Tutorial_FrequencyDomain_
+    Waveforms.ipynb:61-66). Output length is the FD grid's for the same (T, dt, odd_len), so
+    fftshift(fft(h+)) dt lines up with `FDInterpolatedModeSum.frequency` (notebook :187-188)."""
+
+    def __init__(self, pad_output=True, odd_len=True, use_gpu=True, output_type="td", **kwargs):
+        if output_type != "td":
+            raise ValueError("TDInterpolatedModeSum implements output_type='td' only")
+        self.pad_output = pad_output
+        self.odd_len = odd_len
+        self.use_gpu = use_gpu
+        self.output_type = output_type
+        self.engine = TDEngine()
+
+    def waveform(self, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr, n_arr, M, p, e,
+                 dt=10.0, T=1.0, scale=1.0 + 0.0j):
+        """Complex h = h+ - i hx (torch complex128 on the GPU), distance-scaled by `scale`."""
+        om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
+        f_phi = om_phi / (2.0 * np.pi * M * MTSUN_SI)
+        f_r = om_r / (2.0 * np.pi * M * MTSUN_SI)
+        inp = DeviceInputs.from_host(t, teuk_modes, Phi_phi, Phi_r, f_phi, f_r, m_arr, n_arr,
+                                     ylm_p, ylm_m)
+        if self.pad_output:
+            ns = td_length(T, dt, self.odd_len)
+        else:
+            ns = int(np.searchsorted(np.arange(int(t[-1] / dt) + 2) * dt, t[-1], side="right"))
+        return self.engine.run(inp, dt, ns, scale=scale)
+
+    @staticmethod
+    def polarizations(h):
+        """[h+, hx] real (FEW TD list output) from h = h+ - i hx."""
+        return h.real.contiguous(), (-h.imag).contiguous()
+
+
 class FDInterpolatedModeSum:
     """FEW-compatible FD summation module (`create_waveform` of the waveform class)."""
 

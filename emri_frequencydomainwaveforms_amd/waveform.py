@@ -1,4 +1,4 @@
-"""FEW-compatible waveform classes for the FD path.
+"""FEW-compatible waveform classes: the FD path and its TD comparison path.
 
 Call surfaces kept from the reference (so its drivers only change the import line):
   GenerateEMRIWaveform("FastSchwarzschildEccentricFlux",
@@ -26,7 +26,7 @@ import numpy as np
 
 from .amplitude import ModeSelector, RomanAmplitude
 from .constants import Gpc, MRSUN_SI
-from .summation import FDInterpolatedModeSum, require_gpu
+from .summation import FDInterpolatedModeSum, TDInterpolatedModeSum, require_gpu
 from .trajectory import EMRIInspiral
 from .ylm import GetYlms
 
@@ -52,18 +52,21 @@ class FastSchwarzschildEccentricFlux:
     def __init__(self, inspiral_kwargs=None, amplitude_kwargs=None, sum_kwargs=None,
                  Ylm_kwargs=None, use_gpu=False, caustic="uniform", **kwargs):
         sum_kwargs = dict(sum_kwargs or {})
-        if sum_kwargs.get("output_type", "td") != "fd":
-            raise NotImplementedError(
-                "only the frequency-domain summation (sum_kwargs output_type='fd') is built; the "
-                "time-domain InterpolatedModeSum is out of scope for this hot path (SURVEY.md "
-                "section 8f row 3)")
-        sum_kwargs.setdefault("caustic", caustic)
+        # FEW's default output_type is "td" (InterpolatedModeSum); "fd" selects the FD sum
+        self.output_type = sum_kwargs.pop("output_type", "td")
+        if self.output_type not in ("fd", "td"):
+            raise ValueError("sum_kwargs output_type must be 'fd' or 'td'")
         self.use_gpu = use_gpu
         self.inspiral_generator = EMRIInspiral(func="SchwarzEccFlux", **(inspiral_kwargs or {}))
         self.amplitude_generator = RomanAmplitude(**(amplitude_kwargs or {}))
         self.ylm_gen = GetYlms(assume_positive_m=True, **(Ylm_kwargs or {}))
         self.mode_selector = ModeSelector(self.amplitude_generator.m0mask)
-        self.create_waveform = FDInterpolatedModeSum(use_gpu=use_gpu, **sum_kwargs)
+        if self.output_type == "fd":
+            sum_kwargs.setdefault("caustic", caustic)
+            self.create_waveform = FDInterpolatedModeSum(use_gpu=use_gpu, **sum_kwargs)
+        else:
+            sum_kwargs.pop("caustic", None)
+            self.create_waveform = TDInterpolatedModeSum(use_gpu=use_gpu, **sum_kwargs)
         self.last_modes = None
 
     # -- host-side upstream ------------------------------------------------------------------
@@ -101,8 +104,12 @@ class FastSchwarzschildEccentricFlux:
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
                  extra_scale=1.0 + 0.0j, **kwargs):
-        """Complex FD spectrum S = h+ - i hx (torch, on the GPU), distance-scaled."""
+        """Complex FD spectrum S = h+ - i hx (torch, on the GPU), distance-scaled; for
+        output_type "td" the complex time series h = h+ - i hx instead."""
         require_gpu()
+        if self.output_type == "td":
+            return self.time_series(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, dt, T,
+                                    eps, mode_selection, include_minus_m, extra_scale)
         d = self.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
                          mode_selection, include_minus_m)
         K = len(d["m"])
@@ -111,11 +118,28 @@ class FastSchwarzschildEccentricFlux:
                                              d["Phi_phi"], d["Phi_r"], d["m"], d["n"], M, d["p"],
                                              d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale)
 
+    def time_series(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
+                    T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True,
+                    extra_scale=1.0 + 0.0j):
+        """Complex TD waveform h = h+ - i hx at t_i = i dt (torch, on the GPU)."""
+        require_gpu()
+        d = self.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
+                         mode_selection, include_minus_m)
+        K = len(d["m"])
+        scale = complex(extra_scale) * (mu * MRSUN_SI / (dist * Gpc))
+        return self.create_waveform.waveform(d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:],
+                                             d["Phi_phi"], d["Phi_r"], d["m"], d["n"], M, d["p"],
+                                             d["e"], dt=dt, T=T, scale=scale)
+
     def __call__(self, M, mu, p0, e0, theta, phi, dist=1.0, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, show_progress=False, batch_size=-1, mode_selection=None,
                  include_minus_m=True, f_arr=None, mask_positive=False, **kwargs):
-        """FEW FD output: stacked [h+, hx] (2, N) in the source frame."""
+        """FEW output: FD stacked [h+, hx] (2, N) in the source frame; TD complex h."""
         torch = require_gpu()
+        if self.output_type == "td":
+            h = self.time_series(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, dt, T, eps,
+                                 mode_selection, include_minus_m)
+            return h if self.use_gpu else h.cpu().numpy()
         S = self.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, dt, T, eps,
                           mode_selection, include_minus_m, f_arr)
         hp, hc = self.create_waveform.polarizations(S, mask_positive)
@@ -171,9 +195,18 @@ class GenerateEMRIWaveform:
 
     def __call__(self, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
                  Phi_r0, *add_args, mask_positive=False, **kwargs):
+        gen = self.waveform_generator
+        if gen.output_type == "td":
+            # f_arr / mask_positive are FD options; FEW's TD sum has no use for them
+            kwargs.pop("f_arr", None)
+            h = self._spectrum(M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0,
+                               Phi_theta0, Phi_r0, **kwargs)
+            out = list(gen.create_waveform.polarizations(h)) if self.return_list else h
+            if self.use_gpu:
+                return out
+            return [o.cpu().numpy() for o in out] if isinstance(out, list) else out.cpu().numpy()
         S = self._spectrum(M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
                            Phi_r0, **kwargs)
-        gen = self.waveform_generator
         cw = gen.create_waveform
         if self.return_list:
             hp, hc = cw.polarizations(S, mask_positive)

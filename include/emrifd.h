@@ -139,6 +139,49 @@ int efd_modesum_contributions(const void* workspace, int64_t* contributions, voi
 int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* evaluations,
                       int32_t* groups, void* stream);
 
+/* Input of one time-domain mode sum (one waveform). */
+typedef struct efd_td_args {
+    /* sparse trajectory knots, length nt (device); as efd_modesum_args */
+    const double* t;
+    const double* phi_phi;
+    const double* phi_r;
+    const double* f_phi;
+    const double* f_r;
+    int32_t nt;
+    /* harmonics (device); as efd_modesum_args */
+    const double* amp;
+    const int32_t* m;
+    const int32_t* n;
+    const double* ylm_p;
+    const double* ylm_m;
+    int32_t K;
+    /* samples t_i = i dt, 0 <= i < nsamples; zero where t_i > t[nt-1] (FEW pad_output) */
+    double dt;
+    int64_t nsamples;
+    double scale_re, scale_im;  /* h *= scale (complex)                                        */
+    int32_t accumulate;         /* 1: outputs += new values, 0: outputs = new values           */
+    double* out;                /* complex [nsamples] h = h+ - i hx, or NULL                    */
+    double* hp;                 /* real [nsamples] h+, or NULL                                  */
+    double* hc;                 /* real [nsamples] hx, or NULL                                  */
+    void* prof_begin;           /* optional hipEvent_t pair around the TD kernel alone          */
+    void* prof_end;
+} efd_td_args;
+
+/* Bytes of device workspace efd_td_modesum needs for (nt, K); 0 for an invalid shape. */
+size_t efd_td_workspace_bytes(int32_t nt, int32_t K);
+
+/*
+ * Time-domain mode sum <- FEW InterpolatedModeSum, the TD generator the reference compares its
+ * FD waveform against (td_gen: check_mode_by_mode.py:85-99, 254-264; Tutorial_FrequencyDomain_
+ * Waveforms.ipynb:61-66, 184-188):
+ *   h(t_i) = scale * sum_k [ Y+_k A_k(t_i) e^{-i Phi_k(t_i)} + (m_k > 0) Y-_k conj(A_k(t_i))
+ *            e^{+i Phi_k(t_i)} ],  Phi_k = m Phi_phi + n Phi_r,
+ * with not-a-knot cubic splines of A_k, Phi_phi, Phi_r over the knots. Its DFT,
+ * fftshift(fft(h)) dt, is the FD spectrum efd_modesum returns. Asynchronous, allocation-free;
+ * efd_modesum_status works on this workspace too.
+ */
+int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes, void* stream);
+
 /*
  * h+ = (S(f) + conj(S_flip))/2, hx = i (S(f) - conj(S_flip))/2 with S_flip the array reversed
  * (FEW list output). Writes bins [k0, nf) of each (k0 = first bin to keep, e.g. the f >= 0

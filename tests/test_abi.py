@@ -42,13 +42,19 @@ def test_workspace_query_is_host_only():
     assert lib.efd_modesum_workspace_bytes(100, 3000, 6311631) > 0
     assert lib.efd_modesum_workspace_bytes(1, 3000, 100) == 0
     assert lib.efd_modesum_workspace_bytes(2000, 3000, 100) == 0
+    assert lib.efd_td_workspace_bytes(100, 3000) > 0
+    assert lib.efd_td_workspace_bytes(1, 3000) == 0
+    assert lib.efd_td_workspace_bytes(100, 0) == 0
 
 
-def test_struct_layout_matches_c(tmp_path):
-    fields = [f for f, _ in _lib.ModesumArgs._fields_]
+@pytest.mark.parametrize("cname,pycls", [("efd_modesum_args", "ModesumArgs"),
+                                         ("efd_td_args", "TdArgs")])
+def test_struct_layout_matches_c(tmp_path, cname, pycls):
+    cls = getattr(_lib, pycls)
+    fields = [f for f, _ in cls._fields_]
     prog = ["#include <stdio.h>", "#include <stddef.h>", '#include "emrifd.h"', "int main(void){",
-            'printf("%zu\\n", sizeof(efd_modesum_args));']
-    prog += [f'printf("%zu\\n", offsetof(efd_modesum_args, {f}));' for f in fields]
+            f'printf("%zu\\n", sizeof({cname}));']
+    prog += [f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
     prog += ["return 0;}"]
     src = tmp_path / "layout.c"
     src.write_text("\n".join(prog))
@@ -57,9 +63,9 @@ def test_struct_layout_matches_c(tmp_path):
                    check=True)
     out = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
                                           check=True).stdout.split()]
-    assert out[0] == ctypes.sizeof(_lib.ModesumArgs)
+    assert out[0] == ctypes.sizeof(cls)
     for f, off in zip(fields, out[1:]):
-        assert getattr(_lib.ModesumArgs, f).offset == off, f
+        assert getattr(cls, f).offset == off, f
 
 
 def test_no_cpu_fallback_without_gpu():
