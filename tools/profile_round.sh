@@ -14,6 +14,8 @@ timeout -k 10 600 python -m pytest tests -q -m gpu -x > $O/pytest_gpu.log 2>&1 |
 tail -1 $O/pytest_gpu.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 2; }
 cat $O/bench.json
+timeout -k 10 300 python tools/td_vs_fd.py > $O/td_vs_fd.json 2> $O/td_vs_fd.err || { tail -20 $O/td_vs_fd.err; exit 8; }
+cat $O/td_vs_fd.json
 cd /tmp && export TMPDIR=/tmp
 # the same command as the bench line (overlap pipeline): one k_modesum launch per waveform on
 # the sum stream, so the profiled per-launch durations are the quantity the bench reports

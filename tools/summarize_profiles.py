@@ -41,6 +41,8 @@ def main(tag):
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
+    if os.path.exists(os.path.join(src, "td_vs_fd.json")):
+        shutil.copy(os.path.join(src, "td_vs_fd.json"), os.path.join(dst, f"{tag}_td_vs_fd.json"))
     pmc = {}
     ndisp = {}
     for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_valu"):
