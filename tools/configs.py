@@ -1,0 +1,256 @@
+"""Timing of BASELINE.json's other configurations on one MI355X.
+
+    python tools/configs.py [--only 1,3,4,5] [--reps N]
+
+bench.py measures config 2 (the headline line). This tool prints one JSON line per remaining
+configuration, each with two rates:
+
+  device   the hot path alone: host upstream (trajectory, amplitudes, Ylm, mode selection --
+           this repo's stand-ins, NOT FEW physics) prepared beforehand, inputs resident in HBM,
+           HIP-event/synchronised wall time of the device work per waveform;
+  api      the drivers' own call (GenerateEMRIWaveform(...)(*14 params), or Likelihood.get_ll
+           over the walker batch) end to end, host upstream included.
+
+config 1  M=1e6 mu=10 e0=0.35 Tobs=1 yr dt=10 s eps=1e-2 (check_mode_by_mode.py:221-241 plumbing)
+config 3  10x10 grid M = logspace(5, 7), e0 = linspace(0.1, 0.6), mu = 1e-5 M, Tobs=1 yr,
+          eps=1e-2, p0 solved for 0.99 Tobs at every point (check_mode_by_mode.py:200-213)
+config 4  emri_pe.py: nwalkers=16 ntemps=1 injectFD=1 template=fd Tobs=2 eps=1e-2 on the full
+          grid: per proposal half-step B = 8 walkers through Likelihood.get_ll
+          (emri_pe.py:381-414, red_blue.py:149-156); walkers = truth + seeded N(0, sigma)
+          offsets in (ln M, ln mu, p0, e0, Phi_phi0, Phi_r0) (covariance.npy is not shipped
+          to the GPU box; sigma mirrors its scale)
+config 5  downsample=100 (emri_pe.py:322-364 grid), Tobs=4, nwalkers=128 -> B = 64 per
+          half-step, on one GPU (the 8-GPU sharding is parallel.py's, exercised by bench.py
+          --gpus N at round end)
+
+Parity of these configurations against the oracle is tests/test_gpu_configs.py; this tool only
+times (it never imports oracle/).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SUM_KW = dict(pad_output=True, output_type="fd", odd_len=True)
+# injection angles of emri_pe.py:603-617 (qS, phiS, qK, phiK) and dist = 2.4539 Gpc (:612)
+ANGLES = dict(dist=2.4539, qS=0.2, phiS=0.2, qK=0.8, phiK=0.8)
+
+
+def _params(M, mu, p0, e0, Phi_phi0=1.0, Phi_r0=3.0):
+    a = ANGLES
+    return [M, mu, 0.0, p0, e0, 1.0, a["dist"], a["qS"], a["phiS"], a["qK"], a["phiK"],
+            Phi_phi0, 0.0, Phi_r0]
+
+
+def _sync():
+    import torch
+    torch.cuda.synchronize()
+
+
+class PrepareCache:
+    """Memoise the generator's host upstream (prepare) per parameter set, so a second pass over
+    the same walkers times the device work alone. Installed on the instance only."""
+
+    def __init__(self, wg):
+        self.wg = wg
+        self.orig = wg.prepare
+        self.memo = {}
+        self.host_s = 0.0
+        wg.prepare = self
+
+    def __call__(self, *args, **kwargs):
+        key = repr((args, sorted(kwargs.items())))
+        if key not in self.memo:
+            t0 = time.perf_counter()
+            self.memo[key] = self.orig(*args, **kwargs)
+            self.host_s += time.perf_counter() - t0
+        return self.memo[key]
+
+
+def config1(reps):
+    from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
+    from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform
+    T, dt, eps = 1.0, 10.0, 1e-2
+    few = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", sum_kwargs=SUM_KW,
+                               use_gpu=True, return_list=True)
+    p0 = float(get_p_at_t(EMRIInspiral(), 0.99 * T, [1e6, 10.0, 0.0, 0.35, 1.0]))
+    prm = _params(1e6, 10.0, p0, 0.35)
+    kw = dict(T=T, dt=dt, eps=eps)
+    few(*prm, **kw)
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        few(*prm, **kw)
+    _sync()
+    api = (time.perf_counter() - t0) / reps
+    cache = PrepareCache(few.waveform_generator)
+    few(*prm, **kw)
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        few(*prm, **kw)
+    _sync()
+    dev = (time.perf_counter() - t0) / reps
+    nf = len(few.waveform_generator.create_waveform.frequency)
+    K = len(few.waveform_generator.last_modes[0])
+    return {"config": "config1: M=1e6 mu=10 e0=0.35 Tobs=1yr dt=10s eps=1e-2", "p0": p0,
+            "harmonics": K, "N_f": nf, "device_waveforms_per_s": 1.0 / dev,
+            "device_ms": dev * 1e3, "api_waveforms_per_s": 1.0 / api, "api_ms": api * 1e3,
+            "host_upstream_ms": cache.host_s * 1e3,
+            "device_note": "few_gen call with the host upstream memoised: stand-in grouping, "
+                           "splines, records, mode sum, h+/hx split and the [h+, hx] stack"}
+
+
+def config3(reps):
+    import torch
+    import bench
+    from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine
+    Ms = np.logspace(5, 7, 10)
+    e0s = np.linspace(0.1, 0.6, 10)
+    T, dt, eps = 1.0, 10.0, 1e-2
+    t0 = time.perf_counter()
+    ws = [bench.build_workload(T=T, dt=dt, eps=eps, M=M, mu=1e-5 * M, e0=e0)
+          for M in Ms for e0 in e0s]
+    host_s = time.perf_counter() - t0
+    freq = torch.as_tensor(ws[0]["freq"], device="cuda")
+    nf = int(freq.numel())
+    k0 = int(np.searchsorted(ws[0]["freq"], 0.0))
+    inps = [DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
+                                   w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"]) for w in ws]
+    eng = ModeSumEngine()
+    hp = torch.view_as_real(torch.empty(nf - k0, dtype=torch.complex128, device="cuda"))
+    hc = torch.empty_like(hp)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def sweep():
+        for w, inp in zip(ws, inps):
+            eng.launch(inp, freq, None, True, w["prefactor"], stream=st, hp=hp, hc=hc, k0=k0)
+    sweep()
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sweep()
+    _sync()
+    dev = (time.perf_counter() - t0) / reps
+    if not eng.status(st):
+        raise RuntimeError("efd_modesum reported a device error")
+    K = [len(w["m"]) for w in ws]
+    return {"config": "config3: 10x10 grid M=logspace(5,7) e0=linspace(0.1,0.6) mu=1e-5 M "
+                      "Tobs=1yr dt=10s eps=1e-2", "waveforms": len(ws), "N_f": nf,
+            "harmonics_min_max": [min(K), max(K)],
+            "device_waveforms_per_s": len(ws) / dev, "device_ms_per_grid": dev * 1e3,
+            "api_waveforms_per_s": len(ws) / (host_s + dev),
+            "host_upstream_s_per_grid": host_s,
+            "device_note": "100 waveforms back to back on one stream (h+/hx over f >= 0 each), "
+                           "inputs resident; api adds the host stand-in upstream incl. the "
+                           "p0 root solve per point"}
+
+
+def _likelihood_setup(T, eps, downsample, nwalkers, seed=2601996):
+    from emri_frequencydomainwaveforms_amd import fdutils
+    from emri_frequencydomainwaveforms_amd.likelihood import Likelihood
+    from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
+    from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform
+    M, mu, e0, dt = 1e6, 10.0, 0.35, 10.0
+    few = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", sum_kwargs=SUM_KW,
+                               use_gpu=True, return_list=True)
+    p0 = float(get_p_at_t(EMRIInspiral(), 0.99 * T, [M, mu, 0.0, e0, 1.0]))
+    truth = _params(M, mu, p0, e0)
+    kw = dict(T=T, dt=dt, eps=eps)
+    sig = few(*truth, mask_positive=True, **kw)
+    frequency = few.waveform_generator.create_waveform.frequency
+    frequency = frequency.cpu().numpy() if hasattr(frequency, "detach") else np.asarray(frequency)
+    pos = frequency >= 0.0
+    if downsample:
+        # emri_pe.py:333-349: uniform grid to 1.01 x the highest non-zero bin of the injection
+        fixed = frequency[pos]
+        nz = (np.abs(sig[0].cpu().numpy()) > 0)
+        num = int(nz.sum() / downsample)
+        p_freq = np.linspace(0.0, fixed[nz].max() * 1.01, num=num)
+        newfreq = np.hstack((-p_freq[::-1][:-1], p_freq))
+        kw["f_arr"] = newfreq
+        pos = newfreq >= 0.0
+        f_like = newfreq[pos]
+    else:
+        f_like = frequency[pos]
+    gen = fdutils.get_fd_waveform_fromFD(few, pos, dt)
+    like = Likelihood(gen, 2, f_arr=f_like, use_gpu=True)
+    data = gen(*truth, **kw)
+    like.inject_signal(data_stream=data, noise_fn=[fdutils.get_sensitivity] * 2,
+                       noise_kwargs=[{}, {}])
+    rng = np.random.default_rng(seed)
+    B = nwalkers // 2   # red-blue half-step, ntemps = 1
+    walkers = np.tile(np.asarray(truth, dtype=np.float64), (B, 1))
+    sig6 = np.array([1e-6, 1e-6, 1e-5, 1e-6, 1e-3, 1e-3])   # ln M, ln mu, p0, e0, Phi_phi0, Phi_r0
+    z = rng.normal(size=(B, 6)) * sig6
+    walkers[:, 0] *= np.exp(z[:, 0])
+    walkers[:, 1] *= np.exp(z[:, 1])
+    walkers[:, 3] += z[:, 2]
+    walkers[:, 4] += z[:, 3]
+    walkers[:, 11] += z[:, 4]
+    walkers[:, 13] += z[:, 5]
+    walkers[0] = truth            # one walker on the truth: logL = 0 exactly
+    return few, like, walkers, kw, len(f_like)
+
+
+def config_like(name, T, eps, downsample, nwalkers, reps):
+    few, like, walkers, kw, nbins = _likelihood_setup(T, eps, downsample, nwalkers)
+    B = len(walkers)
+    ll = like.get_ll(walkers, **kw)        # warm-up (also the correctness anchor: ll[0] == 0)
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ll = like.get_ll(walkers, **kw)
+    _sync()
+    api = (time.perf_counter() - t0) / reps
+    cache = PrepareCache(few.waveform_generator)
+    like.get_ll(walkers, **kw)
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ll2 = like.get_ll(walkers, **kw)
+    _sync()
+    dev = (time.perf_counter() - t0) / reps
+    return {"config": name, "walkers_per_half_step": B, "N_pos": nbins,
+            "device_loglikes_per_s": B / dev, "device_ms_per_half_step": dev * 1e3,
+            "api_loglikes_per_s": B / api, "api_ms_per_half_step": api * 1e3,
+            "host_upstream_ms_per_walker": cache.host_s / B * 1e3,
+            "ll_truth": float(ll[0]), "ll_min": float(np.min(ll)),
+            "ll_bitwise_repeatable": bool(np.array_equal(ll, ll2)),
+            "device_note": "Likelihood.get_ll over the half-step batch with the host upstream "
+                           "memoised: per walker the FD template written straight into the "
+                           "likelihood buffer + efd_loglike; one host sync per batch"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="1,3,4,5")
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    which = set(args.only.split(","))
+    out = []
+    if "1" in which:
+        out.append(config1(args.reps))
+        print(json.dumps(out[-1]), flush=True)
+    if "3" in which:
+        out.append(config3(args.reps))
+        print(json.dumps(out[-1]), flush=True)
+    if "4" in which:
+        out.append(config_like("config4: emri_pe nwalkers=16 ntemps=1 injectFD=1 template=fd "
+                               "Tobs=2yr eps=1e-2 full grid", 2.0, 1e-2, None, 16, args.reps))
+        print(json.dumps(out[-1]), flush=True)
+    if "5" in which:
+        out.append(config_like("config5: emri_pe downsample=100 Tobs=4yr eps=1e-2 "
+                               "nwalkers=128 (1 GPU)", 4.0, 1e-2, 100, 128, args.reps))
+        print(json.dumps(out[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
