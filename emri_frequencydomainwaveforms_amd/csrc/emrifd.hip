@@ -124,7 +124,11 @@ struct __attribute__((aligned(16))) Item {
 };
 static_assert(sizeof(Item) == 288, "Item must be 288 B");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
-constexpr int NC = (2 * TILE) / PIECES;         // records per LDS stage (two pieces per thread)
+#ifndef EFD_STAGE_ROUNDS
+#define EFD_STAGE_ROUNDS 2
+#endif
+constexpr int ROUNDS = EFD_STAGE_ROUNDS;         // 16-B pieces per thread per LDS stage
+constexpr int NC = (ROUNDS * TILE) / PIECES;     // records per LDS stage
 
 struct Header {
     int64_t contributions;      // C of the last call: (l, m, n) branch x bin pairs (k_items)
@@ -1379,8 +1383,9 @@ __device__ __forceinline__ void accumulate(double wr, double wi, double xr, doub
 // wave w owns the contiguous chunk [tile_base + w*64*BPL, +64*BPL) and lane l its bins
 // chunk + 64 i + l (i < BPL). The tile's list of interval records is sorted in LDS (fixed
 // summation order -> bitwise reproducible), then streamed through a double-buffered LDS stage:
-// the whole workgroup gathers the next NC records with coalesced 16-B loads while the waves
-// evaluate the current NC from LDS (broadcast reads; no dependent global latency in the loop).
+// the whole workgroup streams the next NC records global -> LDS (global_load_lds, 16 B per lane)
+// while the waves evaluate the current NC from LDS (broadcast reads; no dependent global latency
+// in the loop).
 // Each record feeds BPL independent, branch-free evaluations per lane (one per (m, n) group:
 // every l of the group at once); lanes needing the general path get W = 0 there and add their
 // term in a cold block. The sub-branch S of a record is wave-uniform: each S has its own copy of
@@ -1452,24 +1457,27 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
 
-    // staging: a record is PIECES pieces of 16 B; NC records take at most two pieces per thread.
-    // (Plain registers, no lambda-captured arrays: those were demoted to scratch memory.)
-    static_assert(PIECES * NC <= 2 * TILE, "staging assumes at most two 16-B pieces per thread");
-    const int pc0 = tid, pc1 = tid + TILE;
-    const int r0 = pc0 / PIECES, q0 = pc0 % PIECES, r1 = pc1 / PIECES, q1 = pc1 % PIECES;
-    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
-#define EFD_FETCH(c)                                                                          \
+    // staging: a record is PIECES pieces of 16 B; NC records take at most ROUNDS pieces per thread.
+    // The pieces go global -> LDS directly (gfx950 global_load_lds_dwordx4: no VGPR staging,
+    // nothing held across the evaluation loop). The LDS destination of one wave-instruction is
+    // a wave-uniform base + 16 B x lane, so piece p = round * TILE + 64 wave + lane of the chunk
+    // lands at ((uint4*)stage[buf])[p], i.e. record p / PIECES, piece p % PIECES; its global
+    // source is per lane.
+    static_assert(PIECES * NC <= ROUNDS * TILE, "staging: at most ROUNDS 16-B pieces per thread");
+#define EFD_GLDS(c, buf)                                                                      \
     do {                                                                                      \
-        const int e0_ = (c) * NC + r0, e1_ = (c) * NC + r1;                                   \
-        if (r0 < NC && e0_ < cnt)                                                             \
-            pre0 = reinterpret_cast<const uint4*>(items + (keys[e0_] >> 1))[q0];              \
-        if (r1 < NC && e1_ < cnt)                                                             \
-            pre1 = reinterpret_cast<const uint4*>(items + (keys[e1_] >> 1))[q1];              \
-    } while (0)
-#define EFD_STORE(buf)                                                                        \
-    do {                                                                                      \
-        if (r0 < NC) reinterpret_cast<uint4*>(&stage[(buf)][r0])[q0] = pre0;                  \
-        if (r1 < NC) reinterpret_cast<uint4*>(&stage[(buf)][r1])[q1] = pre1;                  \
+        _Pragma("unroll") for (int rd_ = 0; rd_ < ROUNDS; ++rd_) {                            \
+            const int p_ = rd_ * TILE + tid;                                                  \
+            const int r_ = p_ / PIECES, q_ = p_ - r_ * PIECES;                                \
+            if (r_ < NC && (c) * NC + r_ < cnt) {                                             \
+                const uint4* src_ =                                                           \
+                    reinterpret_cast<const uint4*>(items + (keys[(c) * NC + r_] >> 1)) + q_;  \
+                uint4* dst_ = reinterpret_cast<uint4*>(&stage[(buf)][0]) + rd_ * TILE + wave * 64; \
+                __builtin_amdgcn_global_load_lds(                                             \
+                    (__attribute__((address_space(1))) void*)(src_),                          \
+                    (__attribute__((address_space(3))) void*)(dst_), 16, 0, 0);              \
+            }                                                                                 \
+        }                                                                                     \
     } while (0)
 
     int win = 0;        // next segment window
@@ -1595,12 +1603,14 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
         // ---- evaluate the nkeys records in chunks of NC through the double-buffered stage
         const int cnt = nkeys;
         const int nchunk = (cnt + NC - 1) / NC;
-        EFD_FETCH(0);
-        EFD_STORE(0);
+        EFD_GLDS(0, 0);
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's LDS-DMA pieces landed
         __syncthreads();
 
         for (int c = 0; c < nchunk; ++c) {
-            if (c + 1 < nchunk) EFD_FETCH(c + 1);             // loads in flight during the chunk
+            // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
+            // barrier that closed it: its pieces for chunk c+1 stream in during the chunk
+            if (c + 1 < nchunk) EFD_GLDS(c + 1, (c + 1) & 1);
             const int nin = min(NC, cnt - c * NC);
             const Item* stg = stage[c & 1];
             for (int ii = 0; ii < nin; ++ii) {
@@ -1700,15 +1710,13 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                 if (s == 0) by_j(I0{});
                 else by_j(I1{});
             }
-            // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
-            // barrier that closed it; the barrier below publishes the new stage for chunk c+1
-            if (c + 1 < nchunk) EFD_STORE((c + 1) & 1);
+            // retire this wave's LDS-DMA pieces, then the barrier publishes chunk c+1's stage
+            __builtin_amdgcn_s_waitcnt(0x0f70);
             __syncthreads();
         }
         nkeys = 0;
     }
-#undef EFD_FETCH
-#undef EFD_STORE
+#undef EFD_GLDS
 
     // S is written when out != NULL; on a symmetric grid h+ and hx of bins [k0, nf) are written
     // straight from the registers when hp != NULL (the lane holds S(k) and S(nf-1-k), the two
