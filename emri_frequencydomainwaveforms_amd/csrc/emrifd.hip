@@ -1290,6 +1290,83 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
     need_general = act & !good;
 }
 
+// K_{1/3} series with a wave-uniform runtime length J (1..FAST_J): the branches are scalar, and
+// only R, I merge after them.
+__device__ __forceinline__ void kseries_rt(int J, double ww, double& R, double& I) {
+    switch (J) {
+        case 1: kseries<1>(ww, R, I); break;
+        case 2: kseries<2>(ww, R, I); break;
+        case 3: kseries<3>(ww, R, I); break;
+        default: kseries<FAST_J>(ww, R, I); break;
+    }
+}
+
+// spa_fast with the sub-branch and the series length as wave-uniform runtime values: sfk, stfk
+// are +-fk, +-2 pi fk (the sign flipped by one XOR per record), J the record's series length.
+// Same operations in the same order as spa_fast<S, CAUSTIC, J>, so bitwise the same result; one
+// body instead of 2 x 4 compiled copies, so the accumulators stay in place across records (the
+// copies' merge points cost 8 v_mov_b64 per record and the copies 8x the code).
+template <int CAUSTIC>
+__device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double sfk, double stfk,
+                                            int J, bool act, const double2* __restrict__ sct,
+                                            double& wr, double& wi, double& w, bool& need_general) {
+    const double u = sfk - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    w = tt - it->tj;
+    bool good = (unsigned long long)__double_as_longlong(w) <
+                (unsigned long long)__double_as_longlong(it->dtj);
+    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+    const double afd = fabs(fd);
+    good = good & (afd > 0.0);
+    const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
+    const double psi0 = fma(stfk, tt, -ph);
+    const int shift = fd > 0.0 ? 192 : -192;
+    double R = 1.0, I = 0.0;
+    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
+        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        const double a3 = amp * amp * amp;
+        const double t3 = fdds * a3;
+        const double ww = copysign(t3 * t3, fd);
+        good = good & ((J < FAST_J) | (fabs(ww) <= 1.0 / FAST_Y));
+        kseries_rt(J, ww, R, I);
+    }
+    const double a = (act & good) ? amp : 0.0;
+    R *= a;
+    I *= a;
+    double sn, cs;
+    sincos_tab(psi0, shift, sct, sn, cs);
+    wr = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, cs, -I * sn) : R * cs;
+    wi = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, sn, I * cs) : R * sn;
+    need_general = act & !good;
+}
+
+// xor of the sign bit with a wave-uniform mask (0 or 1 << 63)
+__device__ __forceinline__ double sign_xor(double v, unsigned long long m) {
+    return __longlong_as_double(__double_as_longlong(v) ^ (long long)m);
+}
+
+// accumulate<S, PAIRED> with the sub-branch's sign as a runtime mask: own_i gets
+// sg (xr wi + xi wr), mir_i gets -sg (zr wi + zi wr), sg = +1 (S = 0) or -1 (S = 1); the sign is
+// applied to wr, wi once (exact), the products and their order are accumulate's.
+template <bool PAIRED>
+__device__ __forceinline__ void accumulate_rt(unsigned long long sm, double wr, double wi,
+                                              double xr, double xi, double zr, double zi,
+                                              double& own_r, double& own_i, double& mir_r,
+                                              double& mir_i) {
+    const double wis = sign_xor(wi, sm), wrs = sign_xor(wr, sm);
+    own_r = fma(xr, wr, own_r);
+    own_r = fma(-xi, wi, own_r);
+    own_i = fma(xr, wis, own_i);
+    own_i = fma(xi, wrs, own_i);
+    if (PAIRED) {
+        mir_r = fma(zr, wr, mir_r);
+        mir_r = fma(-zi, wi, mir_r);
+        mir_i = fma(-zr, wis, mir_i);
+        mir_i = fma(-zi, wrs, mir_i);
+    }
+}
+
 #if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK)
 // record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
 // FAST_Y, |y| < 18.4
@@ -1406,6 +1483,13 @@ template <bool PAIRED, int CAUSTIC, int BPL>
 // the compiler's unconstrained choice (180 VGPRs, 2 waves) ran 1.33 ms against 1.12 ms
 #ifndef EFD_WAVES_PER_EU
 #define EFD_WAVES_PER_EU 3
+#endif
+// 1: one evaluation body with the sub-branch sign and series length as wave-uniform runtime
+// values (spa_fast_rt); 0: the compile-time (S, J) instantiations (kept for the EFD_EXP_*
+// experiments). Bitwise-identical results and the same speed (1.13 vs 1.15 ms at config 2); the
+// runtime form is 2.3x less code and has no VGPR spills.
+#ifndef EFD_UNIFIED_BODY
+#define EFD_UNIFIED_BODY 1
 #endif
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8))) void k_modesum(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
@@ -1715,8 +1799,53 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
                         default: body(Sc, std::integral_constant<int, FAST_J>{}); break;
                     }
                 };
+#if EFD_UNIFIED_BODY
+                {
+                    // one body: sub-branch sign and series length as wave-uniform values
+                    const unsigned long long sm = s ? 0ull : (1ull << 63);   // S = 0: g = -f
+                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)rfl((uint32_t)it->jser)
+                                                                 : FAST_J;
+                    const double* xo = &it->b[s][0][0];
+                    const double* xm = &it->b[1 - s][0][0];
+                    const unsigned long long am = s ? (1ull << 63) : 0ull;   // accumulate sign
+                    double wr[BPL], wi[BPL], w[BPL];
+#pragma unroll
+                    for (int i = 0; i < BPL; ++i) {
+                        const int32_t k = w_lo + 64 * i + lane;
+                        const bool act = (k >= klo) & (k < khi);
+                        spa_fast_rt<CAUSTIC>(it, sign_xor(fk[i], sm), sign_xor(tfk[i], sm), J,
+                                             act, sctab, wr[i], wi[i], w[i], need[i]);
+                        anyneed = anyneed | need[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < BPL; ++i) {
+                        const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
+                        const double zr = PAIRED ? cubic(xm, w[i]) : 0.0;
+                        const double zi = PAIRED ? cubic(xm + 4, w[i]) : 0.0;
+                        accumulate_rt<PAIRED>(am, wr[i], wi[i], xr, xi, zr, zi, own_r[i],
+                                              own_i[i], mir_r[i], mir_i[i]);
+                    }
+                    if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
+                        const int hg = (int)((key >> 1) / (uint32_t)ni);
+                        const int jr = (int)((key >> 1) - (uint32_t)hg * (uint32_t)ni);
+#pragma unroll
+                        for (int i = 0; i < BPL; ++i) {
+                            if (need[i]) {
+                                const ColdEval ce = spa_general<CAUSTIC>(
+                                    it, sign_xor(fk[i], sm), hg, jr, t, nt, K, gm, gn, coefA,
+                                    coefT);
+                                accumulate_rt<PAIRED>(am, ce.wr, ce.wi, ce.b[2 * s],
+                                                      ce.b[2 * s + 1], ce.b[2 - 2 * s],
+                                                      ce.b[3 - 2 * s], own_r[i], own_i[i],
+                                                      mir_r[i], mir_i[i]);
+                            }
+                        }
+                    }
+                }
+#else
                 if (s == 0) by_j(I0{});
                 else by_j(I1{});
+#endif
             }
             // retire this wave's LDS-DMA pieces, then the barrier publishes chunk c+1's stage
             __builtin_amdgcn_s_waitcnt(0x0f70);
