@@ -143,7 +143,7 @@ static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
-        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, total;
+        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, sctab, total;
     int64_t ntiles, nlanes;
 };
 
@@ -177,6 +177,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.gstart = take(sizeof(int32_t) * (K + 1));
     L.gmem = take(sizeof(int32_t) * K);
     L.gamp = take(sizeof(double) * nt * 4 * K);
+    L.sctab = take(sizeof(double) * 2 * 512);
     L.total = off;
     return L;
 }
@@ -299,8 +300,16 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ marr
                                                 int32_t* __restrict__ gm, int32_t* __restrict__ gn,
                                                 int32_t* __restrict__ gstart,
                                                 int32_t* __restrict__ gmem,
-                                                Header* __restrict__ hdr) {
+                                                Header* __restrict__ hdr,
+                                                double2* __restrict__ sctab_g) {
     __shared__ unsigned long long key[MAX_K];
+    // k_modesum's (sin, cos)(k pi/256) table, computed once per waveform here and copied into
+    // each tile's LDS by LDS-DMA (cheaper than 512 sincospi per tile at small harmonic counts)
+    if (sctab_g != nullptr && threadIdx.x < 512) {
+        double sv, cv;
+        sincospi((double)threadIdx.x / 256.0, &sv, &cv);
+        sctab_g[threadIdx.x] = make_double2(sv, cv);
+    }
     __shared__ int part[1024];
     const int tid = threadIdx.x;
     int P = 1;
@@ -1497,7 +1506,8 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     const int32_t* __restrict__ nsegp, const double* __restrict__ freq, int64_t nf,
     int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,
     const int32_t* __restrict__ gn, const double* __restrict__ t,
-    const double* __restrict__ coefA, const double* __restrict__ coefT, int accumulate_out,
+    const double* __restrict__ coefA, const double* __restrict__ coefT,
+    const double2* __restrict__ sctab_g, int accumulate_out,
     double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
@@ -1522,11 +1532,14 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int ni = nt - 1;
-    for (int k = tid; k < SCTAB; k += TILE) {
-        double sv, cv;
-        sincospi((double)k / (SCTAB / 2), &sv, &cv);   // (sin, cos)(k pi / 256)
-        sctab[k] = make_double2(sv, cv);
-    }
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
+    // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces)
+    static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
+#pragma unroll
+    for (int rd = 0; rd < SCTAB / TILE; ++rd)
+        glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
+               reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
     __syncthreads();
 
     // ---- the tile's record list, built in LDS from the segment table (no global list, no
@@ -1538,7 +1551,6 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     // (segment, then lane order) is fixed, so the result is bitwise reproducible.
     const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
     const int nseg = *nsegp;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
     const int32_t w_hi = w_lo + 64 * BPL;
     double fk[BPL], tfk[BPL];
@@ -2242,6 +2254,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     int32_t* gstart = (int32_t*)(ws + L.gstart);
     int32_t* gmem = (int32_t*)(ws + L.gmem);
     double* gamp = (double*)(ws + L.gamp);
+    double2* sctab_g = (double2*)(ws + L.sctab);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
@@ -2253,7 +2266,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
 
     // K0: (m, n) groups
     hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
-                       hdr);
+                       hdr, sctab_g);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
                        a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
@@ -2307,7 +2320,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh, seginfo,  \
                        nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA, coefT,        \
-                       acc, a->out, a->hp, a->hc, a->k0)
+                       sctab_g, acc, a->out, a->hp, a->hc, a->k0)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
             else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
@@ -2428,7 +2441,7 @@ int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes
 
     HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
     hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
-                       hdr);
+                       hdr, (double2*)nullptr);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
                        a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
