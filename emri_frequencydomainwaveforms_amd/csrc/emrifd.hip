@@ -182,6 +182,11 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     return L;
 }
 
+// rows of scratch / knot data fetched per block ahead of the serial spline recurrences
+#ifndef EFD_SPLINE_PF
+#define EFD_SPLINE_PF 8   // 16: same, 32: slower (k_prep 110 -> 177 us)
+#endif
+
 // ----------------------------------------------------------------------------------------
 // Not-a-knot cubic spline solve (scipy.interpolate.CubicSpline semantics)
 // ----------------------------------------------------------------------------------------
@@ -255,7 +260,7 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
     // back substitution, emitting interval coefficients from the right. CP/DP may live in
     // global memory: they are fetched PF rows at a time (independent loads, one wait per
     // block) so the serial chain does not pay a memory round trip per row.
-    constexpr int PF = 8;
+    constexpr int PF = EFD_SPLINE_PF;
     double xr = X(n - 1), yr = Y(n - 1);
     for (int i0 = n - 2; i0 >= 0; i0 -= PF) {
         double cpb[PF], dpb[PF];
@@ -513,7 +518,7 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
     auto DPs = [&](int i) -> double& { return dpbase[(size_t)i * scratch_stride + q]; };
     // Global loads (y, and DP on the way back) are issued PF rows at a time, ahead of the
     // serial recurrence, so each block of rows waits for memory once.
-    constexpr int PF = 8;
+    constexpr int PF = EFD_SPLINE_PF;
     // forward sweep: dp_i = (r_i - a_i dp_{i-1}) / m_i, r_i from sl_{i-1}, sl_i
     const double y0 = Y(0), y1 = Y(1);
     double yprev = Y(2);

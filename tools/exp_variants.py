@@ -7,7 +7,8 @@
 variant in its own child process, runs config 2's full device pipeline, and prints one JSON line
 per variant: k_modesum ms (HIP events, mean of 5 launches), the spectrum's max deviation from
 the in-tree library's (relative to max|S|), and the EFD_EXP_COUNT counters when compiled in.
-The variant named "base" is the in-tree library.
+The variant named "base" is the in-tree library. EXP_T / EXP_EPS select the workload (default
+config 2: T = 2 yr, eps = 1e-5).
 """
 
 import json
@@ -51,7 +52,8 @@ def child(name, ref_path):
     from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine
 
     caustic = os.environ.get("EXP_CAUSTIC", "uniform")
-    w = bench.build_workload()
+    w = bench.build_workload(T=float(os.environ.get("EXP_T", "2")),
+                             eps=float(os.environ.get("EXP_EPS", "1e-5")))
     inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
                                  w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"])
     freq = torch.as_tensor(w["freq"], device="cuda")
