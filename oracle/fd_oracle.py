@@ -90,7 +90,15 @@ def _kfactor(fdot, fdd, caustic):
         bad = ~np.isfinite(kk)
         if np.any(bad):
             kk = np.where(bad, _kv13_scaled_asymptotic(np.where(bad, arg, 1.0)), kk)
-        return 1j * fdot / np.abs(fdd) * kk * TWO_OVER_SQRT3            # notebook :607-608
+        with np.errstate(invalid="ignore", divide="ignore"):
+            q = 1j * fdot / np.abs(fdd) * kk * TWO_OVER_SQRT3           # notebook :607-608
+        # F'' = 0 exactly (e.g. a linear F on a 2-knot trajectory): |z| = inf, where the
+        # uniform form's limit is the plain SPA factor (the notebook's expression is 0 * inf);
+        # the C restatement and the kernel take the same limit
+        flat = np.asarray(fdd) == 0.0
+        if np.any(flat):
+            q = np.where(flat, _kfactor(fdot, np.where(flat, 1.0, fdd), "spa"), q)
+        return q
     if caustic == "spa":
         return np.exp(1j * np.sign(fdot) * 0.75 * np.pi) / np.sqrt(np.abs(fdot))
     raise ValueError(f"unknown caustic mode {caustic!r}")
