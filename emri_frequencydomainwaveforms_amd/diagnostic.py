@@ -9,8 +9,9 @@ Same arguments, rules and errors as the reference:
   - dt: time-domain signals, rfft * dt with the DC bin dropped (:57-73);
   - df: frequencies (arange(N) + 1) * df (:79-80); f_arr: the given grid (:82-83);
   - PSD: an array (the drivers' usage, emri_pe.py:281-292), or a string naming a sensitivity
-    function; the only one built here is "LISA_Alloc_Sh" / "lisa_alloc" (the drivers' table,
-    FDutils.py:4-5) -- other lisatools curves raise NotImplementedError;
+    function: "cornish_lisa_psd" (the notebooks' mismatch weighting, sensitivity.py) or
+    "LISA_Alloc_Sh" / "lisa_alloc" (the drivers' table, FDutils.py:4-5); other lisatools curves
+    raise NotImplementedError;
     PSD=None raises TypeError exactly like the reference (len() of a float at :97);
   - right-sum rule: x = diff(f) with the first spacing repeated (:97-100); out = 4 sum
     Re(conj(a) b) / PSD * x, or the complex sum with complex=True (:103-110);
@@ -43,14 +44,15 @@ def _as_channels(sig, torch, device):
 
 def _psd_array(PSD, freqs, PSD_args, PSD_kwargs, torch, device):
     if isinstance(PSD, str):
-        from .fdutils import get_sensitivity
-        if PSD not in ("LISA_Alloc_Sh", "lisa_alloc"):
-            raise NotImplementedError(
-                f"sensitivity curve {PSD!r} is not built; pass a PSD array (the reference "
-                "drivers do, emri_pe.py:281-292) or 'LISA_Alloc_Sh'")
         fh = freqs.detach().cpu().numpy() if hasattr(freqs, "detach") else np.asarray(freqs)
-        return torch.as_tensor(get_sensitivity(fh, *PSD_args, **PSD_kwargs), device=device,
-                               dtype=torch.float64)
+        if PSD in ("LISA_Alloc_Sh", "lisa_alloc"):
+            from .fdutils import get_sensitivity
+            vals = get_sensitivity(fh, *PSD_args, **PSD_kwargs)
+        else:   # lisatools' named curves (diagnostic.py:81-82): sensitivity.get_sensitivity
+            from .sensitivity import get_sensitivity
+            with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+                vals = get_sensitivity(fh, PSD, *PSD_args, **PSD_kwargs)
+        return torch.as_tensor(vals, device=device, dtype=torch.float64)
     if PSD is None:
         # the reference evaluates len(1.0) here (diagnostic.py:97) and fails the same way
         raise TypeError("object of type 'float' has no len()")

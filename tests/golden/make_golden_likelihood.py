@@ -113,6 +113,25 @@ def main():
     v0, v1 = FDutils.get_fd_windowed(sig, wfd, window_in_fd=True)
     out["win_fd_infd"] = np.array([v0, v1])
 
+    # ---- lisatools' analytic cornish_lisa_psd (sensitivity.py:1227-1286), the notebooks'
+    # mismatch weighting, and inner products weighted by it by name (diagnostic.py:81-82),
+    # on the positive grid with and without the f = 0 bin (PSD(0) = inf: zero weight there)
+    from lisatools.sensitivity import cornish_lisa_psd, get_sensitivity as lt_sensitivity
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        out["cornish_f"] = fpos
+        out["cornish_psd"] = cornish_lisa_psd(fpos)
+        out["cornish_psd_sky"] = cornish_lisa_psd(fq, sky_averaged=True)
+        out["cornish_asd_q"] = lt_sensitivity(fq, sens_fn="cornish_lisa_psd", return_type="ASD")
+        out["cornish_char_q"] = lt_sensitivity(fq, sens_fn="cornish_lisa_psd",
+                                               return_type="char_strain")
+        out["cornish_ip_norm"] = inner_product(a, b, f_arr=f, PSD="cornish_lisa_psd",
+                                               normalize=True)
+        a0 = [np.concatenate([[1e-20 + 0j], x]) for x in a]
+        b0 = [np.concatenate([[2e-20 + 0j], x]) for x in b]
+        out["cornish_a0"], out["cornish_b0"] = np.array(a0), np.array(b0)
+        out["cornish_ip_f0"] = inner_product(a0, b0, f_arr=fpos, PSD="cornish_lisa_psd",
+                                             normalize=True)
+
     np.savez_compressed(os.path.join(HERE, "likelihood_golden.npz"), **out)
     for k, v in out.items():
         v = np.asarray(v)

@@ -52,6 +52,18 @@ def test_inner_product_and_snr(g):
                                            PSD=g["ipu_psd"]), g["ipu_plain"])
 
 
+def test_inner_product_named_cornish_psd(g):
+    # the notebooks' mismatch call: inner_product(..., normalize=True, PSD="cornish_lisa_psd",
+    # f_arr=freq[freq >= 0]) (Tutorial_FrequencyDomain_Waveforms.ipynb:258-259, 416-417)
+    a, b, f = list(g["ip_a"]), list(g["ip_b"]), g["ip_f"]
+    kw = dict(PSD="cornish_lisa_psd", normalize=True)
+    assert _close(diagnostic.inner_product(a, b, f_arr=f, **kw), g["cornish_ip_norm"])
+    # grid with the f = 0 bin: PSD(0) = inf weighs it zero, the result stays finite
+    v = diagnostic.inner_product(list(g["cornish_a0"]), list(g["cornish_b0"]),
+                                 f_arr=g["cornish_f"], **kw)
+    assert np.isfinite(v) and _close(v, g["cornish_ip_f0"])
+
+
 def test_inner_product_errors(g):
     a, f = list(g["ip_a"]), g["ip_f"]
     with pytest.raises(ValueError):
