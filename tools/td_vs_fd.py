@@ -91,11 +91,20 @@ def main():
     Dw = torch.fft.fftshift(torch.fft.fft(hp_td * win)) * dt
     hp_fd_w = torch.fft.fftshift(torch.fft.fft(torch.fft.ifft(torch.fft.ifftshift(hp_fd)) * win))
     m_hann = mism(Dw[pos], hp_fd_w[pos])
+    # the notebooks' own metric: |1 - inner_product(DFT(TD), FD, normalize=True,
+    # PSD="cornish_lisa_psd", f_arr=freq[freq >= 0])| (Tutorial_FrequencyDomain_Waveforms.ipynb
+    # :258-259 plain, :416-417 Hann-windowed)
+    from emri_frequencydomainwaveforms_amd import diagnostic
+    ipk = dict(PSD="cornish_lisa_psd", f_arr=freq[pos].cpu().numpy(), normalize=True)
+    m_cornish = abs(1.0 - diagnostic.inner_product(D[pos], hp_fd[pos], **ipk))
+    m_cornish_hann = abs(1.0 - diagnostic.inner_product(Dw[pos], hp_fd_w[pos], **ipk))
     out = {"workload": f"config2-shaped: T={args.T} yr dt={dt} s eps={args.eps}",
            "harmonics": int(len(w["m"])), "N": nf,
            "fd_ms": fd_ms, "fd_modesum_kernel_ms": fd_kern,
            "td_ms": td_ms, "td_kernel_ms": td_kern, "td_over_fd": td_ms / fd_ms,
            "mismatch_hplus_plain": m_plain, "mismatch_hplus_hann": m_hann,
+           "mismatch_hplus_cornish_psd": m_cornish,
+           "mismatch_hplus_cornish_psd_hann": m_cornish_hann,
            "static_harmonics_excluded": int(len(w["m"]) - len(sel)),
            "note": "stand-in trajectory/amplitudes (not FEW physics); HIP events, one stream"}
     print(json.dumps(out))
