@@ -105,8 +105,8 @@ def cpu_baseline(w, seconds=15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--caustic", default="uniform", choices=["uniform", "spa"])
     ap.add_argument("--T", type=float, default=2.0)
     ap.add_argument("--eps", type=float, default=1e-5)

@@ -19,7 +19,7 @@ cat $O/td_vs_fd.json
 cd /tmp && export TMPDIR=/tmp
 # the same command as the bench line (overlap pipeline): one k_modesum launch per waveform on
 # the sum stream, so the profiled per-launch durations are the quantity the bench reports
-B="$R/bench.py --no-cpu-baseline --steps 10 --warmup 2"
+B="$R/bench.py --no-cpu-baseline --steps 50 --warmup 5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $B > $O/trace.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_modesum --output-format csv -d $O/pmc_fetch -o run -- python $B > $O/pmc_fetch.log 2>&1 || exit 4
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_modesum --output-format csv -d $O/pmc_write -o run -- python $B > $O/pmc_write.log 2>&1 || exit 5
