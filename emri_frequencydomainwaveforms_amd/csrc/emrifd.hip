@@ -143,7 +143,8 @@ static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
-        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, sctab, total;
+        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, sctab, tkeys, tcnt,
+        total;
     int64_t ntiles, nlanes;
 };
 
@@ -178,6 +179,8 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.gmem = take(sizeof(int32_t) * K);
     L.gamp = take(sizeof(double) * nt * 4 * K);
     L.sctab = take(sizeof(double) * 2 * 512);
+    L.tkeys = take(sizeof(uint32_t) * (size_t)L.ntiles * KEYCAP);   // prebuilt tile lists
+    L.tcnt = take(sizeof(int32_t) * (size_t)L.ntiles);
     L.total = off;
     return L;
 }
@@ -1492,7 +1495,7 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst) {
 // term in a cold block. The sub-branch S of a record is wave-uniform: each S has its own copy of
 // the evaluation (compile-time signs and LDS offsets).
 // ----------------------------------------------------------------------------------------
-template <bool PAIRED, int CAUSTIC, int BPL>
+template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
 // 3 waves per SIMD (<= 168 VGPRs): the LDS footprint allows 3 workgroups per CU anyway, and
 // the compiler's unconstrained choice (180 VGPRs, 2 waves) ran 1.33 ms against 1.12 ms
 #ifndef EFD_WAVES_PER_EU
@@ -1505,6 +1508,12 @@ template <bool PAIRED, int CAUSTIC, int BPL>
 #ifndef EFD_UNIFIED_BODY
 #define EFD_UNIFIED_BODY 1
 #endif
+// 1: the tiles' record lists are built by a lists-only k_modesum instance in the preparation
+// phase (k_tile_lists role) and DMA'd in by the sum; tiles whose list needs more than one
+// KEYCAP pass (tcnt = -1) build it in the sum as before. 0: always in the sum.
+#ifndef EFD_PREBUILT_LISTS
+#define EFD_PREBUILT_LISTS 1
+#endif
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8))) void k_modesum(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
     const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
@@ -1512,7 +1521,8 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,
     const int32_t* __restrict__ gn, const double* __restrict__ t,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
-    const double2* __restrict__ sctab_g, int accumulate_out,
+    const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,
+    int32_t* __restrict__ tcnt, int accumulate_out,
     double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
@@ -1538,14 +1548,31 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     const int lane = tid & 63;
     const int ni = nt - 1;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
-    // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces)
-    static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
+    // Prebuilt record list (LISTS = false with tkeys set): k_tile_lists, launched in the
+    // preparation phase, ran this tile's list build below and stored its keys when they fit in
+    // one KEYCAP pass (tcnt >= 0); they come in by LDS-DMA with the sin/cos table and the build is
+    // skipped. Same keys in the same order, so the sum is bitwise the in-kernel build's.
+    const int pre = (!LISTS && tcnt != nullptr) ? tcnt[tile] : -1;
+    if (pre > 0) {
+        static_assert(KEYCAP % (4 * TILE) == 0, "key copy: whole rounds of 16-B pieces");
 #pragma unroll
-    for (int rd = 0; rd < SCTAB / TILE; ++rd)
-        glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
-               reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
-    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
-    __syncthreads();
+        for (int rd = 0; rd < KEYCAP / (4 * TILE); ++rd) {
+            const int pc = rd * TILE + tid;                     // 16-B piece = 4 keys
+            if (4 * pc < pre)
+                glds16(reinterpret_cast<const uint4*>(tkeys + (size_t)tile * KEYCAP) + pc,
+                       reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
+        }
+    }
+    if (!LISTS) {
+        // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces)
+        static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
+#pragma unroll
+        for (int rd = 0; rd < SCTAB / TILE; ++rd)
+            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
+                   reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+        __syncthreads();
+    }
 
     // ---- the tile's record list, built in LDS from the segment table (no global list, no
     // atomics). Segments are taken in windows of SEGWIN: (1) each thread tests SEGWIN/TILE
@@ -1593,10 +1620,10 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
     int nhit = 0;       // overlapping segments of the current window
     int wtotal = 0;     // keys of the current window
     int wdone = 0;      // keys of the current window already written
-    int nkeys = 0;      // keys waiting in keys[]
+    int nkeys = pre > 0 ? pre : 0;   // keys waiting in keys[]
     while (true) {
         // ---- fill keys[] (block-uniform control flow)
-        while (nkeys < KEYCAP) {
+        while (pre < 0 && nkeys < KEYCAP) {
             if (wdone == wtotal) {                 // need a new window of segments
                 if (win >= nseg) break;
                 // (1) overlap test + ordered compaction: every thread tests its SEGWIN/TILE
@@ -1703,6 +1730,14 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
             nkeys += take;
             wdone += take;
             __syncthreads();
+        }
+        if (LISTS) {
+            // lists-only instance (k_tile_lists): store the first pass when it is the whole list
+            const bool whole = (wdone == wtotal) && (win >= nseg);
+            if (tid == 0) tcnt[tile] = whole ? nkeys : -1;
+            if (whole)
+                for (int i = tid; i < nkeys; i += TILE) tkeys[(size_t)tile * KEYCAP + i] = keys[i];
+            return;
         }
         if (nkeys == 0) break;
 #ifdef EFD_EXP_NOEVAL
@@ -1869,6 +1904,7 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
             __syncthreads();
         }
         nkeys = 0;
+        if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
 
@@ -2260,6 +2296,8 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     int32_t* gmem = (int32_t*)(ws + L.gmem);
     double* gamp = (double*)(ws + L.gamp);
     double2* sctab_g = (double2*)(ws + L.sctab);
+    uint32_t* tkeys = (uint32_t*)(ws + L.tkeys);
+    int32_t* tcnt = (int32_t*)(ws + L.tcnt);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
@@ -2315,6 +2353,26 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
                            blockcnt, nslot, seglh, seginfo, nseg);
     }
     HIP_TRY(hipGetLastError());
+#if EFD_PREBUILT_LISTS
+    // K6: the tiles' record lists (k_modesum's own list build, lists-only instance): moves the
+    // latency-bound build out of the mode sum into the preparation phase, which overlaps the
+    // previous waveform's sum in a two-stream pipeline
+    {
+        const int64_t gq = 8 * XCD_GROUP;
+        const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
+        if (paired)
+            hipLaunchKernelGGL((k_modesum<true, EFD_CAUSTIC_SPA, BPL, true>), grid, block, 0, st,
+                               items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, 0, nullptr,
+                               nullptr, nullptr, (int64_t)0);
+        else
+            hipLaunchKernelGGL((k_modesum<false, EFD_CAUSTIC_SPA, BPL, true>), grid, block, 0, st,
+                               items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, 0, nullptr,
+                               nullptr, nullptr, (int64_t)0);
+        HIP_TRY(hipGetLastError());
+    }
+#endif
     }  // phase 1
     // K8: mode sum
     if (phase & 2) {
@@ -2322,10 +2380,11 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
+        int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
 #define EFD_LAUNCH(P, C)                                                                      \
-    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh, seginfo,  \
-                       nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA, coefT,        \
-                       sctab_g, acc, a->out, a->hp, a->hc, a->k0)
+    hipLaunchKernelGGL((k_modesum<P, C, BPL, false>), grid, block, 0, st, items, ranges, seglh,   \
+                       seginfo, nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA,      \
+                       coefT, sctab_g, tkeys, tcnt_sum, acc, a->out, a->hp, a->hc, a->k0)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
             else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
