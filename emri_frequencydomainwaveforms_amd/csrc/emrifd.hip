@@ -63,7 +63,7 @@ constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds 
 #define EFD_KEYCAP (EFD_TILE >= 256 ? 2048 : 1024)
 #endif
 #ifndef EFD_SEGWIN_F
-#define EFD_SEGWIN_F 4
+#define EFD_SEGWIN_F 1   // 256 segments per window: 4 KB of LDS instead of 16 (4 workgroups/CU)
 #endif
 constexpr int KEYCAP = EFD_KEYCAP;  // record keys per tile pass held in LDS
 constexpr int SEGWIN = EFD_SEGWIN_F * TILE;  // segments examined per window (tile list build)
@@ -1496,10 +1496,12 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst) {
 // the evaluation (compile-time signs and LDS offsets).
 // ----------------------------------------------------------------------------------------
 template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
-// 3 waves per SIMD (<= 168 VGPRs): the LDS footprint allows 3 workgroups per CU anyway, and
-// the compiler's unconstrained choice (180 VGPRs, 2 waves) ran 1.33 ms against 1.12 ms
+// 4 waves per SIMD (<= 128 VGPRs, 19 spilled, all outside the fast path's FMA chains): with
+// 37.6 KB of LDS per workgroup 4 workgroups fit a CU, and the fourth wave hides more FP64
+// latency than the spills cost (config 2: 1.00 ms against 1.09 ms at 3 waves / 147 VGPRs;
+// 5 waves with a one-round stage: 1.07 ms)
 #ifndef EFD_WAVES_PER_EU
-#define EFD_WAVES_PER_EU 3
+#define EFD_WAVES_PER_EU 4
 #endif
 // 1: one evaluation body with the sub-branch sign and series length as wave-uniform runtime
 // values (spa_fast_rt); 0: the compile-time (S, J) instantiations (kept for the EFD_EXP_*
