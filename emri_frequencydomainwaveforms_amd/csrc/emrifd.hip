@@ -1516,7 +1516,7 @@ template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
 #ifndef EFD_PREBUILT_LISTS
 #define EFD_PREBUILT_LISTS 1
 #endif
-__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8))) void k_modesum(
+__device__ __forceinline__ void modesum_tile(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
     const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
     const int32_t* __restrict__ nsegp, const double* __restrict__ freq, int64_t nf,
@@ -1961,6 +1961,35 @@ __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_
 #endif
 }
 
+#define EFD_MODESUM_PARAMS                                                                    \
+    const Item* __restrict__ items, const int4* __restrict__ ranges,                          \
+        const int2* __restrict__ seglh, const int4* __restrict__ seginfo,                     \
+        const int32_t* __restrict__ nsegp, const double* __restrict__ freq, int64_t nf,       \
+        int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,        \
+        const int32_t* __restrict__ gn, const double* __restrict__ t,                         \
+        const double* __restrict__ coefA, const double* __restrict__ coefT,                   \
+        const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,                    \
+        int32_t* __restrict__ tcnt, int accumulate_out, double* __restrict__ out,             \
+        double* __restrict__ hp, double* __restrict__ hc, int64_t k0
+#define EFD_MODESUM_ARGS                                                                      \
+    items, ranges, seglh, seginfo, nsegp, freq, nf, nlanes, ntiles, nt, K, gm, gn, t, coefA,  \
+        coefT, sctab_g, tkeys, tcnt, accumulate_out, out, hp, hc, k0
+
+// K8: the mode sum (one workgroup per tile; prebuilt lists when tcnt is given)
+template <bool PAIRED, int CAUSTIC, int BPL>
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
+void k_modesum(EFD_MODESUM_PARAMS) {
+    modesum_tile<PAIRED, CAUSTIC, BPL, false>(EFD_MODESUM_ARGS);
+}
+
+// K6: the tiles' record lists only (the same build, run in the preparation phase)
+template <bool PAIRED>
+__global__ __launch_bounds__(TILE) void k_tile_lists(EFD_MODESUM_PARAMS) {
+    modesum_tile<PAIRED, EFD_CAUSTIC_SPA, BPL, true>(EFD_MODESUM_ARGS);
+}
+#undef EFD_MODESUM_PARAMS
+#undef EFD_MODESUM_ARGS
+
 // ----------------------------------------------------------------------------------------
 // K9: TD mode sum (FEW's InterpolatedModeSum [FEW-ext]; the reference's comparison path,
 // check_mode_by_mode.py:85-99, 254-264). Sample-stationary: each
@@ -2363,12 +2392,12 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         const int64_t gq = 8 * XCD_GROUP;
         const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
         if (paired)
-            hipLaunchKernelGGL((k_modesum<true, EFD_CAUSTIC_SPA, BPL, true>), grid, block, 0, st,
+            hipLaunchKernelGGL((k_tile_lists<true>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
                                K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, 0, nullptr,
                                nullptr, nullptr, (int64_t)0);
         else
-            hipLaunchKernelGGL((k_modesum<false, EFD_CAUSTIC_SPA, BPL, true>), grid, block, 0, st,
+            hipLaunchKernelGGL((k_tile_lists<false>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
                                K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, 0, nullptr,
                                nullptr, nullptr, (int64_t)0);
@@ -2384,7 +2413,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
         int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
 #define EFD_LAUNCH(P, C)                                                                      \
-    hipLaunchKernelGGL((k_modesum<P, C, BPL, false>), grid, block, 0, st, items, ranges, seglh,   \
+    hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh,          \
                        seginfo, nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA,      \
                        coefT, sctab_g, tkeys, tcnt_sum, acc, a->out, a->hp, a->hc, a->k0)
         if (paired) {
