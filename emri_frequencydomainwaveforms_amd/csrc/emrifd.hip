@@ -116,11 +116,12 @@ struct __attribute__((aligned(16))) Item {
     double ph[4];     // Phi_mn(t) = m Phi_phi + n Phi_r, w = t - tj (scipy PPoly order)
     double fd[3];     // F'(t)
     double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
+    int32_t jser;     // K_{1/3} series terms the fast path needs on this interval (1..FAST_J)
+    int32_t pad;      // b starts 16-B aligned, so its cubics come out of LDS by ds_read_b128
+                      // (8 ds_read2_b64 -> ds_read_b128 per record: k_modesum -3%)
     double b[2][2][4];  // b[0] = Bp (re, im cubics), b[1] = Bm: sub-branch s reads b[s] for its
                         // own bin and b[1-s] for the mirror
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
-    int32_t jser;     // K_{1/3} series terms the fast path needs on this interval (1..FAST_J)
-    int32_t pad;
 };
 static_assert(sizeof(Item) == 288, "Item must be 288 B");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
@@ -1072,7 +1073,9 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     double r = fma(-q, STEP_1, x);
     r = fma(-q, STEP_2, r);
     const int qi = __double2loint(qs);
-    const double2 t = tab[(qi + shift) & (SCTAB - 1)];   // (sin, cos)((q + shift) pi/256)
+    // (sin, cos)((q + shift) pi/256), addressed in bytes: v_lshl_add + v_and
+    const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
+    const double2 t = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
     const double z = r * r;
     const double sr = fma(r * z, fma(z, 8.333333333333333e-03, -1.6666666666666666e-01), r);
     const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), 1.0);
@@ -1080,13 +1083,13 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     c = fma(t.y, cr, -t.x * sr);
 }
 
-// 1/sqrt(x) for finite x > 0 to full double precision: the hardware estimate plus one
-// third-order correction (the OCML sequence without its special-value fix-up, which the
-// callers make unnecessary by masking x <= 0).
+// 1/sqrt(x) for finite x > 0: the hardware estimate plus one Newton (second-order) correction,
+// relative error ~1e-15 (the OCML sequence's third-order step costs one more FP64 operation for
+// the last bits; the SPA amplitude needs no more). The callers mask x <= 0.
 __device__ __forceinline__ double rsqrt_pos(double x) {
     const double y = __builtin_amdgcn_rsq(x);
     const double e = fma(-x * y, y, 1.0);
-    return fma(y * e, fma(e, 0.375, 0.5), y);
+    return fma(y * e, 0.5, y);
 }
 
 // Q factor. The mirror-convention term of one branch is A Y Q e^{i(2 pi g t - Phi)} with
@@ -1319,7 +1322,8 @@ __device__ __forceinline__ void kseries_rt(int J, double ww, double& R, double& 
 }
 
 // spa_fast with the sub-branch and the series length as wave-uniform runtime values: sfk, stfk
-// are +-fk, +-2 pi fk (the sign flipped by one XOR per record), J the record's series length.
+// are g = +-fk, 2 pi g (the tile keeps them signed for the current sub-branch), J the record's
+// series length.
 // Same operations in the same order as spa_fast<S, CAUSTIC, J>, so bitwise the same result; one
 // body instead of 2 x 4 compiled copies, so the accumulators stay in place across records (the
 // copies' merge points cost 8 v_mov_b64 per record and the copies 8x the code).
@@ -1344,44 +1348,21 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
         const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
         const double a3 = amp * amp * amp;
         const double t3 = fdds * a3;
-        const double ww = copysign(t3 * t3, fd);
-        good = good & ((J < FAST_J) | (fabs(ww) <= 1.0 / FAST_Y));
+        // |w|; the sign of F' (w's sign) goes into I through the mask select below, where it
+        // costs one v_bfi instead of a copysign of its own (bitwise the same I: the rounding of
+        // a product is symmetric in sign)
+        const double ww = t3 * t3;
+        good = good & ((J < FAST_J) | (ww <= 1.0 / FAST_Y));
         kseries_rt(J, ww, R, I);
     }
-    const double a = (act & good) ? amp : 0.0;
-    R *= a;
-    I *= a;
+    const double as = (act & good) ? copysign(amp, fd) : 0.0;
+    R *= fabs(as);
+    I *= CAUSTIC == EFD_CAUSTIC_UNIFORM ? as : fabs(as);
     double sn, cs;
     sincos_tab(psi0, shift, sct, sn, cs);
     wr = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, cs, -I * sn) : R * cs;
     wi = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, sn, I * cs) : R * sn;
     need_general = act & !good;
-}
-
-// xor of the sign bit with a wave-uniform mask (0 or 1 << 63)
-__device__ __forceinline__ double sign_xor(double v, unsigned long long m) {
-    return __longlong_as_double(__double_as_longlong(v) ^ (long long)m);
-}
-
-// accumulate<S, PAIRED> with the sub-branch's sign as a runtime mask: own_i gets
-// sg (xr wi + xi wr), mir_i gets -sg (zr wi + zi wr), sg = +1 (S = 0) or -1 (S = 1); the sign is
-// applied to wr, wi once (exact), the products and their order are accumulate's.
-template <bool PAIRED>
-__device__ __forceinline__ void accumulate_rt(unsigned long long sm, double wr, double wi,
-                                              double xr, double xi, double zr, double zi,
-                                              double& own_r, double& own_i, double& mir_r,
-                                              double& mir_i) {
-    const double wis = sign_xor(wi, sm), wrs = sign_xor(wr, sm);
-    own_r = fma(xr, wr, own_r);
-    own_r = fma(-xi, wi, own_r);
-    own_i = fma(xr, wis, own_i);
-    own_i = fma(xi, wrs, own_i);
-    if (PAIRED) {
-        mir_r = fma(zr, wr, mir_r);
-        mir_r = fma(-zi, wi, mir_r);
-        mir_i = fma(-zr, wis, mir_i);
-        mir_i = fma(-zi, wrs, mir_i);
-    }
 }
 
 #if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK)
@@ -1596,6 +1577,16 @@ __device__ __forceinline__ void modesum_tile(
         tfk[i] = TWO_PI * fk[i];
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
+#if EFD_UNIFIED_BODY
+    // Sub-branch sign state (wave-uniform): fk, tfk hold g = -+f, 2 pi g of the sub-branch s_cur
+    // and own_i, mir_i hold sg * (the true sums), sg = -1 for s_cur = 1. A record of the other
+    // sub-branch flips the 4 BPL registers in place (one v_xor each) instead of making signed
+    // copies of fk, tfk, wi, wr for every record (16 VALU per record); negation commutes with
+    // round-to-nearest, so the sums are bitwise those of the signed-copy form.
+    int s_cur = 0;
+#pragma unroll
+    for (int i = 0; i < BPL; ++i) { fk[i] = -fk[i]; tfk[i] = -tfk[i]; }   // s = 0: g = -f
+#endif
 
     // staging: a record is PIECES pieces of 16 B; NC records take at most ROUNDS pieces per thread.
     // The pieces go global -> LDS directly (gfx950 global_load_lds_dwordx4: no VGPR staging,
@@ -1855,20 +1846,29 @@ __device__ __forceinline__ void modesum_tile(
                 };
 #if EFD_UNIFIED_BODY
                 {
-                    // one body: sub-branch sign and series length as wave-uniform values
-                    const unsigned long long sm = s ? 0ull : (1ull << 63);   // S = 0: g = -f
+                    // one body: sub-branch sign (the register state above) and series length as
+                    // wave-uniform values
+                    if (s != s_cur) {
+#pragma unroll
+                        for (int i = 0; i < BPL; ++i) {
+                            fk[i] = -fk[i];
+                            tfk[i] = -tfk[i];
+                            own_i[i] = -own_i[i];
+                            mir_i[i] = -mir_i[i];
+                        }
+                        s_cur = s;
+                    }
                     const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)rfl((uint32_t)it->jser)
                                                                  : FAST_J;
                     const double* xo = &it->b[s][0][0];
                     const double* xm = &it->b[1 - s][0][0];
-                    const unsigned long long am = s ? (1ull << 63) : 0ull;   // accumulate sign
                     double wr[BPL], wi[BPL], w[BPL];
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t k = w_lo + 64 * i + lane;
                         const bool act = (k >= klo) & (k < khi);
-                        spa_fast_rt<CAUSTIC>(it, sign_xor(fk[i], sm), sign_xor(tfk[i], sm), J,
-                                             act, sctab, wr[i], wi[i], w[i], need[i]);
+                        spa_fast_rt<CAUSTIC>(it, fk[i], tfk[i], J, act, sctab, wr[i], wi[i], w[i],
+                                             need[i]);
                         anyneed = anyneed | need[i];
                     }
 #pragma unroll
@@ -1876,8 +1876,8 @@ __device__ __forceinline__ void modesum_tile(
                         const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
                         const double zr = PAIRED ? cubic(xm, w[i]) : 0.0;
                         const double zi = PAIRED ? cubic(xm + 4, w[i]) : 0.0;
-                        accumulate_rt<PAIRED>(am, wr[i], wi[i], xr, xi, zr, zi, own_r[i],
-                                              own_i[i], mir_r[i], mir_i[i]);
+                        accumulate<0, PAIRED>(wr[i], wi[i], xr, xi, zr, zi, own_r[i], own_i[i],
+                                              mir_r[i], mir_i[i]);
                     }
                     if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
                         const int hg = (int)((key >> 1) / (uint32_t)ni);
@@ -1886,12 +1886,10 @@ __device__ __forceinline__ void modesum_tile(
                         for (int i = 0; i < BPL; ++i) {
                             if (need[i]) {
                                 const ColdEval ce = spa_general<CAUSTIC>(
-                                    it, sign_xor(fk[i], sm), hg, jr, t, nt, K, gm, gn, coefA,
-                                    coefT);
-                                accumulate_rt<PAIRED>(am, ce.wr, ce.wi, ce.b[2 * s],
-                                                      ce.b[2 * s + 1], ce.b[2 - 2 * s],
-                                                      ce.b[3 - 2 * s], own_r[i], own_i[i],
-                                                      mir_r[i], mir_i[i]);
+                                    it, fk[i], hg, jr, t, nt, K, gm, gn, coefA, coefT);
+                                accumulate<0, PAIRED>(ce.wr, ce.wi, ce.b[2 * s], ce.b[2 * s + 1],
+                                                      ce.b[2 - 2 * s], ce.b[3 - 2 * s], own_r[i],
+                                                      own_i[i], mir_r[i], mir_i[i]);
                             }
                         }
                     }
@@ -1909,6 +1907,11 @@ __device__ __forceinline__ void modesum_tile(
         if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
+#if EFD_UNIFIED_BODY
+    if (s_cur)
+#pragma unroll
+        for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
+#endif
 
     // S is written when out != NULL; on a symmetric grid h+ and hx of bins [k0, nf) are written
     // straight from the registers when hp != NULL (the lane holds S(k) and S(nf-1-k), the two

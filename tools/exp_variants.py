@@ -65,7 +65,7 @@ def child(name, ref_path):
     st = torch.cuda.current_stream().cuda_stream
     fS = torch.view_as_real(S)
     ms = []
-    for _ in range(6):
+    for _ in range(int(os.environ.get("EXP_REPS", "6"))):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         b.record()
@@ -84,7 +84,7 @@ def child(name, ref_path):
     if has_cnt:
         cnt = (ctypes.c_ulonglong * 16)()
         lib.efd_exp_counters(cnt)
-        runs = 7  # the counters accumulate over every launch above
+        runs = 1 + int(os.environ.get("EXP_REPS", "6"))  # counters accumulate over every launch
         out["counters_per_launch"] = {k: cnt[i] / runs for i, k in enumerate(
             ("record_evals", "cold_evals", "cold_lanes", "skips", "lanes_overshoot",
              "lanes_y_mid", "lanes_y_small", "unused", "y_ge153", "y_ge75", "y_ge48",
