@@ -68,6 +68,7 @@ constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds 
 constexpr int KEYCAP = EFD_KEYCAP;  // record keys per tile pass held in LDS
 constexpr int SEGWIN = EFD_SEGWIN_F * TILE;  // segments examined per window (tile list build)
 constexpr int MAX_K = 8192;         // harmonics per call (k_group sorts them in LDS)
+constexpr int64_t MAX_LANES = int64_t(1) << 28;   // k_modesum's packed record header
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
@@ -1748,9 +1749,30 @@ __device__ __forceinline__ void modesum_tile(
             // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
             // barrier that closed it: its pieces for chunk c+1 stream in during the chunk
             if (c + 1 < nchunk) EFD_GLDS(c + 1, (c + 1) & 1);
-            const int nin = min(NC, cnt - c * NC);
+            const int nin = (int)rfl((uint32_t)min(NC, cnt - c * NC));   // loop bound in an SGPR
             const Item* stg = stage[c & 1];
+#if EFD_UNIFIED_BODY
+            // the chunk's record headers, one lane per record, read from LDS once per chunk:
+            // hdr_a = klo[s] | s << 28 | jser << 29, hdr_b = khi[s]; each record then takes two
+            // v_readlane instead of an LDS round trip and 5 address / readfirstlane operations
+            static_assert(FAST_J < 8, "header: jser in 3 bits");
+            uint32_t hdr_a = 0, hdr_b = 0;
+            if (lane < nin) {
+                const uint32_t kl = keys[c * NC + lane];
+                const int sl = (int)(kl & 1);
+                const Item* il = stg + lane;
+                hdr_a = (uint32_t)il->klo[sl] | ((uint32_t)sl << 28) | ((uint32_t)il->jser << 29);
+                hdr_b = (uint32_t)il->khi[sl];
+            }
+#endif
             for (int ii = 0; ii < nin; ++ii) {
+#if EFD_UNIFIED_BODY
+                const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane((int)hdr_a, ii);
+                const int s = (int)((ha >> 28) & 1u);
+                const int32_t klo = (int32_t)(ha & 0x0fffffffu);
+                const int32_t khi = __builtin_amdgcn_readlane((int)hdr_b, ii);
+                const Item* it = stg + ii;
+#else
                 const uint32_t key = rfl(keys[c * NC + ii]);
                 // S = 0: g = -f (parent at the own bin, partner at the mirror); S = 1: g = +f
                 // (partner at the own bin, parent at the mirror). Bm is zero for m = 0 groups.
@@ -1758,6 +1780,7 @@ __device__ __forceinline__ void modesum_tile(
                 const Item* it = stg + ii;
                 const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
                 const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
+#endif
                 if (khi <= w_lo || klo >= w_hi) {              // misses this wave's chunk
 #ifdef EFD_EXP_COUNT
                     if (lane == 0) atomicAdd(&g_exp_count[3], 1ull);
@@ -1815,8 +1838,9 @@ __device__ __forceinline__ void modesum_tile(
                             }
                         }
 #endif
-                        const int hg = (int)((key >> 1) / (uint32_t)ni);   // the record's group
-                        const int jr = (int)((key >> 1) - (uint32_t)hg * (uint32_t)ni);   // interval
+                        const uint32_t kc = rfl(keys[c * NC + ii]);
+                        const int hg = (int)((kc >> 1) / (uint32_t)ni);   // the record's group
+                        const int jr = (int)((kc >> 1) - (uint32_t)hg * (uint32_t)ni);   // interval
 #pragma unroll
                         for (int i = 0; i < BPL; ++i) {
                             if (need[i]) {
@@ -1858,8 +1882,7 @@ __device__ __forceinline__ void modesum_tile(
                         }
                         s_cur = s;
                     }
-                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)rfl((uint32_t)it->jser)
-                                                                 : FAST_J;
+                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)(ha >> 29) : FAST_J;
                     const double* xo = &it->b[s][0][0];
                     const double* xm = &it->b[1 - s][0][0];
                     double wr[BPL], wi[BPL], w[BPL];
@@ -1880,6 +1903,7 @@ __device__ __forceinline__ void modesum_tile(
                                               mir_r[i], mir_i[i]);
                     }
                     if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
+                        const uint32_t key = rfl(keys[c * NC + ii]);
                         const int hg = (int)((key >> 1) / (uint32_t)ni);
                         const int jr = (int)((key >> 1) - (uint32_t)hg * (uint32_t)ni);
 #pragma unroll
@@ -2307,6 +2331,8 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         return fail(EFD_ERR_ARG, "efd_modesum: unknown caustic mode");
     const int paired = a->grid_symmetric ? 1 : 0;
     const Layout L = make_layout(a->nt, a->K, a->nf, paired);
+    if (L.nlanes >= MAX_LANES)   // k_modesum packs a record's lane bound into 28 bits
+        return fail(EFD_ERR_ARG, "efd_modesum: more than 2^28 - 1 bins per side of the grid");
     if (workspace_bytes < L.total)
         return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small (see efd_modesum_workspace_bytes)");
 
