@@ -85,3 +85,27 @@ def test_header_constants_match_python():
             continue
         assert hasattr(_lib, name), name
         assert getattr(_lib, name) == int(val), name
+
+
+def test_argument_errors_are_host_side():
+    """Shape errors return EFD_ERR_ARG with a message before anything touches the device, e.g.
+    a grid with more than 2^28 - 1 bins per side (k_modesum packs a record's lane bound into 28
+    bits of its chunk header)."""
+    lib = _lib.load()
+    fake = ctypes.c_void_p(16)   # never dereferenced: validation fails first
+    a = _lib.ModesumArgs()
+    for f in ("t", "phi_phi", "phi_r", "f_phi", "f_r", "amp", "m", "n", "ylm_p", "ylm_m", "freq",
+              "out"):
+        setattr(a, f, fake)
+    a.nt, a.K, a.caustic, a.scale_re = 100, 3000, 1, 1.0
+    a.grid_symmetric = 1
+    buf = ctypes.create_string_buffer(256)
+    a.nf = 2 ** 29 + 1
+    assert lib.efd_modesum(ctypes.byref(a), fake, ctypes.c_size_t(1 << 40), None) == -1
+    lib.efd_last_error(buf, 256)
+    assert b"2^28" in buf.value
+    a.nf = 1000
+    a.nt = 1
+    assert lib.efd_modesum(ctypes.byref(a), fake, ctypes.c_size_t(1 << 40), None) == -1
+    lib.efd_last_error(buf, 256)
+    assert b"nt out of range" in buf.value
