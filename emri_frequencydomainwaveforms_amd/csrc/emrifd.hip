@@ -1366,7 +1366,7 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
     need_general = act & !good;
 }
 
-#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK)
+#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
 // record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
 // FAST_Y, |y| < 18.4
 __device__ unsigned long long g_exp_count[16];  // [8..15]: |y| bands of kfactor_slow's J
@@ -1872,6 +1872,13 @@ __device__ __forceinline__ void modesum_tile(
                 {
                     // one body: sub-branch sign (the register state above) and series length as
                     // wave-uniform values
+#ifdef EFD_EXP_JDIST   // records by series length [0..3], sub-branch flips [4], records [5]
+                    if (lane == 0) {
+                        atomicAdd(&g_exp_count[min((int)(ha >> 29), 4) - 1], 1ull);
+                        atomicAdd(&g_exp_count[5], 1ull);
+                        if (s != s_cur) atomicAdd(&g_exp_count[4], 1ull);
+                    }
+#endif
                     if (s != s_cur) {
 #pragma unroll
                         for (int i = 0; i < BPL; ++i) {
@@ -2273,7 +2280,7 @@ extern "C" {
 
 int efd_version(void) { return EFD_VERSION; }
 
-#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK)
+#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
 int efd_exp_counters(unsigned long long* out) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 16));
