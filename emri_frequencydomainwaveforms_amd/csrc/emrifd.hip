@@ -146,7 +146,7 @@ static_assert(sizeof(Header) == 64, "Header must be 64 B");
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
         seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, sctab, tkeys, tcnt,
-        total;
+        tperm, total;
     int64_t ntiles, nlanes;
 };
 
@@ -183,6 +183,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.sctab = take(sizeof(double) * 2 * 512);
     L.tkeys = take(sizeof(uint32_t) * (size_t)L.ntiles * KEYCAP);   // prebuilt tile lists
     L.tcnt = take(sizeof(int32_t) * (size_t)L.ntiles);
+    L.tperm = take(sizeof(int32_t) * (size_t)L.ntiles);   // cost-ordered dispatch (k_tile_order)
     L.total = off;
     return L;
 }
@@ -1506,7 +1507,7 @@ __device__ __forceinline__ void modesum_tile(
     const int32_t* __restrict__ gn, const double* __restrict__ t,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,
-    int32_t* __restrict__ tcnt, int accumulate_out,
+    int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm, int accumulate_out,
     double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
@@ -1520,11 +1521,20 @@ __device__ __forceinline__ void modesum_tile(
     // of dense (low |f|) and empty (near Nyquist) tiles. The lane order runs from -Nyquist to
     // f = 0, so walking it backwards dispatches the dense band first and the cheap high-|f|
     // tiles last (short tail). The grid is padded to a multiple of 8 * XCD_GROUP.
+    // With a cost order (tperm, k_tile_order) block b takes the b-th most expensive tile instead:
+    // longest-first dispatch, so the launch does not end on expensive tiles started late;
+    // consecutive blocks (similar cost) land on different XCDs.
     const int64_t b = blockIdx.x;
-    const int64_t r = b >> 3, grp = r / XCD_GROUP;
-    const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
-    const int64_t tile = (int64_t)gridDim.x - 1 - lin;
-    if (tile >= ntiles) return;
+    int64_t tile;
+    if (tperm != nullptr) {
+        if (b >= ntiles) return;
+        tile = tperm[b];
+    } else {
+        const int64_t r = b >> 3, grp = r / XCD_GROUP;
+        const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
+        tile = (int64_t)gridDim.x - 1 - lin;
+        if (tile >= ntiles) return;
+    }
 #ifdef EFD_EXP_TCLK
     const unsigned long long t_start = wall_clock64();
 #endif
@@ -2003,11 +2013,11 @@ __device__ __forceinline__ void modesum_tile(
         const int32_t* __restrict__ gn, const double* __restrict__ t,                         \
         const double* __restrict__ coefA, const double* __restrict__ coefT,                   \
         const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,                    \
-        int32_t* __restrict__ tcnt, int accumulate_out, double* __restrict__ out,             \
-        double* __restrict__ hp, double* __restrict__ hc, int64_t k0
+        int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm, int accumulate_out,    \
+        double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0
 #define EFD_MODESUM_ARGS                                                                      \
     items, ranges, seglh, seginfo, nsegp, freq, nf, nlanes, ntiles, nt, K, gm, gn, t, coefA,  \
-        coefT, sctab_g, tkeys, tcnt, accumulate_out, out, hp, hc, k0
+        coefT, sctab_g, tkeys, tcnt, tperm, accumulate_out, out, hp, hc, k0
 
 // K8: the mode sum (one workgroup per tile; prebuilt lists when tcnt is given)
 template <bool PAIRED, int CAUSTIC, int BPL>
@@ -2023,6 +2033,40 @@ __global__ __launch_bounds__(TILE) void k_tile_lists(EFD_MODESUM_PARAMS) {
 }
 #undef EFD_MODESUM_PARAMS
 #undef EFD_MODESUM_ARGS
+
+// K7: dispatch order for the sum, most expensive tiles first (longest-processing-time list
+// scheduling). Cost = the tile's record count from k_tile_lists (tcnt; -1, a list over one
+// KEYCAP pass, is the most expensive class), bucketed at quarter octaves: a counting sort in
+// LDS by one workgroup. The order within a bucket follows LDS atomics and may vary from run to
+// run; it changes only which block runs a tile, never a tile's arithmetic, so the spectrum is
+// bitwise the same in every order.
+constexpr int ORDER_BUCKETS = 64;
+__device__ __forceinline__ int tile_cost_bucket(int32_t c) {
+    if (c < 0) return ORDER_BUCKETS - 1;
+    const float l = __log2f((float)c + 1.0f) * 4.0f;
+    return min((int)l, ORDER_BUCKETS - 2);
+}
+__global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__ tcnt,
+                                                     int64_t ntiles, int32_t* __restrict__ tperm) {
+    __shared__ int hist[ORDER_BUCKETS];
+    const int tid = threadIdx.x;
+    if (tid < ORDER_BUCKETS) hist[tid] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < ntiles; i += 1024) atomicAdd(&hist[tile_cost_bucket(tcnt[i])], 1);
+    __syncthreads();
+    if (tid == 0) {   // exclusive scan, most expensive bucket first
+        int acc = 0;
+        for (int q = ORDER_BUCKETS - 1; q >= 0; --q) { const int h = hist[q]; hist[q] = acc; acc += h; }
+    }
+    __syncthreads();
+    for (int64_t i = tid; i < ntiles; i += 1024) {
+        const int pos = atomicAdd(&hist[tile_cost_bucket(tcnt[i])], 1);
+        tperm[pos] = (int32_t)i;
+    }
+}
+#ifndef EFD_COST_ORDER
+#define EFD_COST_ORDER 1
+#endif
 
 // ----------------------------------------------------------------------------------------
 // K9: TD mode sum (FEW's InterpolatedModeSum [FEW-ext]; the reference's comparison path,
@@ -2430,14 +2474,19 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         if (paired)
             hipLaunchKernelGGL((k_tile_lists<true>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, 0, nullptr,
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, 0, nullptr,
                                nullptr, nullptr, (int64_t)0);
         else
             hipLaunchKernelGGL((k_tile_lists<false>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, 0, nullptr,
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, 0, nullptr,
                                nullptr, nullptr, (int64_t)0);
         HIP_TRY(hipGetLastError());
+#if EFD_COST_ORDER
+        hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
+                           (int32_t*)(ws + L.tperm));
+        HIP_TRY(hipGetLastError());
+#endif
     }
 #endif
     }  // phase 1
@@ -2448,10 +2497,12 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
         int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
+        const int32_t* tperm = (EFD_PREBUILT_LISTS && EFD_COST_ORDER) ? (const int32_t*)(ws + L.tperm)
+                                                                      : nullptr;
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh,          \
                        seginfo, nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA,      \
-                       coefT, sctab_g, tkeys, tcnt_sum, acc, a->out, a->hp, a->hc, a->k0)
+                       coefT, sctab_g, tkeys, tcnt_sum, tperm, acc, a->out, a->hp, a->hc, a->k0)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
             else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);

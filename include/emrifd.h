@@ -115,7 +115,8 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
 /*
  * The same call in two phases on possibly different streams (the caller orders them, e.g. with
  * an event): _prepare runs everything up to the tiles' record lists (grouping, splines,
- * inverse splines, interval records, segment table, per-tile key lists; latency-bound),
+ * inverse splines, interval records, segment table, per-tile key lists and the tiles'
+ * longest-first dispatch order; latency-bound),
  * _sum the mode-sum kernel (reads
  * freq, writes out / hp / hc). With two workspaces, waveform i+1's prepare overlaps waveform
  * i's sum. efd_modesum == _prepare then _sum on one stream.

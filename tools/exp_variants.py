@@ -81,6 +81,34 @@ def child(name, ref_path):
         out["max_rel_dev_vs_base"] = float(np.abs(Sh - R).max() / np.abs(R).max())
     elif name == "base" and ref_path:
         np.save(ref_path, Sh)
+    if has_cnt and os.environ.get("EXP_TCLK"):
+        # per-tile wall clock of the last launch (-DEFD_EXP_TCLK; 100 MHz s_memrealtime ticks):
+        # how much of the launch runs below full tile concurrency (the tail)
+        nt_ = min(int(os.environ["EXP_TCLK"]), 16384)
+        ev = (ctypes.c_uint * 16384)()
+        clk = (ctypes.c_ulonglong * 16384)()
+        lib.efd_exp_tiles(ev, clk)
+        c = np.frombuffer(clk, dtype=np.uint64)[:nt_]
+        st0 = (c >> np.uint64(32)).astype(np.int64)
+        dur = (c & np.uint64(0xffffffff)).astype(np.int64)
+        st0 -= st0.min()
+        en = st0 + dur
+        span = int(en.max())
+        grid = np.arange(0, span + 1, max(span // 400, 1))
+        conc = np.array([int(((st0 <= g) & (en > g)).sum()) for g in grid])
+        full = conc.max()
+        below = grid[conc < 0.5 * full]
+        if os.environ.get("EXP_TCLK_OUT"):
+            np.savez(os.environ["EXP_TCLK_OUT"] + f"_{name}.npz", start=st0, dur=dur,
+                     evals=np.frombuffer(ev, dtype=np.uint32)[:nt_].copy())
+        out["tiles"] = {"n": nt_, "span_us": span / 100.0, "sum_tile_us": float(dur.sum()) / 100.0,
+                        "max_concurrency": int(full),
+                        "mean_tile_us": float(dur.mean()) / 100.0,
+                        "max_tile_us": float(dur.max()) / 100.0,
+                        "p99_tile_us": float(np.percentile(dur, 99)) / 100.0,
+                        "last_start_us": float(st0.max()) / 100.0,
+                        "us_below_half_concurrency": float(len(below) * (grid[1] - grid[0])) / 100.0,
+                        "longest_tiles": [int(i) for i in np.argsort(dur)[-5:]]}
     if has_cnt:
         cnt = (ctypes.c_ulonglong * 16)()
         lib.efd_exp_counters(cnt)
