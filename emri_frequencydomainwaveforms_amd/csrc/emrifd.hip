@@ -1499,6 +1499,11 @@ template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
 #ifndef EFD_PREBUILT_LISTS
 #define EFD_PREBUILT_LISTS 1
 #endif
+// sum dispatch order from k_tile_order: 0 = fixed (f = 0 outward), 1 = tiles longest first,
+// 2 = groups of XCD_GROUP neighbouring tiles longest first
+#ifndef EFD_COST_ORDER
+#define EFD_COST_ORDER 1
+#endif
 __device__ __forceinline__ void modesum_tile(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
     const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
@@ -1527,8 +1532,17 @@ __device__ __forceinline__ void modesum_tile(
     const int64_t b = blockIdx.x;
     int64_t tile;
     if (tperm != nullptr) {
+#if EFD_COST_ORDER == 2
+        // groups of XCD_GROUP neighbouring tiles (shared records stay in one XCD's L2), the
+        // groups in cost order
+        const int64_t r = b >> 3, slot = (r / XCD_GROUP) * 8 + (b & 7);
+        if (slot >= (ntiles + XCD_GROUP - 1) / XCD_GROUP) return;
+        tile = (int64_t)tperm[slot] * XCD_GROUP + r % XCD_GROUP;
+        if (tile >= ntiles) return;
+#else
         if (b >= ntiles) return;
         tile = tperm[b];
+#endif
     } else {
         const int64_t r = b >> 3, grp = r / XCD_GROUP;
         const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
@@ -2052,21 +2066,31 @@ __global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__
     const int tid = threadIdx.x;
     if (tid < ORDER_BUCKETS) hist[tid] = 0;
     __syncthreads();
-    for (int64_t i = tid; i < ntiles; i += 1024) atomicAdd(&hist[tile_cost_bucket(tcnt[i])], 1);
+#if EFD_COST_ORDER == 2
+    // units: groups of XCD_GROUP consecutive tiles, cost = their summed record counts
+    const int64_t nu = (ntiles + XCD_GROUP - 1) / XCD_GROUP;
+    auto ucost = [&](int64_t u) {
+        int32_t c = 0;
+        for (int64_t i = u * XCD_GROUP; i < min((u + 1) * XCD_GROUP, ntiles); ++i)
+            c += tcnt[i] < 0 ? 2 * KEYCAP : tcnt[i];
+        return c;
+    };
+#else
+    const int64_t nu = ntiles;
+    auto ucost = [&](int64_t u) { return tcnt[u]; };
+#endif
+    for (int64_t i = tid; i < nu; i += 1024) atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
     __syncthreads();
     if (tid == 0) {   // exclusive scan, most expensive bucket first
         int acc = 0;
         for (int q = ORDER_BUCKETS - 1; q >= 0; --q) { const int h = hist[q]; hist[q] = acc; acc += h; }
     }
     __syncthreads();
-    for (int64_t i = tid; i < ntiles; i += 1024) {
-        const int pos = atomicAdd(&hist[tile_cost_bucket(tcnt[i])], 1);
+    for (int64_t i = tid; i < nu; i += 1024) {
+        const int pos = atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
         tperm[pos] = (int32_t)i;
     }
 }
-#ifndef EFD_COST_ORDER
-#define EFD_COST_ORDER 1
-#endif
 
 // ----------------------------------------------------------------------------------------
 // K9: TD mode sum (FEW's InterpolatedModeSum [FEW-ext]; the reference's comparison path,
