@@ -1542,6 +1542,7 @@ __device__ __forceinline__ void modesum_tile(
 #else
         if (b >= ntiles) return;
         tile = tperm[b];
+        if ((uint64_t)tile >= (uint64_t)ntiles) return;   // never index past the grid
 #endif
     } else {
         const int64_t r = b >> 3, grp = r / XCD_GROUP;
@@ -2055,6 +2056,10 @@ __global__ __launch_bounds__(TILE) void k_tile_lists(EFD_MODESUM_PARAMS) {
 // run; it changes only which block runs a tile, never a tile's arithmetic, so the spectrum is
 // bitwise the same in every order.
 constexpr int ORDER_BUCKETS = 64;
+// grids whose tiles all fit the resident workgroup slots at once (4 per CU x 256 CUs) start
+// every tile together: no order to choose, so the sort is skipped (config 5's downsampled grid
+// has 43 tiles)
+constexpr int64_t ORDER_MIN_TILES = 1024;
 __device__ __forceinline__ int tile_cost_bucket(int32_t c) {
     if (c < 0) return ORDER_BUCKETS - 1;
     const float l = __log2f((float)c + 1.0f) * 4.0f;
@@ -2079,14 +2084,31 @@ __global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__
     const int64_t nu = ntiles;
     auto ucost = [&](int64_t u) { return tcnt[u]; };
 #endif
-    for (int64_t i = tid; i < nu; i += 1024) atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
+    // the first 16 x 1024 units' buckets stay in registers: one round of independent loads
+    // instead of a dependent load-atomic chain per pass (the sort sits on the preparation
+    // phase's critical path at small harmonic counts)
+    constexpr int PER = 16;
+    int bk[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int64_t i = tid + (int64_t)q * 1024;
+        bk[q] = i < nu ? tile_cost_bucket(ucost(i)) : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if (bk[q] >= 0) atomicAdd(&hist[bk[q]], 1);
+    for (int64_t i = tid + (int64_t)PER * 1024; i < nu; i += 1024)
+        atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
     __syncthreads();
     if (tid == 0) {   // exclusive scan, most expensive bucket first
         int acc = 0;
         for (int q = ORDER_BUCKETS - 1; q >= 0; --q) { const int h = hist[q]; hist[q] = acc; acc += h; }
     }
     __syncthreads();
-    for (int64_t i = tid; i < nu; i += 1024) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if (bk[q] >= 0) tperm[atomicAdd(&hist[bk[q]], 1)] = (int32_t)(tid + q * 1024);
+    for (int64_t i = tid + (int64_t)PER * 1024; i < nu; i += 1024) {
         const int pos = atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
         tperm[pos] = (int32_t)i;
     }
@@ -2507,6 +2529,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
                                nullptr, nullptr, (int64_t)0);
         HIP_TRY(hipGetLastError());
 #if EFD_COST_ORDER
+        if (L.ntiles > ORDER_MIN_TILES)
         hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
                            (int32_t*)(ws + L.tperm));
         HIP_TRY(hipGetLastError());
@@ -2521,8 +2544,8 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
         int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
-        const int32_t* tperm = (EFD_PREBUILT_LISTS && EFD_COST_ORDER) ? (const int32_t*)(ws + L.tperm)
-                                                                      : nullptr;
+        const int32_t* tperm = (EFD_PREBUILT_LISTS && EFD_COST_ORDER && L.ntiles > ORDER_MIN_TILES)
+                                   ? (const int32_t*)(ws + L.tperm) : nullptr;
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh,          \
                        seginfo, nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA,      \
