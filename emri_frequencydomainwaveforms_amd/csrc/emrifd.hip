@@ -36,6 +36,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -75,7 +76,8 @@ constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
 constexpr double INV_SQRT_3_2PI = 1.44720250911653531871; // sqrt(2 pi / 3)
 
 // Fast-path series length: FAST_J terms of each of R and I/w, exact (truncation < 1e-17) for
-// |y| >= FAST_Y (kfactor_slow's bands: J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48).
+// |y| >= FAST_Y (J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48); lanes below FAST_Y take the general
+// path, whose K_{1/3} factor comes from the piecewise-polynomial table of kfactor_table.inc.
 #ifndef EFD_FAST_J
 #define EFD_FAST_J 4
 #endif
@@ -138,7 +140,7 @@ struct Header {
     int32_t runs_overflow;      // set by k_prep when a harmonic has > MAXRUNS monotonic runs
     int32_t groups;             // G: distinct (m, n) of the call (k_group)
     int32_t bad_mn;             // set by k_group when |m| > 255 or |n| > 1023
-    int32_t pad0;
+    int32_t bad_tile;           // set by k_modesum when a dispatch-order entry is out of range
     int64_t pad[4];             // 64 B
 };
 static_assert(sizeof(Header) == 64, "Header must be 64 B");
@@ -1121,6 +1123,43 @@ __constant__ double KC[20] = {
 
 
 
+// G(w) from the table of tools/gen_kfactor_table.py for w = 1/|y| in [2^KTAB_E_LO, 2^KTAB_E_HI)
+// (y > 0; for y < 0 the caller negates I): interval (binade e, quarter k) from the bits of w,
+// local variable x = 8 m - (9 + 2k) in [-1, 1) exact (m = mantissa in [1, 2)), then one Horner
+// chain of KTAB_DEG FMAs each for Re and Im. Max error 1.1e-16 against mpmath. Outside the range
+// the interval index is clamped (callers mask or never get there).
+#include "kfactor_table.inc"
+constexpr double KTAB_WMIN = 0x1p-8, KTAB_WMAX = 0x1p10;
+static_assert(KTAB_E_LO == -8 && KTAB_E_HI == 10, "KTAB_WMIN/WMAX follow the table's range");
+__device__ __forceinline__ void kfactor_tab(double ww, double& R, double& I) {
+    const uint32_t hi = (uint32_t)__double2hiint(ww);
+    const int k = (int)((hi >> 18) & 3u);
+    const int idx = min(max(4 * ((int)(hi >> 20) - 1023 - KTAB_E_LO) + k, 0), KTAB_N - 1);
+    const double m = __hiloint2double((int)((hi & 0x000FFFFFu) | 0x3FF00000u), __double2loint(ww));
+    const double x = fma(8.0, m, -(double)(9 + 2 * k));
+    const double2* c = KTAB[idx];
+    // coefficients in groups of KTAB_GRP pairs: a compiler barrier between groups keeps the
+    // loads from being hoisted all at once (the general path runs inside k_modesum's 128-VGPR
+    // budget)
+    constexpr int KTAB_GRP = 4;
+    static_assert((KTAB_DEG + 1) % KTAB_GRP == 0, "whole coefficient groups");
+    double r = 0.0, im = 0.0;
+#pragma unroll
+    for (int g = KTAB_DEG + 1 - KTAB_GRP; g >= 0; g -= KTAB_GRP) {
+        double2 cc[KTAB_GRP];
+#pragma unroll
+        for (int j = 0; j < KTAB_GRP; ++j) cc[j] = c[g + j];
+#pragma unroll
+        for (int j = KTAB_GRP - 1; j >= 0; --j) {
+            r = fma(r, x, cc[j].x);
+            im = fma(im, x, cc[j].y);
+        }
+        asm volatile("" ::: "memory");
+    }
+    R = r;
+    I = im;
+}
+
 template <int J>
 __device__ __forceinline__ void kseries(double ww, double& R, double& I) {
     if (J == 1) {
@@ -1171,24 +1210,16 @@ __constant__ double ASC_M[42] = {
     5.151509808884057e-96, 3.089670017323505e-99};
 __constant__ int ASC_DEG[19] = {10, 12, 15, 17, 19, 21, 22, 24, 26, 27, 29, 30, 32, 34, 35, 37, 38, 40, 41};
 
-// (R + i I) for |y| < FAST_Y: asymptotic with up to 40 terms down to |y| = 18.4, below that the
+// (R + i I) for |y| < FAST_Y: the table (kfactor_tab) down to |y| = 2^-10, below that the
 // ascending series K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3}) divided by Q_spa.
 __device__ __noinline__ void kfactor_slow(double fd, double fdd, double& R, double& I) {
     const double y = TWO_PI * fd * fd * fd / (3.0 * fdd * fdd);
     const double ay = fabs(y);
-    if (ay >= 18.4) {
-        const double w = 1.0 / y, u = w * w;
-        int J = 20;  // 40 terms
-        if (ay >= 153.0) J = 4; else if (ay >= 75.0) J = 5; else if (ay >= 48.0) J = 6;
-        else if (ay >= 29.4) J = 8; else if (ay >= 23.1) J = 10; else if (ay >= 20.3) J = 12;
-        else if (ay >= 19.0) J = 14; else J = 20;
-        double r = 0.0, im = 0.0;
-        for (int jj = J - 1; jj >= 0; --jj) {
-            r = fma(r, u, KB[jj]);
-            im = fma(im, u, KC[jj]);
-        }
-        R = r;
-        I = w * im;
+    if (ay * KTAB_WMAX > 1.0) {   // |y| > 2^-10: asymptotic series above 256, else the table
+        const double ww = 1.0 / ay;
+        if (ww < KTAB_WMIN) kseries<FAST_J>(ww, R, I);
+        else kfactor_tab(ww, R, I);
+        if (y < 0.0) I = -I;
         return;
     }
     // ascending series for K_{1/3}(z), z = -i y; K~ = K e^{z}: sp, sm = sum_k c+-_k q^k,
@@ -1370,7 +1401,9 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
 #if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
 // record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
 // FAST_Y, |y| < 18.4
-__device__ unsigned long long g_exp_count[16];  // [8..15]: |y| bands of kfactor_slow's J
+__device__ unsigned long long g_exp_count[32];  // [8..15]: |y| bands of kfactor_slow's J;
+// [16, 17]: cold wave evaluations / lanes (one-body kernel); [18..23]: overshoot bands of
+// max(-w, w - dtj) / dtj: < 1e-12, 1e-9, 1e-6, 1e-3, 1e-1, larger
 __device__ unsigned int g_exp_tile[16384];       // record evaluations per tile (first 16384)
 __device__ unsigned long long g_exp_tclk[16384];  // wall clock (s_memrealtime) per tile
 #endif
@@ -1392,8 +1425,13 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
     double ph, fd, fdd;
     ColdEval c;
     const double wl = tt - it->tj;
+#ifdef EFD_EXP_COLD_NOFWD   // timing experiment: no generic forward evaluation
+    if (true) {
+        const double w = fmin(fmax(wl, 0.0), it->dtj);
+#else
     if (wl >= 0.0 && wl < it->dtj) {
         const double w = wl;
+#endif
         for (int q = 0; q < 4; ++q) c.b[q] = cubic(it->b[q >> 1][q & 1], w);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
@@ -1401,6 +1439,12 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
     } else {  // t(g) overshot the record's knot interval: evaluate like scipy
 #ifdef EFD_EXP_COUNT
         atomicAdd(&g_exp_count[4], 1ull);
+        {
+            const double ov = fmax(-wl, wl - it->dtj) / it->dtj;
+            const int band = ov < 1e-12 ? 18 : ov < 1e-9 ? 19 : ov < 1e-6 ? 20 : ov < 1e-3 ? 21
+                           : ov < 1e-1 ? 22 : 23;
+            atomicAdd(&g_exp_count[band], 1ull);
+        }
 #endif
         const FwdEval fe = forward_generic(tt, t, nt, jrec, h, K, gm[h], gn[h], coefA, coefT);
         for (int q = 0; q < 4; ++q) c.b[q] = fe.b[q];
@@ -1425,7 +1469,9 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
                 atomicAdd(&g_exp_count[band], 1ull);
             }
 #endif
+#ifndef EFD_EXP_COLD_NOKF   // timing experiment: no slow K_{1/3} factor
             kfactor_slow(fd, fdd, R, I);
+#endif
         }
     }
     double sn, cs;
@@ -1499,8 +1545,7 @@ template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
 #ifndef EFD_PREBUILT_LISTS
 #define EFD_PREBUILT_LISTS 1
 #endif
-// sum dispatch order from k_tile_order: 0 = fixed (f = 0 outward), 1 = tiles longest first,
-// 2 = groups of XCD_GROUP neighbouring tiles longest first
+// sum dispatch order from k_tile_order: 0 = fixed (f = 0 outward), 1 = tiles longest first
 #ifndef EFD_COST_ORDER
 #define EFD_COST_ORDER 1
 #endif
@@ -1512,8 +1557,9 @@ __device__ __forceinline__ void modesum_tile(
     const int32_t* __restrict__ gn, const double* __restrict__ t,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,
-    int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm, int accumulate_out,
-    double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
+    int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm, Header* __restrict__ hdr,
+    int accumulate_out, double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc,
+    int64_t k0) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -1532,18 +1578,14 @@ __device__ __forceinline__ void modesum_tile(
     const int64_t b = blockIdx.x;
     int64_t tile;
     if (tperm != nullptr) {
-#if EFD_COST_ORDER == 2
-        // groups of XCD_GROUP neighbouring tiles (shared records stay in one XCD's L2), the
-        // groups in cost order
-        const int64_t r = b >> 3, slot = (r / XCD_GROUP) * 8 + (b & 7);
-        if (slot >= (ntiles + XCD_GROUP - 1) / XCD_GROUP) return;
-        tile = (int64_t)tperm[slot] * XCD_GROUP + r % XCD_GROUP;
-        if (tile >= ntiles) return;
-#else
-        if (b >= ntiles) return;
+        if (b >= ntiles) return;   // grid padding
         tile = tperm[b];
-        if ((uint64_t)tile >= (uint64_t)ntiles) return;   // never index past the grid
-#endif
+        if ((uint64_t)tile >= (uint64_t)ntiles) {
+            // a corrupt or stale order entry: never index past the grid, and make
+            // efd_modesum_status report it (the tile's bins would be left unwritten)
+            if (threadIdx.x == 0) hdr->bad_tile = 1;
+            return;
+        }
     } else {
         const int64_t r = b >> 3, grp = r / XCD_GROUP;
         const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
@@ -1934,7 +1976,21 @@ __device__ __forceinline__ void modesum_tile(
                         accumulate<0, PAIRED>(wr[i], wi[i], xr, xi, zr, zi, own_r[i], own_i[i],
                                               mir_r[i], mir_i[i]);
                     }
+#ifdef EFD_EXP_NOSLOW
+                    anyneed = false;
+#endif
                     if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
+#ifdef EFD_EXP_COUNT
+                        {
+                            unsigned long long nl_ = 0;
+#pragma unroll
+                            for (int i = 0; i < BPL; ++i) nl_ += __popcll(__ballot(need[i]));
+                            if (lane == 0) {
+                                atomicAdd(&g_exp_count[16], 1ull);
+                                atomicAdd(&g_exp_count[17], nl_);
+                            }
+                        }
+#endif
                         const uint32_t key = rfl(keys[c * NC + ii]);
                         const int hg = (int)((key >> 1) / (uint32_t)ni);
                         const int jr = (int)((key >> 1) - (uint32_t)hg * (uint32_t)ni);
@@ -2028,11 +2084,12 @@ __device__ __forceinline__ void modesum_tile(
         const int32_t* __restrict__ gn, const double* __restrict__ t,                         \
         const double* __restrict__ coefA, const double* __restrict__ coefT,                   \
         const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,                    \
-        int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm, int accumulate_out,    \
-        double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0
+        int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,                        \
+        Header* __restrict__ hdr, int accumulate_out, double* __restrict__ out,               \
+        double* __restrict__ hp, double* __restrict__ hc, int64_t k0
 #define EFD_MODESUM_ARGS                                                                      \
     items, ranges, seglh, seginfo, nsegp, freq, nf, nlanes, ntiles, nt, K, gm, gn, t, coefA,  \
-        coefT, sctab_g, tkeys, tcnt, tperm, accumulate_out, out, hp, hc, k0
+        coefT, sctab_g, tkeys, tcnt, tperm, hdr, accumulate_out, out, hp, hc, k0
 
 // K8: the mode sum (one workgroup per tile; prebuilt lists when tcnt is given)
 template <bool PAIRED, int CAUSTIC, int BPL>
@@ -2056,14 +2113,29 @@ __global__ __launch_bounds__(TILE) void k_tile_lists(EFD_MODESUM_PARAMS) {
 // run; it changes only which block runs a tile, never a tile's arithmetic, so the spectrum is
 // bitwise the same in every order.
 constexpr int ORDER_BUCKETS = 64;
-// grids whose tiles all fit the resident workgroup slots at once (4 per CU x 256 CUs) start
-// every tile together: no order to choose, so the sort is skipped (config 5's downsampled grid
-// has 43 tiles)
-constexpr int64_t ORDER_MIN_TILES = 1024;
 __device__ __forceinline__ int tile_cost_bucket(int32_t c) {
     if (c < 0) return ORDER_BUCKETS - 1;
     const float l = __log2f((float)c + 1.0f) * 4.0f;
     return min((int)l, ORDER_BUCKETS - 2);
+}
+// Wave-aggregated LDS atomic: the lanes of a wave holding the same bucket take one add by their
+// lowest lane (a tile list's neighbours mostly share a bucket, so one add serves many lanes
+// instead of a contended add per lane); returns the old value plus the lane's rank among them.
+__device__ __forceinline__ int wave_bucket_add(int* hist, int bucket, bool valid) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long todo = __ballot(valid);
+    int res = 0;
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const int bl = __shfl(bucket, leader, 64);
+        const unsigned long long same = __ballot(valid && bucket == bl) & todo;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&hist[bl], __popcll(same));
+        base = __shfl(base, leader, 64);
+        if ((same >> lane) & 1ull) res = base + __popcll(same & ((1ull << lane) - 1ull));
+        todo &= ~same;
+    }
+    return res;
 }
 __global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__ tcnt,
                                                      int64_t ntiles, int32_t* __restrict__ tperm) {
@@ -2071,34 +2143,25 @@ __global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__
     const int tid = threadIdx.x;
     if (tid < ORDER_BUCKETS) hist[tid] = 0;
     __syncthreads();
-#if EFD_COST_ORDER == 2
-    // units: groups of XCD_GROUP consecutive tiles, cost = their summed record counts
-    const int64_t nu = (ntiles + XCD_GROUP - 1) / XCD_GROUP;
-    auto ucost = [&](int64_t u) {
-        int32_t c = 0;
-        for (int64_t i = u * XCD_GROUP; i < min((u + 1) * XCD_GROUP, ntiles); ++i)
-            c += tcnt[i] < 0 ? 2 * KEYCAP : tcnt[i];
-        return c;
-    };
-#else
-    const int64_t nu = ntiles;
-    auto ucost = [&](int64_t u) { return tcnt[u]; };
-#endif
-    // the first 16 x 1024 units' buckets stay in registers: one round of independent loads
+    // the first 16 x 1024 tiles' buckets stay in registers: one round of independent loads
     // instead of a dependent load-atomic chain per pass (the sort sits on the preparation
-    // phase's critical path at small harmonic counts)
+    // phase's critical path at small harmonic counts); every lane of a wave runs the same
+    // number of passes (wave_bucket_add's ballots need the whole wave)
     constexpr int PER = 16;
     int bk[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int64_t i = tid + (int64_t)q * 1024;
-        bk[q] = i < nu ? tile_cost_bucket(ucost(i)) : -1;
+        bk[q] = i < ntiles ? tile_cost_bucket(tcnt[i]) : -1;
     }
 #pragma unroll
-    for (int q = 0; q < PER; ++q)
-        if (bk[q] >= 0) atomicAdd(&hist[bk[q]], 1);
-    for (int64_t i = tid + (int64_t)PER * 1024; i < nu; i += 1024)
-        atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
+    for (int q = 0; q < PER; ++q) wave_bucket_add(hist, bk[q], bk[q] >= 0);
+    const int64_t npass = (ntiles + 1023) / 1024;
+    for (int64_t p = PER; p < npass; ++p) {
+        const int64_t i = tid + p * 1024;
+        const int bkt = i < ntiles ? tile_cost_bucket(tcnt[i]) : 0;
+        wave_bucket_add(hist, bkt, i < ntiles);
+    }
     __syncthreads();
     if (tid == 0) {   // exclusive scan, most expensive bucket first
         int acc = 0;
@@ -2106,11 +2169,15 @@ __global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < PER; ++q)
-        if (bk[q] >= 0) tperm[atomicAdd(&hist[bk[q]], 1)] = (int32_t)(tid + q * 1024);
-    for (int64_t i = tid + (int64_t)PER * 1024; i < nu; i += 1024) {
-        const int pos = atomicAdd(&hist[tile_cost_bucket(ucost(i))], 1);
-        tperm[pos] = (int32_t)i;
+    for (int q = 0; q < PER; ++q) {
+        const int pos = wave_bucket_add(hist, bk[q], bk[q] >= 0);
+        if (bk[q] >= 0) tperm[pos] = (int32_t)(tid + q * 1024);
+    }
+    for (int64_t p = PER; p < npass; ++p) {
+        const int64_t i = tid + p * 1024;
+        const int bkt = i < ntiles ? tile_cost_bucket(tcnt[i]) : 0;
+        const int pos = wave_bucket_add(hist, bkt, i < ntiles);
+        if (i < ntiles) tperm[pos] = (int32_t)i;
     }
 }
 
@@ -2373,7 +2440,7 @@ int efd_version(void) { return EFD_VERSION; }
 #if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
 int efd_exp_counters(unsigned long long* out) {
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 16));
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 32));
     return EFD_OK;
 }
 int efd_exp_tiles(unsigned int* out, unsigned long long* clk) {
@@ -2405,6 +2472,29 @@ int efd_spline_build(const double* x, int n, const double* y, int ninterp, doubl
 size_t efd_modesum_workspace_bytes(int32_t nt, int32_t K, int64_t nf) {
     if (nt < 2 || nt > MAX_NT || K <= 0 || K > MAX_K || nf <= 0) return 0;
     return make_layout(nt, K, nf, 0).total;  // unpaired has the most tiles
+}
+
+// Workgroup slots k_modesum has resident at once on the current device (CUs x workgroups per
+// CU from the occupancy query), cached per device. A grid with no more tiles than that starts
+// every tile together, so there is no dispatch order to choose and k_tile_order is skipped (it
+// would only lengthen the preparation: config 5's 43-tile downsampled grid lost 5.7% of its rate
+// to it). The kernels' shapes do not depend on the caustic mode or pairing.
+static int64_t resident_tile_slots() {
+    constexpr int MAX_DEV = 64;
+    static std::atomic<int64_t> cache[MAX_DEV];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return 1024;
+    int64_t v = cache[dev].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&k_modesum<true, EFD_CAUSTIC_UNIFORM, BPL>),
+            TILE, 0) != hipSuccess || cus <= 0 || per_cu <= 0)
+        return 1024;   // MI355X: 256 CUs x 4 workgroups (LDS-bound)
+    v = (int64_t)cus * per_cu;
+    cache[dev].store(v, std::memory_order_relaxed);
+    return v;
 }
 
 // phase: 1 = prepare (K0-K5), 2 = sum (K8), 3 = both
@@ -2520,19 +2610,20 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         if (paired)
             hipLaunchKernelGGL((k_tile_lists<true>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, 0, nullptr,
-                               nullptr, nullptr, (int64_t)0);
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, hdr, 0,
+                               nullptr, nullptr, nullptr, (int64_t)0);
         else
             hipLaunchKernelGGL((k_tile_lists<false>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, 0, nullptr,
-                               nullptr, nullptr, (int64_t)0);
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, hdr, 0,
+                               nullptr, nullptr, nullptr, (int64_t)0);
         HIP_TRY(hipGetLastError());
 #if EFD_COST_ORDER
-        if (L.ntiles > ORDER_MIN_TILES)
-        hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
-                           (int32_t*)(ws + L.tperm));
-        HIP_TRY(hipGetLastError());
+        if (L.ntiles > resident_tile_slots()) {
+            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
+                               (int32_t*)(ws + L.tperm));
+            HIP_TRY(hipGetLastError());
+        }
 #endif
     }
 #endif
@@ -2544,12 +2635,14 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
         int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
-        const int32_t* tperm = (EFD_PREBUILT_LISTS && EFD_COST_ORDER && L.ntiles > ORDER_MIN_TILES)
-                                   ? (const int32_t*)(ws + L.tperm) : nullptr;
+        const int32_t* tperm =
+            (EFD_PREBUILT_LISTS && EFD_COST_ORDER && L.ntiles > resident_tile_slots())
+                ? (const int32_t*)(ws + L.tperm) : nullptr;
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh,          \
                        seginfo, nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA,      \
-                       coefT, sctab_g, tkeys, tcnt_sum, tperm, acc, a->out, a->hp, a->hc, a->k0)
+                       coefT, sctab_g, tkeys, tcnt_sum, tperm, hdr, acc, a->out, a->hp, a->hc, \
+                       a->k0)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
             else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
@@ -2587,6 +2680,9 @@ int efd_modesum_status(const void* workspace, void* stream) {
         return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
     if (h.bad_mn != 0)
         return fail(EFD_ERR_ARG, "efd_modesum: |m| > 255 or |n| > 1023");
+    if (h.bad_tile != 0)
+        return fail(EFD_ERR_HIP, "efd_modesum: a tile dispatch-order entry was out of range "
+                                 "(prepare/sum workspace mismatch?); bins were left unwritten");
     return EFD_OK;
 }
 

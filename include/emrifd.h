@@ -127,7 +127,9 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
                     void* stream);
 
 /* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
- * this workspace (a harmonic with more than 8 monotonic frequency runs -> EFD_ERR_ARG). */
+ * this workspace: a harmonic with more than 8 monotonic frequency runs, or |m| > 255 or
+ * |n| > 1023 -> EFD_ERR_ARG; a tile dispatch-order entry out of range in the sum (its bins left
+ * unwritten, e.g. a sum run on a workspace another call prepared) -> EFD_ERR_HIP. */
 int efd_modesum_status(const void* workspace, void* stream);
 
 /* Contributions C (harmonic branch x bin pairs, the reference's per-(l, m, n) formulation) of

@@ -81,7 +81,7 @@ def child(name, ref_path):
         out["max_rel_dev_vs_base"] = float(np.abs(Sh - R).max() / np.abs(R).max())
     elif name == "base" and ref_path:
         np.save(ref_path, Sh)
-    if has_cnt and os.environ.get("EXP_TCLK"):
+    if has_cnt and os.environ.get("EXP_TCLK") and "tclk" in name:
         # per-tile wall clock of the last launch (-DEFD_EXP_TCLK; 100 MHz s_memrealtime ticks):
         # how much of the launch runs below full tile concurrency (the tail)
         nt_ = min(int(os.environ["EXP_TCLK"]), 16384)
@@ -91,7 +91,12 @@ def child(name, ref_path):
         c = np.frombuffer(clk, dtype=np.uint64)[:nt_]
         st0 = (c >> np.uint64(32)).astype(np.int64)
         dur = (c & np.uint64(0xffffffff)).astype(np.int64)
-        st0 -= st0.min()
+        # the kernel keeps the low 32 bits of the start (100 MHz: wraps every ~43 s); a launch
+        # is far shorter than half a wrap, so start times relative to tile 0, taken modulo 2^32
+        # into (-2^31, 2^31], are exact even when the wrap falls inside the launch
+        rel = (st0 - st0[0]) % (1 << 32)
+        rel = np.where(rel > (1 << 31), rel - (1 << 32), rel)
+        st0 = rel - rel.min()
         en = st0 + dur
         span = int(en.max())
         grid = np.arange(0, span + 1, max(span // 400, 1))
@@ -110,13 +115,14 @@ def child(name, ref_path):
                         "us_below_half_concurrency": float(len(below) * (grid[1] - grid[0])) / 100.0,
                         "longest_tiles": [int(i) for i in np.argsort(dur)[-5:]]}
     if has_cnt:
-        cnt = (ctypes.c_ulonglong * 16)()
+        cnt = (ctypes.c_ulonglong * 32)()
         lib.efd_exp_counters(cnt)
         runs = 1 + int(os.environ.get("EXP_REPS", "6"))  # counters accumulate over every launch
         out["counters_per_launch"] = {k: cnt[i] / runs for i, k in enumerate(
             ("record_evals", "cold_evals", "cold_lanes", "skips", "lanes_overshoot",
              "lanes_y_mid", "lanes_y_small", "unused", "y_ge153", "y_ge75", "y_ge48",
-             "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18"))}
+             "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18", "cold_wave_evals", "cold_wave_lanes",
+             "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1"))}
     print("EXPRESULT " + json.dumps(out), flush=True)
 
 
