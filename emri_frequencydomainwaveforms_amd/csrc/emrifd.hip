@@ -36,6 +36,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <string>
@@ -147,8 +148,9 @@ static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
-        seginfo, nseg, slotlh, slotinfo, slotcnt, gm, gn, gstart, gmem, gamp, sctab, tkeys, tcnt,
-        tperm, total;
+        seginfo, nseg, slotlh, slotinfo, slotcnt, slottiles, segbase, stb0, stb1, gm, gn, gstart,
+        gmem, gamp, sctab, tkeys, tcnt, tperm, total;
+    int64_t stbcap;
     int64_t ntiles, nlanes;
 };
 
@@ -177,6 +179,13 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.slotlh = take(sizeof(int2) * 2 * MAXRUNS * K);
     L.slotinfo = take(sizeof(int4) * 2 * MAXRUNS * K);
     L.slotcnt = take(sizeof(int32_t) * ((2 * MAXRUNS * K + 255) / 256));
+    L.slottiles = take(sizeof(int32_t) * ((2 * MAXRUNS * K + 255) / 256));
+    L.segbase = take(sizeof(int32_t) * 2 * MAXRUNS * K);
+    // segment-tile boundaries (k_seg_tiles): one (p0, p1) pair per (segment, tile it covers);
+    // segments past the capacity keep the bisection
+    L.stbcap = 64 * L.ntiles + 4 * (int64_t)(2 * MAXRUNS * K);
+    L.stb0 = take(sizeof(int32_t) * (size_t)L.stbcap);
+    L.stb1 = take(sizeof(int32_t) * (size_t)L.stbcap);
     L.gm = take(sizeof(int32_t) * K);
     L.gn = take(sizeof(int32_t) * K);
     L.gstart = take(sizeof(int32_t) * (K + 1));
@@ -933,9 +942,11 @@ __global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict
                                                        const Header* __restrict__ hdr,
                                                        int2* __restrict__ slot_lh,
                                                        int4* __restrict__ slot_info,
-                                                       int32_t* __restrict__ blockcnt) {
+                                                       int32_t* __restrict__ blockcnt,
+                                                       int32_t* __restrict__ blocktiles) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    __shared__ int wc[4];
+    __shared__ int wc[4], wt[4];
+    int ntl = 0;   // tiles the slot's segment covers
     bool valid = false;
     if (i < K * MAXRUNS * 2) {
         const int G = hdr->groups;
@@ -980,42 +991,123 @@ __global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict
         slot_lh[i] = lh;
         slot_info[i] = info;
         valid = info.y > 0;
+        if (valid) ntl = (lh.y - 1) / TILE_LANES - lh.x / TILE_LANES + 1;
     }
     const unsigned long long bal = __ballot(valid);
-    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(bal);
+    int tsum = ntl;
+    for (int o = 32; o > 0; o >>= 1) tsum += __shfl_xor(tsum, o);
+    if ((threadIdx.x & 63) == 0) {
+        wc[threadIdx.x >> 6] = __popcll(bal);
+        wt[threadIdx.x >> 6] = tsum;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) blockcnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+    if (threadIdx.x == 0) {
+        blockcnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+        blocktiles[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
+    }
 }
 
 // one workgroup per slot block: its output offset is the sum of the earlier blocks' counts
+// Segment-tile boundaries: segment s covers tiles [t0, t1] (t0 = lo / TILE_LANES); its
+// (p0, p1) pairs for those tiles sit at stb[toff(s) .. toff(s) + t1 - t0] in compacted segment
+// order, and segbase[s] = toff(s) - t0 (so the pair of tile t is stb[segbase[s] + t]), or
+// SEG_NO_STB when the pairs would pass the capacity (that segment keeps the bisection).
+constexpr int32_t SEG_NO_STB = INT32_MIN;
+#ifndef EFD_STB
+#define EFD_STB 1   // 0: every segment takes the bisection (reference for the bitwise check)
+#endif
 __global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict__ slot_lh,
                                                          const int4* __restrict__ slot_info,
                                                          const int32_t* __restrict__ blockcnt,
-                                                         int nslot, int2* __restrict__ seglh,
+                                                         const int32_t* __restrict__ blocktiles,
+                                                         int nslot, int64_t stbcap,
+                                                         int2* __restrict__ seglh,
                                                          int4* __restrict__ seginfo,
+                                                         int32_t* __restrict__ segbase,
                                                          int32_t* __restrict__ nseg) {
     __shared__ int wc[4];
+    __shared__ int64_t wt[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int blk = blockIdx.x;
     int before = 0;
-    for (int b = tid; b < blk; b += 256) before += blockcnt[b];
-    for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o);
-    if (lane == 0) wc[wave] = before;
+    int64_t tbefore = 0;
+    for (int b = tid; b < blk; b += 256) { before += blockcnt[b]; tbefore += blocktiles[b]; }
+    for (int o = 32; o > 0; o >>= 1) {
+        before += __shfl_xor(before, o);
+        tbefore += __shfl_xor(tbefore, o);
+    }
+    if (lane == 0) { wc[wave] = before; wt[wave] = tbefore; }
     __syncthreads();
     const int base = wc[0] + wc[1] + wc[2] + wc[3];
+    const int64_t tbase = wt[0] + wt[1] + wt[2] + wt[3];
     __syncthreads();
     const int i = blk * 256 + tid;
     int4 info = make_int4(0, 0, 0, 0);
-    if (i < nslot) info = slot_info[i];
+    int2 lh = make_int2(0, 0);
+    if (i < nslot) { info = slot_info[i]; lh = slot_lh[i]; }
     const bool valid = info.y > 0;
+    const int ntl = valid ? (lh.y - 1) / TILE_LANES - lh.x / TILE_LANES + 1 : 0;
+    // exclusive scan of the tile counts over the block's slots (slot order)
+    int incl = ntl;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
     const unsigned long long bal = __ballot(valid);
+    if (lane == 63) wt[wave] = incl;
     if (lane == 0) wc[wave] = __popcll(bal);
     __syncthreads();
     int pos = base;
-    for (int w = 0; w < wave; ++w) pos += wc[w];
+    int64_t toff = tbase + incl - ntl;
+    for (int w = 0; w < wave; ++w) { pos += wc[w]; toff += wt[w]; }
     pos += __popcll(bal & ((1ull << lane) - 1ull));
-    if (valid) { seglh[pos] = slot_lh[i]; seginfo[pos] = info; }
+    if (valid) {
+        seglh[pos] = lh;
+        seginfo[pos] = info;
+        segbase[pos] = (EFD_STB && toff + ntl <= stbcap) ? (int32_t)(toff - lh.x / TILE_LANES)
+                                                         : SEG_NO_STB;
+    }
     if (blk == (int)gridDim.x - 1 && tid == 0) *nseg = base + wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+// One workgroup per segment (grid-stride): for every record p of the segment in lane order
+// (and the end marker p = n), the tiles t of [t0, t1] whose first record reaching them is p
+// (p0(t) = first p with khi > t*TL) and whose first record past them is p (p1(t) = first p with
+// klo >= (t+1)*TL). Lane ranges are monotone in p, so each tile gets exactly one of each: the
+// same answers as k_modesum's bisection, from two loads instead of ~2 log2(n) dependent ones.
+__device__ __forceinline__ int div_floor_nn(int64_t a) { return (int)(a / TILE_LANES); }   // a >= 0
+__global__ __launch_bounds__(256) void k_seg_tiles(const int4* __restrict__ ranges,
+                                                   const int2* __restrict__ seglh,
+                                                   const int4* __restrict__ seginfo,
+                                                   const int32_t* __restrict__ segbase,
+                                                   const int32_t* __restrict__ nsegp,
+                                                   int32_t* __restrict__ stb0,
+                                                   int32_t* __restrict__ stb1) {
+    const int nseg = *nsegp;
+    for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const int32_t sbase = segbase[sg];
+        if (sbase == SEG_NO_STB) continue;
+        const int2 lh = seglh[sg];
+        const int4 info = seginfo[sg];
+        const int base = info.x, n = info.y, dir = info.z, sb = info.w;
+        const int t0 = lh.x / TILE_LANES, t1 = (lh.y - 1) / TILE_LANES;
+        auto rng = [&](int p) {   // (klo, khi) of record p in lane order
+            const int4 rg = ranges[base + (dir > 0 ? p : n - 1 - p)];
+            return sb ? make_int2(rg.z, rg.w) : make_int2(rg.x, rg.y);
+        };
+        for (int p = threadIdx.x; p <= n; p += blockDim.x) {
+            const int2 cur = p < n ? rng(p) : make_int2(0, 0);
+            const int2 prv = p > 0 ? rng(p - 1) : make_int2(0, 0);
+            // p0: khi_{p-1} <= t TL < khi_p
+            int a = p > 0 ? (int)((prv.y + TILE_LANES - 1) / TILE_LANES) : t0;
+            int b = p < n ? (cur.y > 0 ? div_floor_nn(cur.y - 1) : -1) : t1;
+            for (int t = max(a, t0); t <= min(b, t1); ++t) stb0[sbase + t] = p;
+            // p1: klo_{p-1} < (t+1) TL <= klo_p
+            a = p > 0 ? div_floor_nn(prv.x) : t0;
+            b = p < n ? div_floor_nn(cur.x) - 1 : t1;
+            for (int t = max(a, t0); t <= min(b, t1); ++t) stb1[sbase + t] = p;
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1059,8 +1151,9 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 }
 
 // sin/cos for the fast path: reduce by pi/256 against a 512-entry table of
-// (sin, cos)(k pi/256) held in LDS, then short Taylor polynomials on |r| <= pi/512 (sin to r^5,
-// cos to r^4: truncation < 1e-16 relative) and the angle-sum formula: ~14 FP64 operations
+// (sin, cos)(k pi/256) held in LDS, then short Taylor polynomials on |r| <= pi/512 (sin to r^3:
+// truncation r^5/120 < 7.4e-14, far below the ~1e-9 rad rounding of phases that reach 1e7 rad;
+// cos to r^4: < 1e-16) and the angle-sum formula: ~13 FP64 operations
 // instead of ~26 plus the quadrant logic of sincos_big. `shift` (an integer number of table
 // steps) is added to the angle exactly, through the table index. Valid for |x| < 2^31 pi/256.
 constexpr int SCTAB = 512;
@@ -1081,7 +1174,11 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
     const double2 t = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
     const double z = r * r;
+#ifdef EFD_SIN_R5
     const double sr = fma(r * z, fma(z, 8.333333333333333e-03, -1.6666666666666666e-01), r);
+#else
+    const double sr = fma(r * z, -1.6666666666666666e-01, r);
+#endif
     const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), 1.0);
     s = fma(t.x, cr, t.y * sr);
     c = fma(t.y, cr, -t.x * sr);
@@ -1557,9 +1654,10 @@ __device__ __forceinline__ void modesum_tile(
     const int32_t* __restrict__ gn, const double* __restrict__ t,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,
-    int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm, Header* __restrict__ hdr,
-    int accumulate_out, double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc,
-    int64_t k0) {
+    int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,
+    const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,
+    const int32_t* __restrict__ stb1, Header* __restrict__ hdr, int accumulate_out,
+    double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -1722,8 +1820,16 @@ __device__ __forceinline__ void modesum_tile(
                     continue;
                 }
                 win += SEGWIN;
-                // (2) bisect each hit segment for its records reaching into the tile
+                // (2) each hit segment's records reaching into the tile: [p0, p1) from the
+                // segment-tile boundaries of k_seg_tiles, or by bisection
                 for (int i = tid; i < nhit; i += TILE) {
+                    const int32_t sbase = segbase[hits[i]];
+                    if (sbase != SEG_NO_STB) {
+                        const int q0 = stb0[sbase + tile], q1 = stb1[sbase + tile];
+                        hp0[i] = q0;
+                        hcnt[i] = max(q1 - q0, 0);
+                        continue;
+                    }
                     const int4 info = seginfo[hits[i]];
                     const int base = info.x, n = info.y, dir = info.z, sb = info.w;
                     int lo = 0, hi = n;            // first p (lane order) with khi > tlo
@@ -2085,11 +2191,13 @@ __device__ __forceinline__ void modesum_tile(
         const double* __restrict__ coefA, const double* __restrict__ coefT,                   \
         const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,                    \
         int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,                        \
-        Header* __restrict__ hdr, int accumulate_out, double* __restrict__ out,               \
-        double* __restrict__ hp, double* __restrict__ hc, int64_t k0
+        const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,                \
+        const int32_t* __restrict__ stb1, Header* __restrict__ hdr, int accumulate_out,       \
+        double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0
 #define EFD_MODESUM_ARGS                                                                      \
     items, ranges, seglh, seginfo, nsegp, freq, nf, nlanes, ntiles, nt, K, gm, gn, t, coefA,  \
-        coefT, sctab_g, tkeys, tcnt, tperm, hdr, accumulate_out, out, hp, hc, k0
+        coefT, sctab_g, tkeys, tcnt, tperm, segbase, stb0, stb1, hdr, accumulate_out, out, hp,  \
+        hc, k0
 
 // K8: the mode sum (one workgroup per tile; prebuilt lists when tcnt is given)
 template <bool PAIRED, int CAUSTIC, int BPL>
@@ -2545,6 +2653,9 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     double2* sctab_g = (double2*)(ws + L.sctab);
     uint32_t* tkeys = (uint32_t*)(ws + L.tkeys);
     int32_t* tcnt = (int32_t*)(ws + L.tcnt);
+    int32_t* segbase = (int32_t*)(ws + L.segbase);
+    int32_t* stb0 = (int32_t*)(ws + L.stb0);
+    int32_t* stb1 = (int32_t*)(ws + L.stb1);
 
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
@@ -2592,12 +2703,16 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         int4* slot_info = (int4*)(ws + L.slotinfo);
         const int nblk = (nslot + 255) / 256;
         int32_t* blockcnt = (int32_t*)(ws + L.slotcnt);
+        int32_t* blocktiles = (int32_t*)(ws + L.slottiles);
         hipLaunchKernelGGL(k_segment_slots, dim3(nblk), dim3(256), 0, st, runs, ranges, nt, K,
                            (int)(paired ? nl : nf), (int)(paired ? nl1 : nf), hdr, slot_lh,
-                           slot_info, blockcnt);
+                           slot_info, blockcnt, blocktiles);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_segment_compact, dim3(nblk), dim3(256), 0, st, slot_lh, slot_info,
-                           blockcnt, nslot, seglh, seginfo, nseg);
+                           blockcnt, blocktiles, nslot, L.stbcap, seglh, seginfo, segbase, nseg);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_seg_tiles, dim3((unsigned)std::min(nslot, 1024)), dim3(256), 0, st,
+                           ranges, seglh, seginfo, segbase, nseg, stb0, stb1);
     }
     HIP_TRY(hipGetLastError());
 #if EFD_PREBUILT_LISTS
@@ -2610,13 +2725,13 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         if (paired)
             hipLaunchKernelGGL((k_tile_lists<true>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, hdr, 0,
-                               nullptr, nullptr, nullptr, (int64_t)0);
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, segbase,
+                               stb0, stb1, hdr, 0, nullptr, nullptr, nullptr, (int64_t)0);
         else
             hipLaunchKernelGGL((k_tile_lists<false>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, hdr, 0,
-                               nullptr, nullptr, nullptr, (int64_t)0);
+                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, segbase,
+                               stb0, stb1, hdr, 0, nullptr, nullptr, nullptr, (int64_t)0);
         HIP_TRY(hipGetLastError());
 #if EFD_COST_ORDER
         if (L.ntiles > resident_tile_slots()) {
@@ -2641,8 +2756,8 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh,          \
                        seginfo, nseg, a->freq, nf, nl, L.ntiles, nt, K, gm, gn, a->t, coefA,      \
-                       coefT, sctab_g, tkeys, tcnt_sum, tperm, hdr, acc, a->out, a->hp, a->hc, \
-                       a->k0)
+                       coefT, sctab_g, tkeys, tcnt_sum, tperm, segbase, stb0, stb1, hdr, acc,      \
+                       a->out, a->hp, a->hc, a->k0)
         if (paired) {
             if (a->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
             else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
