@@ -2062,7 +2062,11 @@ __device__ __forceinline__ void modesum_tile(
                         }
                         s_cur = s;
                     }
+#ifdef EFD_EXP_JFIX   // experiment: every record takes the FAST_J-term series (no J dispatch)
+                    const int J = FAST_J;
+#else
                     const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)(ha >> 29) : FAST_J;
+#endif
                     const double* xo = &it->b[s][0][0];
                     const double* xm = &it->b[1 - s][0][0];
                     double wr[BPL], wi[BPL], w[BPL];

@@ -127,6 +127,16 @@ class get_fd_waveform_fromFD:
         return (self.window is None and self._suffix_k0 is not None
                 and hasattr(gen, "fill_channels"))
 
+    @property
+    def can_pipeline(self):
+        return self.can_fill and hasattr(self.waveform_generator, "submit_channels")
+
+    def submit(self, pipeline, out, *args, **kwargs):
+        """fill, queued on a WaveformPipeline slot (returns the slot; see
+        GenerateEMRIWaveform.submit_channels)."""
+        return self.waveform_generator.submit_channels(pipeline, out, *args, k0=self._suffix_k0,
+                                                       **kwargs)
+
     def fill(self, out, *args, **kwargs):
         """Write [ch1, ch2] into out (complex128 [2][num_bins], device) without copies.
 

@@ -52,6 +52,9 @@ class Likelihood:
         from .reductions import Reducer
         self._red = Reducer(self.device)
         self._buf = None
+        # walkers whose templates are in flight at once in get_ll (WaveformPipeline slots);
+        # one HIP stream each (the box exposes 4 hardware queues per process)
+        self.num_streams = 4
         self._specific_likelihood_setup()
 
     def _specific_likelihood_setup(self):
@@ -172,6 +175,18 @@ class Likelihood:
             for i in range(num_likes):
                 h = self._as_channels(h_all[i])
                 self._red.loglike(h, self._d, self._w, out=out[i:i + 1])
+        elif getattr(tm, "can_pipeline", False):
+            # several walkers in flight: each pipeline slot has its own template buffer,
+            # stream and reduction scratch; walker i's template and logL run on one slot's
+            # stream, the batch costs one host synchronisation
+            P = self._pipeline_for(tm)
+            for i, params_i in enumerate(params):
+                j = P.next_slot()
+                slot = tm.submit(P, self._pbufs[j], *params_i, *args, **kwargs)
+                with torch.cuda.stream(P.stream(slot)):
+                    self._preds[slot].loglike(self._pbufs[slot], self._d, self._w_templ,
+                                              out=out[i:i + 1])
+            P.wait()
         elif getattr(tm, "can_fill", False):
             if self._buf is None or tuple(self._buf.shape) != (nch, nb):
                 self._buf = torch.empty((nch, nb), dtype=torch.complex128, device=self.device)
@@ -187,6 +202,27 @@ class Likelihood:
         if self.use_gpu and self.return_cupy:
             return out
         return out.cpu().numpy()
+
+    def _pipeline_for(self, tm):
+        """The WaveformPipeline (self.num_streams slots) and per-slot buffers of get_ll."""
+        torch = self.torch
+        from .reductions import Reducer
+        from .summation import WaveformPipeline
+        nch, nb = self._d.shape
+        caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),
+                                  "create_waveform", None), "caustic", "uniform")
+        P = getattr(self, "_pipe", None)
+        if P is None or P.caustic != caustic:
+            P = self._pipe = WaveformPipeline(self.num_streams, caustic=caustic,
+                                              device=self.device)
+            self._pbufs = [None] * P.num_slots
+            self._preds = [Reducer(self.device) for _ in range(P.num_slots)]
+        for j in range(P.num_slots):
+            if self._pbufs[j] is None or tuple(self._pbufs[j].shape) != (nch, nb):
+                with torch.cuda.stream(P.stream(j)):
+                    self._pbufs[j] = torch.empty((nch, nb), dtype=torch.complex128,
+                                                 device=self.device)
+        return P
 
     def _as_channels(self, chans):
         torch = self.torch

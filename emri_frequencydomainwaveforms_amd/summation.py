@@ -64,14 +64,17 @@ class DeviceInputs:
     K: int
 
     @classmethod
-    def from_host(cls, t, amps, phi_phi, phi_r, f_phi, f_r, m, n, ylm_p, ylm_m, device=None):
+    def from_host(cls, t, amps, phi_phi, phi_r, f_phi, f_r, m, n, ylm_p, ylm_m, device=None,
+                  stream=None, staging=None):
         """amps: complex [nt][K] (FEW teuk_modes layout).
 
         One host->device transfer: the arrays are packed (256-B aligned) into a reused pinned
-        staging buffer and copied asynchronously on the current stream into one device buffer,
-        whose typed slices are the fields (the ten separate pageable copies this replaces cost
-        ~0.17 ms per waveform). Kernels launched on the current stream see the data in order;
-        the staging buffer is reused only after its previous copy has completed.
+        staging buffer and copied asynchronously on `stream` (default: the current stream) into
+        one device buffer, whose typed slices are the fields (the ten separate pageable copies
+        this replaces cost ~0.17 ms per waveform). Kernels launched on that stream see the data
+        in order; the staging buffer is reused only after its previous copy has completed.
+        `staging`: a dict owned by the caller (one per pipeline slot) instead of the per-device
+        default, so waveforms on different streams do not wait on each other's copies.
         """
         torch = require_gpu()
         dev = device or torch.device("cuda", torch.cuda.current_device())
@@ -88,14 +91,14 @@ class DeviceInputs:
                   ("m", np.ascontiguousarray(m, dtype=np.int32).ravel()),
                   ("n", np.ascontiguousarray(n, dtype=np.int32).ravel()),
                   ("ylm_p", c128(ylm_p)), ("ylm_m", c128(ylm_m))]
-        views = _staged_upload([a for _, a in fields], dev)
+        views = _staged_upload([a for _, a in fields], dev, stream, staging)
         return cls(**{name: v for (name, _), v in zip(fields, views)}, nt=int(nt), K=int(K))
 
 
 _STAGING = {}
 
 
-def _staged_upload(arrays, dev):
+def _staged_upload(arrays, dev, stream=None, staging=None):
     """Copy host arrays into one device buffer through a cached pinned buffer (see from_host)."""
     torch = _torch()
     offs, off = [], 0
@@ -104,21 +107,23 @@ def _staged_upload(arrays, dev):
         offs.append(off)
         off += a.nbytes
     total = max(off, 1)
-    key = (dev.type, dev.index)
-    st = _STAGING.get(key)
-    if st is None or st["buf"].numel() < total:
-        st = {"buf": torch.empty(max(total, 1 << 20), dtype=torch.uint8, pin_memory=True),
-              "done": None}
-        _STAGING[key] = st
-    if st["done"] is not None:
+    if staging is None:
+        staging = _STAGING.setdefault((dev.type, dev.index), {})
+    st = staging
+    if st.get("buf") is None or st["buf"].numel() < total:
+        st["buf"] = torch.empty(max(total, 1 << 20), dtype=torch.uint8, pin_memory=True)
+        st["done"] = None
+    if st.get("done") is not None:
         st["done"].synchronize()        # the previous copy out of the staging buffer finished
     hb = st["buf"].numpy()
     for a, o in zip(arrays, offs):
         hb[o:o + a.nbytes] = a.view(np.uint8)
-    d = torch.empty(total, dtype=torch.uint8, device=dev)
-    d.copy_(st["buf"][:total], non_blocking=True)
+    strm = stream if stream is not None else torch.cuda.current_stream(dev)
+    with torch.cuda.stream(strm):
+        d = torch.empty(total, dtype=torch.uint8, device=dev)
+        d.copy_(st["buf"][:total], non_blocking=True)
     done = torch.cuda.Event()
-    done.record(torch.cuda.current_stream(dev))
+    done.record(strm)
     st["done"] = done
     dt = {np.dtype(np.float64): torch.float64, np.dtype(np.int32): torch.int32}
     return [d[o:o + a.nbytes].view(dt[a.dtype]) for a, o in zip(arrays, offs)]
@@ -213,6 +218,87 @@ class ModeSumEngine:
             if not self.status():
                 raise _lib.EFDError(f"efd_modesum: {_lib.last_error(self.lib)}")
         return out
+
+
+class WaveformPipeline:
+    """Several FD waveforms in flight on one device.
+
+    One waveform's device chain is mostly latency-bound preparation (grouping, spline
+    recurrences, interval records, tile lists: a few workgroups each) and, for the small
+    harmonic counts of parameter scans and MCMC walkers (eps = 1e-2: tens of harmonics), a short
+    mode sum. Run one at a time they leave most of the GPU idle. The pipeline owns `num_slots`
+    slots -- a ModeSumEngine workspace, a HIP stream and a pinned staging buffer each -- and
+    `submit` puts waveform i's whole chain (input upload, efd_modesum, h+/hx) on slot
+    i % num_slots's stream, so independent waveforms overlap. Nothing synchronises the host
+    until `wait()` (which also surfaces device-side errors of every slot). A slot's workspace,
+    device inputs and staging buffer are reused only in stream order (or after that slot's
+    previous upload finished), so results match the one-at-a-time path bitwise.
+    """
+
+    def __init__(self, num_slots=4, caustic="uniform", device=None):
+        torch = require_gpu()
+        if num_slots < 1:
+            raise ValueError("num_slots must be >= 1")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.slots = [dict(engine=ModeSumEngine(caustic=caustic),
+                           stream=torch.cuda.Stream(self.device), staging={}, used=False)
+                      for _ in range(num_slots)]
+        self._next = 0
+        self.caustic = caustic
+
+    @property
+    def num_slots(self):
+        return len(self.slots)
+
+    def next_slot(self):
+        """Index of the slot the next `submit` uses."""
+        return self._next
+
+    def stream(self, slot):
+        return self.slots[slot]["stream"]
+
+    def submit(self, host, freq, grid_symmetric, scale=1.0 + 0.0j, out=None, hp=None, hc=None,
+               k0=0, accumulate=False):
+        """Queue one waveform; returns its slot index.
+
+        host: dict of host arrays t, amp (complex [nt][K]), phi_phi, phi_r, f_phi, f_r, m, n,
+        ylm_p, ylm_m. Outputs as ModeSumEngine.launch: out (float64 view of the complex
+        spectrum) and/or hp, hc (float64 views of complex [nf - k0], symmetric grids: the
+        polarisations written by the mode sum itself). Follow-up work on the outputs belongs on
+        `stream(slot)` (or after `wait()`).
+        """
+        torch = _torch()
+        i = self._next
+        self._next = (i + 1) % len(self.slots)
+        sl = self.slots[i]
+        st = sl["stream"]
+        inp = DeviceInputs.from_host(host["t"], host["amp"], host["phi_phi"], host["phi_r"],
+                                     host["f_phi"], host["f_r"], host["m"], host["n"],
+                                     host["ylm_p"], host["ylm_m"], device=self.device, stream=st,
+                                     staging=sl["staging"])
+        # the caller produced freq / outputs on its own stream: order this slot after that work
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):   # the workspace, if (re)allocated, belongs to this stream
+            sl["engine"].launch(inp, freq, out, grid_symmetric, scale, accumulate,
+                                stream=st.cuda_stream, hp=hp, hc=hc, k0=k0)
+        sl["inp"] = inp          # keeps the device inputs alive until the slot's next waveform
+        sl["used"] = True
+        return i
+
+    def join(self):
+        """Make the current stream wait for every slot (device-side; no host sync)."""
+        torch = _torch()
+        cur = torch.cuda.current_stream(self.device)
+        for sl in self.slots:
+            if sl["used"]:
+                cur.wait_stream(sl["stream"])
+
+    def wait(self):
+        """Synchronise every slot and raise if any reported a device-side error."""
+        for sl in self.slots:
+            if sl["used"] and not sl["engine"].status(sl["stream"].cuda_stream):
+                raise _lib.EFDError(f"efd_modesum: {_lib.last_error(sl['engine'].lib)}")
+        self.join()
 
 
 def td_length(T, dt, odd_len=True):
@@ -327,6 +413,9 @@ class FDInterpolatedModeSum:
         self.frequency = None
         self._freq_dev = None
         self._freq_key = None
+        self._k0 = 0
+        self._fh = None
+        self._f_obj = None
 
     @property
     def caustic(self):
@@ -336,10 +425,20 @@ class FDInterpolatedModeSum:
         torch = require_gpu()
         dev = torch.device("cuda", torch.cuda.current_device())
         if f_arr is not None:
+            # the drivers pass the same f_arr object on every call (emri_pe.py:344-364): a
+            # device tensor seen last time is taken as is (no device->host copy, so the walker
+            # loop of a pipelined Likelihood never synchronises); a host array is compared with
+            # the cached copy before any validation
+            if f_arr is self._f_obj and hasattr(f_arr, "detach"):
+                return self._freq_dev, self._sym
             if hasattr(f_arr, "detach"):
                 fh = f_arr.detach().cpu().numpy().astype(np.float64)
             else:
                 fh = np.asarray(f_arr, dtype=np.float64)
+            if (self._freq_key is not None and self._freq_key[0] == "f"
+                    and np.array_equal(fh, self._fh)):
+                self._f_obj = f_arr
+                return self._freq_dev, self._sym
             if fh.ndim != 1 or len(fh) == 0 or np.any(np.diff(fh) <= 0):
                 raise ValueError("f_arr must be a strictly increasing 1-D frequency array")
             key = ("f", fh.tobytes())
@@ -351,9 +450,47 @@ class FDInterpolatedModeSum:
                 fh = fd_grid(T, dt, self.odd_len)
             self._freq_dev = torch.as_tensor(fh, device=dev)
             self._sym = is_symmetric(fh)
+            self._k0 = int(np.searchsorted(fh, 0.0))   # first f >= 0 bin (sorted grid)
             self._freq_key = key
+            self._fh = fh
             self.frequency = self._freq_dev if self.use_gpu else fh
+        self._f_obj = f_arr
         return self._freq_dev, self._sym
+
+    def submit_channels(self, pipeline, out, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr,
+                        n_arr, M, p, e, dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j):
+        """Queue [h+, hx] over f >= 0 into the rows of out (complex128 [2][nf - k0]) on a
+        WaveformPipeline slot: no host synchronisation. Symmetric grids (FEW's own and the
+        drivers' downsampled f_arr) get the polarisations from the mode sum itself; other grids
+        go through the spectrum and efd_polarizations on the slot's stream. Returns the slot."""
+        torch = require_gpu()
+        om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
+        host = dict(t=t, amp=teuk_modes, phi_phi=Phi_phi, phi_r=Phi_r,
+                    f_phi=om_phi / (2.0 * np.pi * M * MTSUN_SI),
+                    f_r=om_r / (2.0 * np.pi * M * MTSUN_SI), m=m_arr, n=n_arr, ylm_p=ylm_p,
+                    ylm_m=ylm_m)
+        freq, sym = self._grid(T, dt, f_arr)
+        nf, k0 = int(freq.numel()), self._k0
+        if (out.dtype != torch.complex128 or tuple(out.shape) != (2, nf - k0)
+                or not out.is_contiguous()):
+            raise ValueError(f"submit_channels: out must be contiguous complex128 [2][{nf - k0}]")
+        if sym:
+            return pipeline.submit(host, freq, True, scale, hp=torch.view_as_real(out[0]),
+                                   hc=torch.view_as_real(out[1]), k0=k0)
+        slot = pipeline.next_slot()
+        sl = pipeline.slots[slot]
+        st = pipeline.stream(slot)
+        with torch.cuda.stream(st):
+            S = sl.get("S")
+            if S is None or S.numel() != nf:
+                sl["S"] = S = torch.empty(nf, dtype=torch.complex128, device=freq.device)
+        pipeline.submit(host, freq, False, scale, out=torch.view_as_real(S))
+        lib = self.engine.lib
+        _lib.check(lib.efd_polarizations(torch.view_as_real(S).data_ptr(), nf, k0,
+                                         torch.view_as_real(out[0]).data_ptr(),
+                                         torch.view_as_real(out[1]).data_ptr(), st.cuda_stream),
+                   "efd_polarizations", lib)
+        return slot
 
     def spectrum(self, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr, n_arr, M, p, e,
                  dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j):
@@ -367,10 +504,11 @@ class FDInterpolatedModeSum:
         return self.engine.run(inp, freq, grid_symmetric=sym, scale=scale)
 
     def positive_start(self):
-        """Index of the first f >= 0 bin of the last grid (emri_pe.py:239 mask, sorted grid)."""
-        torch = require_gpu()
-        return int(torch.searchsorted(self._freq_dev, torch.zeros(
-            1, dtype=torch.float64, device=self._freq_dev.device)).item())
+        """Index of the first f >= 0 bin of the last grid (emri_pe.py:239 mask, sorted grid);
+        kept on the host when the grid is set up, so asking costs no device synchronisation."""
+        if self._freq_key is None:
+            raise ValueError("no grid yet: call the generator first")
+        return self._k0
 
     def polarizations(self, S, mask_positive=False, out=None):
         """[h+, hx] (FEW list output) from S; mask_positive keeps f >= 0.

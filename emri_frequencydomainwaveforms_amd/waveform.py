@@ -118,6 +118,20 @@ class FastSchwarzschildEccentricFlux:
                                              d["Phi_phi"], d["Phi_r"], d["m"], d["n"], M, d["p"],
                                              d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale)
 
+    def submit_channels(self, pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0,
+                        Phi_r0=0.0, dt=10.0, T=1.0, eps=1e-5, mode_selection=None,
+                        include_minus_m=True, f_arr=None, extra_scale=1.0 + 0.0j, **kwargs):
+        """Queue [h+, hx] over f >= 0 into out on a WaveformPipeline slot (FD only)."""
+        if self.output_type != "fd":
+            raise ValueError("submit_channels is the FD path")
+        d = self.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
+                         mode_selection, include_minus_m)
+        K = len(d["m"])
+        scale = complex(extra_scale) * (mu * MRSUN_SI / (dist * Gpc))
+        return self.create_waveform.submit_channels(
+            pipeline, out, d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:], d["Phi_phi"],
+            d["Phi_r"], d["m"], d["n"], M, d["p"], d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale)
+
     def time_series(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                     T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True,
                     extra_scale=1.0 + 0.0j):
@@ -179,6 +193,22 @@ class GenerateEMRIWaveform:
         gen = self.waveform_generator
         return gen.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, extra_scale=rot,
                             **kwargs)
+
+    def submit_channels(self, pipeline, out, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK,
+                        Phi_phi0, Phi_theta0, Phi_r0, k0=None, **kwargs):
+        """fill_channels on a WaveformPipeline slot: queued, no host synchronisation (the
+        walker loop of Likelihood.get_ll keeps several templates in flight). Returns the slot;
+        work that reads out belongs on pipeline.stream(slot)."""
+        gen = self.waveform_generator
+        theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
+        rot = 1.0 + 0.0j
+        if self.frame == "detector":
+            rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
+        slot = gen.submit_channels(pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0,
+                                   Phi_r0, extra_scale=rot, **kwargs)
+        if k0 is not None and k0 != gen.create_waveform.positive_start():
+            raise ValueError("positive_frequency_mask does not match the generator's grid")
+        return slot
 
     def fill_channels(self, out, *params, k0=None, **kwargs):
         """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).

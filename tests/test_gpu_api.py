@@ -89,9 +89,12 @@ def test_emri_pe_likelihood_path(setup):
     walkers = np.stack([params, params, params])
     walkers[1, 0] *= 1.0 + 1e-5
     walkers[2, 4] += 1e-3
-    ll = like(walkers, **kw)                             # fused path (fill into one buffer)
+    assert fd_gen.can_pipeline
+    ll = like(walkers, **kw)           # pipelined fused path (templates on 4 streams at once)
     assert ll[0] == 0.0
     assert np.all(ll[1:] < 0.0)
+    like.num_streams, like._pipe = 1, None   # one template in flight at a time: same values
+    np.testing.assert_array_equal(like(walkers, **kw), ll)
 
     # generic path (template returns channels) gives bitwise the same values
     like_g = Likelihood(lambda *a, **k: fd_gen(*a, **k), 2, f_arr=f_arr, use_gpu=True)
