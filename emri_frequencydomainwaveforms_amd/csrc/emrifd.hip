@@ -1158,7 +1158,8 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 // steps) is added to the angle exactly, through the table index. Valid for |x| < 2^31 pi/256.
 constexpr int SCTAB = 512;
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
-                                           double& s, double& c) {
+                                           double& s, double& c, double extra = 0.0,
+                                           bool use_extra = false) {
     constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
     constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
     constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
@@ -1169,6 +1170,7 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     const double q = qs - SHIFTER;
     double r = fma(-q, STEP_1, x);
     r = fma(-q, STEP_2, r);
+    if (use_extra) r += extra;   // a small angle (|extra| < 1e-3) added after the reduction
     const int qi = __double2loint(qs);
     // (sin, cos)((q + shift) pi/256), addressed in bytes: v_lshl_add + v_and
     const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
@@ -1440,6 +1442,46 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
     need_general = act & !good;
 }
 
+// The same factor in polar form, G = rho e^{i theta} (fast path, EFD_POLAR): log G of the
+// Hankel series, re-expanded as rho = sum_j RH_j u^j and theta = w sum_j TH_j u^j (y > 0; theta
+// is odd in y), u = w^2. The first omitted terms fall below 1e-17 at the same |y| bounds as
+// KB / KC (JSER_Y), so a record's series length J serves both forms. theta is added to the
+// reduced sin/cos argument (|r| <= pi/512, where it costs no rounding) and rho scales the
+// amplitude: two FP64 operations fewer per evaluation than rotating by (R + iI).
+#ifndef EFD_POLAR
+#define EFD_POLAR 1
+#endif
+__constant__ double KTH[4] = {-0.069444444444444444444, 0.035525977366255144033,
+                              -0.11095169967421124829, 0.85188445191064930488};
+__constant__ double KRH[4] = {1.0, -0.034722222222222222222, 0.055097415123456790123,
+                              -0.283034838766718107};
+static_assert(FAST_J <= 4, "KTH / KRH hold 4 terms");
+template <int J>
+__device__ __forceinline__ void kpolar(double ww, double& rho, double& th) {
+    if (J == 1) {
+        rho = 1.0;
+        th = ww * KTH[0];
+        return;
+    }
+    const double uu = ww * ww;
+    double r = KRH[J - 1], t = KTH[J - 1];
+#pragma unroll
+    for (int j = J - 2; j >= 0; --j) {
+        r = fma(r, uu, KRH[j]);
+        t = fma(t, uu, KTH[j]);
+    }
+    rho = r;
+    th = ww * t;
+}
+__device__ __forceinline__ void kpolar_rt(int J, double ww, double& rho, double& th) {
+    switch (J) {
+        case 1: kpolar<1>(ww, rho, th); break;
+        case 2: kpolar<2>(ww, rho, th); break;
+        case 3: kpolar<3>(ww, rho, th); break;
+        default: kpolar<FAST_J>(ww, rho, th); break;
+    }
+}
+
 // K_{1/3} series with a wave-uniform runtime length J (1..FAST_J): the branches are scalar, and
 // only R, I merge after them.
 __device__ __forceinline__ void kseries_rt(int J, double ww, double& R, double& I) {
@@ -1470,10 +1512,40 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
     good = good & (afd > 0.0);
+#if EFD_POLAR
+    // F' = 0 gives amp = inf here; every quantity it reaches is selected away below (selects,
+    // not multiplications by a zero mask), so no NaN reaches the sums
+    const double amp = CAUSTIC == EFD_CAUSTIC_UNIFORM ? rsqrt_pos(afd)
+                                                      : (afd > 0.0 ? rsqrt_pos(afd) : 0.0);
+#else
     const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
+#endif
     const double psi0 = fma(stfk, tt, -ph);
     const int shift = fd > 0.0 ? 192 : -192;
     double R = 1.0, I = 0.0;
+#if EFD_POLAR
+    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
+        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        const double a3 = amp * amp * amp;
+        const double t3 = fdds * a3;
+        const double ww = t3 * t3;   // 1/|y|
+        good = good & ((J < FAST_J) | (ww <= 1.0 / FAST_Y));
+        double rho, th;
+        kpolar_rt(J, ww, rho, th);
+        // theta is odd in y: the sign of F' (= sign of y) onto it by one XOR of the high word
+        const bool ok = act & good;
+        const double ths = ok ? __hiloint2double(__double2hiint(th) ^ (__double2hiint(fd) & INT32_MIN),
+                                                 __double2loint(th))
+                              : 0.0;
+        const double am = ok ? amp * rho : 0.0;
+        double sn, cs;
+        sincos_tab(psi0, shift, sct, sn, cs, ths, true);
+        wr = am * cs;
+        wi = am * sn;
+        need_general = act & !good;
+        return;
+    }
+#else
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
         const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
         const double a3 = amp * amp * amp;
@@ -1485,6 +1557,7 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
         good = good & ((J < FAST_J) | (ww <= 1.0 / FAST_Y));
         kseries_rt(J, ww, R, I);
     }
+#endif
     const double as = (act & good) ? copysign(amp, fd) : 0.0;
     R *= fabs(as);
     I *= CAUSTIC == EFD_CAUSTIC_UNIFORM ? as : fabs(as);
