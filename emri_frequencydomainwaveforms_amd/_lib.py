@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_stats",
     "efd_td_workspace_bytes",
     "efd_td_modesum",
+    "efd_upload",
     "efd_polarizations",
     "efd_loglike",
     "efd_inner_product",
@@ -151,6 +152,9 @@ def load(path=None):
         lib.efd_td_workspace_bytes.argtypes = [i32, i32]
         lib.efd_td_modesum.restype = ctypes.c_int
         lib.efd_td_modesum.argtypes = [ctypes.POINTER(TdArgs), vp, sz, vp]
+    if hasattr(lib, "efd_upload"):   # absent only in older experiment builds
+        lib.efd_upload.restype = ctypes.c_int
+        lib.efd_upload.argtypes = [vp, vp, sz, vp]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int

@@ -2983,6 +2983,13 @@ int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes
     return EFD_OK;
 }
 
+int efd_upload(void* dst, const void* src, size_t bytes, void* stream) {
+    if (bytes == 0) return EFD_OK;
+    if (!dst || !src) return fail(EFD_ERR_ARG, "efd_upload: NULL pointer");
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return EFD_OK;
+}
+
 int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, double* hc,
                       void* stream) {
     if (!S || !hp || !hc || nf <= 0 || k0 < 0 || k0 > nf)

@@ -180,9 +180,10 @@ class Likelihood:
             # stream and reduction scratch; walker i's template and logL run on one slot's
             # stream, the batch costs one host synchronisation
             P = self._pipeline_for(tm)
+            P.order_after_current()
             for i, params_i in enumerate(params):
                 j = P.next_slot()
-                slot = tm.submit(P, self._pbufs[j], *params_i, *args, **kwargs)
+                slot = tm.submit(P, self._pbufs[j], *params_i, *args, order=False, **kwargs)
                 with torch.cuda.stream(P.stream(slot)):
                     self._preds[slot].loglike(self._pbufs[slot], self._d, self._w_templ,
                                               out=out[i:i + 1])

@@ -241,7 +241,7 @@ class WaveformPipeline:
             raise ValueError("num_slots must be >= 1")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.slots = [dict(engine=ModeSumEngine(caustic=caustic),
-                           stream=torch.cuda.Stream(self.device), staging={}, used=False)
+                           stream=torch.cuda.Stream(self.device), used=False)
                       for _ in range(num_slots)]
         self._next = 0
         self.caustic = caustic
@@ -258,32 +258,101 @@ class WaveformPipeline:
         return self.slots[slot]["stream"]
 
     def submit(self, host, freq, grid_symmetric, scale=1.0 + 0.0j, out=None, hp=None, hc=None,
-               k0=0, accumulate=False):
+               k0=0, accumulate=False, order=True):
         """Queue one waveform; returns its slot index.
 
         host: dict of host arrays t, amp (complex [nt][K]), phi_phi, phi_r, f_phi, f_r, m, n,
         ylm_p, ylm_m. Outputs as ModeSumEngine.launch: out (float64 view of the complex
         spectrum) and/or hp, hc (float64 views of complex [nf - k0], symmetric grids: the
         polarisations written by the mode sum itself). Follow-up work on the outputs belongs on
-        `stream(slot)` (or after `wait()`).
+        `stream(slot)` (or after `wait()`). order=False skips making the slot wait for the
+        current stream (the caller did it once for the batch: `order_after_current`).
         """
         torch = _torch()
         i = self._next
         self._next = (i + 1) % len(self.slots)
         sl = self.slots[i]
         st = sl["stream"]
-        inp = DeviceInputs.from_host(host["t"], host["amp"], host["phi_phi"], host["phi_r"],
-                                     host["f_phi"], host["f_r"], host["m"], host["n"],
-                                     host["ylm_p"], host["ylm_m"], device=self.device, stream=st,
-                                     staging=sl["staging"])
-        # the caller produced freq / outputs on its own stream: order this slot after that work
-        st.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(st):   # the workspace, if (re)allocated, belongs to this stream
-            sl["engine"].launch(inp, freq, out, grid_symmetric, scale, accumulate,
-                                stream=st.cuda_stream, hp=hp, hc=hc, k0=k0)
-        sl["inp"] = inp          # keeps the device inputs alive until the slot's next waveform
+        if order:
+            # the caller produced freq / outputs on its own stream: order this slot after it
+            st.wait_stream(torch.cuda.current_stream(self.device))
+        inp = self._upload(sl, host)
+        eng = sl["engine"]
+        if eng._ws is None:
+            with torch.cuda.stream(st):   # the workspace belongs to this slot's stream
+                eng._workspace(inp.nt, inp.K, int(freq.numel()), freq.device)
+        elif int(eng.lib.efd_modesum_workspace_bytes(inp.nt, inp.K, int(freq.numel()))) \
+                > eng._ws.numel():
+            with torch.cuda.stream(st):
+                eng._workspace(inp.nt, inp.K, int(freq.numel()), freq.device)
+        eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
+                   hp=hp, hc=hc, k0=k0)
         sl["used"] = True
         return i
+
+    def order_after_current(self):
+        """Make every slot wait for the work queued so far on the current stream (once per
+        batch, instead of `order=True` on each submit)."""
+        torch = _torch()
+        cur = torch.cuda.current_stream(self.device)
+        for sl in self.slots:
+            sl["stream"].wait_stream(cur)
+
+    def _upload(self, sl, host):
+        """The waveform's inputs into the slot's device buffer: packed into the slot's pinned
+        buffer, one asynchronous copy on the slot's stream (efd_upload). Buffers grow as needed
+        and are reused in stream order; the field views are rebuilt only when (nt, K) change."""
+        torch = _torch()
+        amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
+        nt, K = amps.shape
+        t = np.ascontiguousarray(host["t"], dtype=np.float64)
+        if len(t) != nt:
+            raise ValueError("amplitude array must be [N_t, K]")
+        f64 = lambda x: np.ascontiguousarray(x, dtype=np.float64).ravel()  # noqa: E731
+        c128 = lambda x: np.ascontiguousarray(x, dtype=np.complex128).view(np.float64).ravel()  # noqa: E731
+        arrays = [t, f64(host["phi_phi"]), f64(host["phi_r"]), f64(host["f_phi"]),
+                  f64(host["f_r"]), amps.view(np.float64).ravel(),
+                  np.ascontiguousarray(host["m"], dtype=np.int32).ravel(),
+                  np.ascontiguousarray(host["n"], dtype=np.int32).ravel(),
+                  c128(host["ylm_p"]), c128(host["ylm_m"])]
+        key = (nt, K)
+        lay = sl.get("layout")
+        if lay is None or lay[0] != key:
+            offs, off = [], 0
+            for a in arrays:
+                off = (off + 255) // 256 * 256
+                offs.append(off)
+                off += a.nbytes
+            lay = (key, offs, max(off, 1))
+        _, offs, total = lay
+        if sl.get("pin") is None or sl["pin"].numel() < total:
+            sl["pin"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8, pin_memory=True)
+            sl["pin_np"] = sl["pin"].numpy()
+            sl["pin_done"] = None
+        if sl.get("pin_done") is not None:
+            sl["pin_done"].synchronize()   # the slot's previous copy out of the pinned buffer
+        hb = sl["pin_np"]
+        for a, o in zip(arrays, offs):
+            hb[o:o + a.nbytes] = a.view(np.uint8)
+        if sl.get("dbuf") is None or sl["dbuf"].numel() < total:
+            with torch.cuda.stream(sl["stream"]):
+                sl["dbuf"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8,
+                                         device=self.device)
+            sl["layout"] = None
+        lib = sl["engine"].lib
+        _lib.check(lib.efd_upload(sl["dbuf"].data_ptr(), sl["pin"].data_ptr(), total,
+                                  sl["stream"].cuda_stream), "efd_upload", lib)
+        if sl.get("pin_done") is None:
+            sl["pin_done"] = torch.cuda.Event()
+        sl["pin_done"].record(sl["stream"])
+        if sl.get("layout") is None or sl["layout"][0] != key or sl.get("inp") is None:
+            d = sl["dbuf"]
+            dt = {np.dtype(np.float64): torch.float64, np.dtype(np.int32): torch.int32}
+            views = [d[o:o + a.nbytes].view(dt[a.dtype]) for a, o in zip(arrays, offs)]
+            names = ("t", "phi_phi", "phi_r", "f_phi", "f_r", "amp", "m", "n", "ylm_p", "ylm_m")
+            sl["inp"] = DeviceInputs(**dict(zip(names, views)), nt=int(nt), K=int(K))
+            sl["layout"] = lay
+        return sl["inp"]
 
     def join(self):
         """Make the current stream wait for every slot (device-side; no host sync)."""
@@ -458,17 +527,19 @@ class FDInterpolatedModeSum:
         return self._freq_dev, self._sym
 
     def submit_channels(self, pipeline, out, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr,
-                        n_arr, M, p, e, dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j):
+                        n_arr, M, p, e, dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j,
+                        f_phi=None, f_r=None, order=True):
         """Queue [h+, hx] over f >= 0 into the rows of out (complex128 [2][nf - k0]) on a
         WaveformPipeline slot: no host synchronisation. Symmetric grids (FEW's own and the
         drivers' downsampled f_arr) get the polarisations from the mode sum itself; other grids
         go through the spectrum and efd_polarizations on the slot's stream. Returns the slot."""
         torch = require_gpu()
-        om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
-        host = dict(t=t, amp=teuk_modes, phi_phi=Phi_phi, phi_r=Phi_r,
-                    f_phi=om_phi / (2.0 * np.pi * M * MTSUN_SI),
-                    f_r=om_r / (2.0 * np.pi * M * MTSUN_SI), m=m_arr, n=n_arr, ylm_p=ylm_p,
-                    ylm_m=ylm_m)
+        if f_phi is None or f_r is None:
+            om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
+            f_phi = om_phi / (2.0 * np.pi * M * MTSUN_SI)
+            f_r = om_r / (2.0 * np.pi * M * MTSUN_SI)
+        host = dict(t=t, amp=teuk_modes, phi_phi=Phi_phi, phi_r=Phi_r, f_phi=f_phi, f_r=f_r,
+                    m=m_arr, n=n_arr, ylm_p=ylm_p, ylm_m=ylm_m)
         freq, sym = self._grid(T, dt, f_arr)
         nf, k0 = int(freq.numel()), self._k0
         if (out.dtype != torch.complex128 or tuple(out.shape) != (2, nf - k0)
@@ -476,7 +547,7 @@ class FDInterpolatedModeSum:
             raise ValueError(f"submit_channels: out must be contiguous complex128 [2][{nf - k0}]")
         if sym:
             return pipeline.submit(host, freq, True, scale, hp=torch.view_as_real(out[0]),
-                                   hc=torch.view_as_real(out[1]), k0=k0)
+                                   hc=torch.view_as_real(out[1]), k0=k0, order=order)
         slot = pipeline.next_slot()
         sl = pipeline.slots[slot]
         st = pipeline.stream(slot)
@@ -484,7 +555,7 @@ class FDInterpolatedModeSum:
             S = sl.get("S")
             if S is None or S.numel() != nf:
                 sl["S"] = S = torch.empty(nf, dtype=torch.complex128, device=freq.device)
-        pipeline.submit(host, freq, False, scale, out=torch.view_as_real(S))
+        pipeline.submit(host, freq, False, scale, out=torch.view_as_real(S), order=order)
         lib = self.engine.lib
         _lib.check(lib.efd_polarizations(torch.view_as_real(S).data_ptr(), nf, k0,
                                          torch.view_as_real(out[0]).data_ptr(),

@@ -25,7 +25,8 @@ kernel's complex scale, so it costs nothing.
 import numpy as np
 
 from .amplitude import ModeSelector, RomanAmplitude
-from .constants import Gpc, MRSUN_SI
+from .constants import Gpc, MRSUN_SI, MTSUN_SI
+from .frequencies import get_fundamental_frequencies
 from .summation import FDInterpolatedModeSum, TDInterpolatedModeSum, require_gpu
 from .trajectory import EMRIInspiral
 from .ylm import GetYlms
@@ -98,8 +99,13 @@ class FastSchwarzschildEccentricFlux:
             ylms = ylms.copy()
             ylms[K:] = 0.0
         self.last_modes = (amp.l_arr[keep], amp.m_arr[keep], amp.n_arr[keep])
+        # orbital frequencies along the trajectory (FEW's get_fundamental_frequencies, as the
+        # notebook's F(t) at Tutorial_FD_construction_single_mode.ipynb:227, 280)
+        om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
         return dict(t=t, p=p, e=e, Phi_phi=Phi_phi, Phi_r=Phi_r, teuk=teuk, ylms=ylms,
-                    m=amp.m_arr[keep], n=amp.n_arr[keep])
+                    m=amp.m_arr[keep], n=amp.n_arr[keep],
+                    f_phi=om_phi / (2.0 * np.pi * M * MTSUN_SI),
+                    f_r=om_r / (2.0 * np.pi * M * MTSUN_SI))
 
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
@@ -120,7 +126,8 @@ class FastSchwarzschildEccentricFlux:
 
     def submit_channels(self, pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0,
                         Phi_r0=0.0, dt=10.0, T=1.0, eps=1e-5, mode_selection=None,
-                        include_minus_m=True, f_arr=None, extra_scale=1.0 + 0.0j, **kwargs):
+                        include_minus_m=True, f_arr=None, extra_scale=1.0 + 0.0j, order=True,
+                        **kwargs):
         """Queue [h+, hx] over f >= 0 into out on a WaveformPipeline slot (FD only)."""
         if self.output_type != "fd":
             raise ValueError("submit_channels is the FD path")
@@ -130,7 +137,8 @@ class FastSchwarzschildEccentricFlux:
         scale = complex(extra_scale) * (mu * MRSUN_SI / (dist * Gpc))
         return self.create_waveform.submit_channels(
             pipeline, out, d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:], d["Phi_phi"],
-            d["Phi_r"], d["m"], d["n"], M, d["p"], d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale)
+            d["Phi_r"], d["m"], d["n"], M, d["p"], d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale,
+            f_phi=d["f_phi"], f_r=d["f_r"], order=order)
 
     def time_series(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                     T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True,

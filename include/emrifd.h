@@ -187,6 +187,13 @@ size_t efd_td_workspace_bytes(int32_t nt, int32_t K);
 int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * Asynchronous host -> device copy of `bytes` from `src` (pinned host memory) to `dst` on
+ * `stream`: the input upload of a waveform on a pipeline slot's stream, issued through this
+ * library's HIP runtime (no host synchronisation). Plumbing for the Python host layer.
+ */
+int efd_upload(void* dst, const void* src, size_t bytes, void* stream);
+
+/*
  * h+ = (S(f) + conj(S_flip))/2, hx = i (S(f) - conj(S_flip))/2 with S_flip the array reversed
  * (FEW list output). Writes bins [k0, nf) of each (k0 = first bin to keep, e.g. the f >= 0
  * bin for mask_positive) into hp, hc (complex [nf - k0]).

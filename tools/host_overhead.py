@@ -57,7 +57,7 @@ def main():
     like.get_ll(walkers, **kw)
     pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(18)
+    pstats.Stats(pr, stream=s).sort_stats(os.environ.get("HO_SORT", "tottime")).print_stats(int(os.environ.get("HO_N", "18")))
     B = len(walkers)
     print(json.dumps({"config": args.config, "walkers": B, "slots": args.slots,
                       "wall_ms_per_walker": wall / B * 1e3,
