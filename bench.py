@@ -201,6 +201,10 @@ def main():
     # per-launch k_modesum duration, live over the timed region (HIP events on the sum stream;
     # with the overlap pipeline the next waveform's preparation kernels share the GPU with it)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # idle time of the sum stream between consecutive mode sums (the next sum's start waits for
+    # its preparation and for the launch): what the pipeline loses beside the kernel itself
+    gaps = [evs[i][1].elapsed_time(evs[i + 1][0]) for i in range(len(evs) - 1)]
+    gap_ms = float(np.mean(gaps)) if gaps else 0.0
     C, n_eval, n_groups = slots[0]["eng"].stats(s_sum.cuda_stream)
 
     if world > 1:
@@ -264,6 +268,8 @@ def main():
                          "kernel_timing": "HIP events around each k_modesum launch in the timed "
                                           "region (sum stream), mean",
                          "contributions_per_s": C / (kern_ms * 1e-3),
+                         "sum_gap_ms": gap_ms,
+                         "sum_gap_ms_min_max": [min(gaps, default=0.0), max(gaps, default=0.0)],
                          "fp64_valu": fp64},
             "cpu_baseline": cpu,
         }
