@@ -136,3 +136,34 @@ def test_spectrum_matches_oracle_through_api(setup):
                              d["m"], d["n"], d["ylms"][:K], d["ylms"][K:], freq,
                              MU * MRSUN_SI / Gpc)
     assert np.abs(S - R).max() <= 1e-9 * np.abs(R).max()
+
+
+def test_pipelined_likelihood_asymmetric_grid(setup):
+    """An f_arr that is not mirror-symmetric takes the pipeline's spectrum + efd_polarizations
+    branch on the slot streams: same values as the one-at-a-time generic path."""
+    params, kw, gen, gen_list = setup
+    S = gen(*params, **kw).cpu().numpy()
+    freq = gen.waveform_generator.create_waveform.frequency.cpu().numpy()
+    nz = np.abs(S[freq >= 0]) > 1e-50 * np.abs(S).max()
+    fmax = freq[freq >= 0][nz].max() * 1.01
+    # more bins on the positive side than the negative one: sorted, odd length, not symmetric
+    f_arr = np.hstack((-np.linspace(fmax, 0.0, 40)[:-1], np.linspace(0.0, fmax, 61)))
+    kw2 = dict(kw, f_arr=f_arr)
+    gen_list(*params, **kw2)
+    assert not gen_list.waveform_generator.create_waveform._sym
+    pos = f_arr >= 0
+    fd_gen = get_fd_waveform_fromFD(gen_list, pos, DT)
+    assert fd_gen.can_pipeline
+    sig = fd_gen(*params, **kw2)
+    walkers = np.stack([params] * 5)
+    walkers[1, 0] *= 1.0 + 1e-5
+    walkers[2, 4] += 1e-3
+    walkers[3, 11] += 0.1
+    walkers[4, 3] += 1e-4
+    like = Likelihood(fd_gen, 2, f_arr=f_arr[pos], use_gpu=True)
+    like.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2, noise_kwargs=[{}, {}])
+    ll = like.get_ll(walkers, **kw2)
+    like_g = Likelihood(lambda *a, **k: fd_gen(*a, **k), 2, f_arr=f_arr[pos], use_gpu=True)
+    like_g.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2, noise_kwargs=[{}, {}])
+    np.testing.assert_array_equal(like_g.get_ll(walkers, **kw2), ll)
+    assert ll[0] == 0.0 and np.all(ll[1:] < 0.0)
