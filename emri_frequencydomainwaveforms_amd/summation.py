@@ -141,13 +141,21 @@ class ModeSumEngine:
         self._ws_key = None
         self.last_contributions = None
 
-    def _workspace(self, nt, K, nf, device):
+    def _workspace(self, nt, K, nf, device, stream=None):
+        """The workspace for (nt, K, nf), grown when too small. With `stream` (a torch stream)
+        a new allocation is made on it, so the caching allocator ties the block to the stream
+        that uses it (WaveformPipeline slots)."""
         torch = _torch()
         nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf))
         if nbytes == 0:
             raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
         if self._ws is None or self._ws.numel() < nbytes or self._ws.device != device:
-            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self._ws = None
+            if stream is not None:
+                with torch.cuda.stream(stream):
+                    self._ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            else:
+                self._ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
         return self._ws
 
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
@@ -278,13 +286,7 @@ class WaveformPipeline:
             st.wait_stream(torch.cuda.current_stream(self.device))
         inp = self._upload(sl, host)
         eng = sl["engine"]
-        if eng._ws is None:
-            with torch.cuda.stream(st):   # the workspace belongs to this slot's stream
-                eng._workspace(inp.nt, inp.K, int(freq.numel()), freq.device)
-        elif int(eng.lib.efd_modesum_workspace_bytes(inp.nt, inp.K, int(freq.numel()))) \
-                > eng._ws.numel():
-            with torch.cuda.stream(st):
-                eng._workspace(inp.nt, inp.K, int(freq.numel()), freq.device)
+        eng._workspace(inp.nt, inp.K, int(freq.numel()), freq.device, stream=st)
         eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
                    hp=hp, hc=hc, k0=k0)
         sl["used"] = True
