@@ -115,6 +115,12 @@ def main():
     ap.add_argument("--pipeline", default="overlap", choices=["overlap", "serial"],
                     help="overlap: prepare(i+1) on a second stream beside sum(i), fused h+/hx; "
                          "serial: one stream, efd_modesum + efd_polarizations")
+    ap.add_argument("--sum-streams", type=int, default=1,
+                    help="overlap pipeline: consecutive mode sums alternate over this many streams "
+                         "(> 1 lets sum i+1 start during sum i's tail)")
+    ap.add_argument("--slots", type=int, default=2,
+                    help="overlap pipeline depth: workspaces in flight (preparation runs up to "
+                         "slots - 1 waveforms ahead of the sum)")
     args = ap.parse_args()
 
     import torch
@@ -143,7 +149,7 @@ def main():
     # i's mode sum runs on the sum stream; the sum writes h+/hx directly (fused polarisations).
     # "serial": one stream, efd_modesum then efd_polarizations (the unfused path).
     slots = []
-    for _ in range(2 if overlap else 1):
+    for _ in range(max(2, args.slots) if overlap else 1):
         hp = torch.empty(nf - k0, dtype=torch.complex128, device=dev)
         slots.append(dict(eng=ModeSumEngine(caustic=args.caustic), fhp=torch.view_as_real(hp),
                           fhc=torch.view_as_real(torch.empty_like(hp)),
@@ -151,7 +157,9 @@ def main():
                               torch.empty(nf, dtype=torch.complex128, device=dev)),
                           prep_done=torch.cuda.Event(), sum_done=None))
     s_prep = torch.cuda.Stream(dev)
-    s_sum = torch.cuda.Stream(dev) if overlap else s_prep
+    s_sums = [torch.cuda.Stream(dev) for _ in range(max(1, args.sum_streams))] if overlap \
+        else [s_prep]
+    s_sum = s_sums[0]
     lib = slots[0]["eng"].lib
 
     def step(i, ev=None):
@@ -164,11 +172,12 @@ def main():
             eng.launch(inp, freq, None, True, w["prefactor"], stream=s_prep.cuda_stream,
                        phase="prepare")
             sl["prep_done"].record(s_prep)
-            s_sum.wait_event(sl["prep_done"])
-            eng.launch(inp, freq, None, True, w["prefactor"], stream=s_sum.cuda_stream,
+            ss = s_sums[i % len(s_sums)]
+            ss.wait_event(sl["prep_done"])
+            eng.launch(inp, freq, None, True, w["prefactor"], stream=ss.cuda_stream,
                        prof_events=pe, hp=sl["fhp"], hc=sl["fhc"], k0=k0, phase="sum")
             done = torch.cuda.Event()
-            done.record(s_sum)
+            done.record(ss)
             sl["sum_done"] = done
         else:
             st = s_prep.cuda_stream
@@ -179,8 +188,8 @@ def main():
     evs = []
     for i in range(args.steps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s_sum)   # creates the events; the library re-records them around k_modesum
-        b.record(s_sum)
+        a.record(s_sums[i % len(s_sums)])   # creates the events; the library re-records them
+        b.record(s_sums[i % len(s_sums)])   # around k_modesum
         evs.append((a, b))
     for i in range(args.warmup):
         step(i)
@@ -261,7 +270,8 @@ def main():
                        "harmonics": K, "mn_groups": n_groups, "N_t": nt, "N_f": nf,
                        "contributions": C, "spa_evaluations": n_eval,
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
-                       "pipeline": args.pipeline},
+                       "pipeline": args.pipeline,
+                       "slots": len(slots), "sum_streams": len(s_sums)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_modesum", "kernel_ms": kern_ms,

@@ -70,7 +70,6 @@ constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds 
 constexpr int KEYCAP = EFD_KEYCAP;  // record keys per tile pass held in LDS
 constexpr int SEGWIN = EFD_SEGWIN_F * TILE;  // segments examined per window (tile list build)
 constexpr int MAX_K = 8192;         // harmonics per call (k_group sorts them in LDS)
-constexpr int64_t MAX_LANES = int64_t(1) << 28;   // k_modesum's packed record header
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
@@ -1159,7 +1158,7 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 constexpr int SCTAB = 512;
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
                                            double& s, double& c, double extra = 0.0,
-                                           bool use_extra = false) {
+                                           bool use_extra = false, double extra_scale = 1.0) {
     constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
     constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
     constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
@@ -1170,7 +1169,8 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     const double q = qs - SHIFTER;
     double r = fma(-q, STEP_1, x);
     r = fma(-q, STEP_2, r);
-    if (use_extra) r += extra;   // a small angle (|extra| < 1e-3) added after the reduction
+    // a small angle (|extra_scale * extra| < 1e-3) added after the reduction
+    if (use_extra) r = fma(extra_scale, extra, r);
     const int qi = __double2loint(qs);
     // (sin, cos)((q + shift) pi/256), addressed in bytes: v_lshl_add + v_and
     const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
@@ -1444,42 +1444,43 @@ __device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk,
 
 // The same factor in polar form, G = rho e^{i theta} (fast path, EFD_POLAR): log G of the
 // Hankel series, re-expanded as rho = sum_j RH_j u^j and theta = w sum_j TH_j u^j (y > 0; theta
-// is odd in y), u = w^2. The first omitted terms fall below 1e-17 at the same |y| bounds as
-// KB / KC (JSER_Y), so a record's series length J serves both forms. theta is added to the
-// reduced sin/cos argument (|r| <= pi/512, where it costs no rounding) and rho scales the
-// amplitude: two FP64 operations fewer per evaluation than rotating by (R + iI).
+// is odd in y), u = w^2, TH = {-0.069444444444444444444, 0.035525977366255144033,
+// -0.11095169967421124829, 0.85188445191064930488}. The first omitted terms fall below 1e-17 at
+// the same |y| bounds as KB / KC (JSER_Y), so a record's series length J serves both forms.
+// theta is added to the reduced sin/cos argument (|r| <= pi/512, where it costs no rounding) and
+// rho scales the amplitude: two FP64 operations fewer per evaluation than rotating by (R + iI).
 #ifndef EFD_POLAR
 #define EFD_POLAR 1
 #endif
-__constant__ double KTH[4] = {-0.069444444444444444444, 0.035525977366255144033,
-                              -0.11095169967421124829, 0.85188445191064930488};
 __constant__ double KRH[4] = {1.0, -0.034722222222222222222, 0.055097415123456790123,
                               -0.283034838766718107};
-static_assert(FAST_J <= 4, "KTH / KRH hold 4 terms");
-template <int J>
-__device__ __forceinline__ void kpolar(double ww, double& rho, double& th) {
-    if (J == 1) {
-        rho = 1.0;
-        th = ww * KTH[0];
-        return;
-    }
+// Runtime series length J as increments on the 2-term form, which every record evaluates (81% of
+// records need J = 2; for J = 1 the second terms fall below the rounding of the first): a
+// switch over J-term Horner chains merged its results through 64-bit register copies (2 VALU
+// per evaluation, each as costly as an FMA), the increments accumulate in place. theta comes
+// out in units of its leading coefficient (thn = theta / TH_0), so both chains start from the
+// inline constant 1.0 and the caller's add of theta to the reduced angle becomes an FMA with
+// TH_0: one VALU operation fewer per evaluation than the TH-form chain.
+constexpr double KTH0 = -0.069444444444444444444;   // TH_0
+__constant__ double KTHN[4] = {1.0, -0.51157407407407407407, 1.5977044753086419754,
+                               -12.267136107513349990};   // TH_j / TH_0
+__device__ __forceinline__ void kpolar_rt(int J, double ww, double& rho, double& thn) {
+    static_assert(FAST_J == 4, "kpolar_rt: increments up to 4 terms");
     const double uu = ww * ww;
-    double r = KRH[J - 1], t = KTH[J - 1];
-#pragma unroll
-    for (int j = J - 2; j >= 0; --j) {
-        r = fma(r, uu, KRH[j]);
-        t = fma(t, uu, KTH[j]);
+    double r = fma(KRH[1], uu, 1.0);   // KRH[0] == 1
+    double t = fma(KTHN[1], uu, 1.0);
+    if (J >= 3) {   // wave-uniform
+        const double u2 = uu * uu;
+        r = fma(KRH[2], u2, r);
+        t = fma(KTHN[2], u2, t);
+        if (J >= 4) {
+            const double u3 = u2 * uu;
+            r = fma(KRH[3], u3, r);
+            t = fma(KTHN[3], u3, t);
+        }
     }
     rho = r;
-    th = ww * t;
-}
-__device__ __forceinline__ void kpolar_rt(int J, double ww, double& rho, double& th) {
-    switch (J) {
-        case 1: kpolar<1>(ww, rho, th); break;
-        case 2: kpolar<2>(ww, rho, th); break;
-        case 3: kpolar<3>(ww, rho, th); break;
-        default: kpolar<FAST_J>(ww, rho, th); break;
-    }
+    thn = ww * t;
 }
 
 // K_{1/3} series with a wave-uniform runtime length J (1..FAST_J): the branches are scalar, and
@@ -1530,16 +1531,16 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
         const double t3 = fdds * a3;
         const double ww = t3 * t3;   // 1/|y|
         good = good & ((J < FAST_J) | (ww <= 1.0 / FAST_Y));
-        double rho, th;
-        kpolar_rt(J, ww, rho, th);
+        double rho, thn;
+        kpolar_rt(J, ww, rho, thn);
         // theta is odd in y: the sign of F' (= sign of y) onto it by one XOR of the high word
         const bool ok = act & good;
-        const double ths = ok ? __hiloint2double(__double2hiint(th) ^ (__double2hiint(fd) & INT32_MIN),
-                                                 __double2loint(th))
+        const double ths = ok ? __hiloint2double(__double2hiint(thn) ^ (__double2hiint(fd) & INT32_MIN),
+                                                 __double2loint(thn))
                               : 0.0;
         const double am = ok ? amp * rho : 0.0;
         double sn, cs;
-        sincos_tab(psi0, shift, sct, sn, cs, ths, true);
+        sincos_tab(psi0, shift, sct, sn, cs, ths, true, KTH0);   // theta = KTH0 * thn
         wr = am * cs;
         wi = am * sn;
         need_general = act & !good;
@@ -1568,12 +1569,80 @@ __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double 
     need_general = act & !good;
 }
 
+// Lane predicates as wave masks in scalar registers (EFD_SALU_MASKS): every VALU instruction
+// issues in 4 cycles per wave64, an FP64 FMA's cost, so the per-lane booleans of spa_fast_rt
+// (lane range: 2 integer compares per bin; the |y| test of a series-length-4 record, evaluated for
+// every record; the any-lane test of the general path: a select and a compare per record) are
+// replaced by masks: the lane range from the record's bounds in SALU (lane_range_mask), each
+// comparison's result taken by ballot (the compare itself writes the mask), the |y| test only
+// in a wave-uniform branch for records that need it, and the masks combined in SALU.
+#ifndef EFD_SALU_MASKS
+#define EFD_SALU_MASKS 1
+#endif
+// lanes l of the wave with lo <= l < hi (wave-uniform bounds, any range). Selects, not a clamp:
+// min/max of a uniform value becomes v_med3 + v_readfirstlane (2 VALU), the selects stay SALU.
+__device__ __forceinline__ uint64_t lanes_below(int32_t x) {
+    const uint64_t m = x >= 64 ? ~0ull : ((1ull << (x & 63)) - 1ull);
+    return x <= 0 ? 0ull : m;
+}
+__device__ __forceinline__ uint64_t lane_range_mask(int32_t lo, int32_t hi) {
+    return lanes_below(hi) & ~lanes_below(lo);
+}
+// spa_fast_rt with the active lanes given as a mask and the general-path lanes returned as one;
+// the same arithmetic (bitwise the same W and w)
+template <int CAUSTIC>
+__device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
+                                           int J, uint64_t actm, const double2* __restrict__ sct,
+                                           double& wr, double& wi, double& w, uint64_t& needm) {
+    static_assert(EFD_POLAR, "mask form of the polar fast path");
+    const double u = sfk - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    w = tt - it->tj;
+    uint64_t goodm = __builtin_amdgcn_ballot_w64((unsigned long long)__double_as_longlong(w) <
+                                                 (unsigned long long)__double_as_longlong(it->dtj));
+    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+    const double afd = fabs(fd);
+    goodm &= __builtin_amdgcn_ballot_w64(afd > 0.0);
+    // F' = 0 gives amp = NaN here; every quantity it reaches is selected away below
+    const double amp = rsqrt_pos(afd);
+    const double psi0 = fma(stfk, tt, -ph);
+    const int shift = fd > 0.0 ? 192 : -192;
+    double sn, cs;
+    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
+        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        const double a3 = amp * amp * amp;
+        const double t3 = fdds * a3;
+        const double ww = t3 * t3;   // 1/|y|
+        // J < FAST_J: the record's |y| bound covers every in-interval lane
+        if (J >= FAST_J) goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
+        double rho, thn;
+        kpolar_rt(J, ww, rho, thn);
+        const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
+        // theta is odd in y and thn > 0 where ok: the sign of F' (= sign of y) by a copysign
+        const double ths = ok ? copysign(thn, fd) : 0.0;
+        const double am = ok ? amp * rho : 0.0;
+        sincos_tab(psi0, shift, sct, sn, cs, ths, true, KTH0);   // theta = KTH0 * thn
+        wr = am * cs;
+        wi = am * sn;
+    } else {
+        const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
+        const double am = ok ? amp : 0.0;
+        sincos_tab(psi0, shift, sct, sn, cs);
+        wr = am * cs;
+        wi = am * sn;
+    }
+    needm = actm & ~goodm;
+}
+
 #if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
 // record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
 // FAST_Y, |y| < 18.4
 __device__ unsigned long long g_exp_count[32];  // [8..15]: |y| bands of kfactor_slow's J;
 // [16, 17]: cold wave evaluations / lanes (one-body kernel); [18..23]: overshoot bands of
-// max(-w, w - dtj) / dtj: < 1e-12, 1e-9, 1e-6, 1e-3, 1e-1, larger
+// max(-w, w - dtj) / dtj: < 1e-12, 1e-9, 1e-6, 1e-3, 1e-1, larger; [24, 25, 26]: chunk barrier
+// balance: sum over chunks of the busiest wave's record evaluations, of all waves' evaluations,
+// and the number of chunks
 __device__ unsigned int g_exp_tile[16384];       // record evaluations per tile (first 16384)
 __device__ unsigned long long g_exp_tclk[16384];  // wall clock (s_memrealtime) per tile
 #endif
@@ -1737,6 +1806,9 @@ __device__ __forceinline__ void modesum_tile(
     __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
     __shared__ int wcnt[(SEGWIN / TILE) * NWAVE];
     __shared__ double2 sctab[SCTAB];   // (sin, cos)(k pi/128) for sincos_tab
+#ifdef EFD_EXP_COUNT
+    __shared__ int wimb[2][NWAVE];     // records each wave evaluated in a chunk (barrier balance)
+#endif
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
     // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
@@ -1998,25 +2070,40 @@ __device__ __forceinline__ void modesum_tile(
             const int nin = (int)rfl((uint32_t)min(NC, cnt - c * NC));   // loop bound in an SGPR
             const Item* stg = stage[c & 1];
 #if EFD_UNIFIED_BODY
-            // the chunk's record headers, one lane per record, read from LDS once per chunk:
-            // hdr_a = klo[s] | s << 28 | jser << 29, hdr_b = khi[s]; each record then takes two
-            // v_readlane instead of an LDS round trip and 5 address / readfirstlane operations
+            // the chunk's record headers, one lane per record, read from LDS once per chunk and
+            // packed into one word: the sub-branch's lane range clamped to the tile, relative
+            // to its first lane (10 bits each), s and the series length: hdr = lo | hi << 10 |
+            // s << 20 | jser << 21. Each record then takes one v_readlane (a VALU instruction,
+            // as costly as an FMA) instead of an LDS round trip and 5 address / readfirstlane
+            // operations (round 1), or two readlanes of absolute bounds (round 2 first form).
             static_assert(FAST_J < 8, "header: jser in 3 bits");
-            uint32_t hdr_a = 0, hdr_b = 0;
+            static_assert(TILE_LANES < 1024, "header: tile-relative lane bounds in 10 bits");
+            uint32_t hdr = 0;
             if (lane < nin) {
                 const uint32_t kl = keys[c * NC + lane];
                 const int sl = (int)(kl & 1);
                 const Item* il = stg + lane;
-                hdr_a = (uint32_t)il->klo[sl] | ((uint32_t)sl << 28) | ((uint32_t)il->jser << 29);
-                hdr_b = (uint32_t)il->khi[sl];
+                const uint32_t lo = (uint32_t)min(max(il->klo[sl] - tlo, 0), TILE_LANES);
+                const uint32_t hi = (uint32_t)min(max(il->khi[sl] - tlo, 0), TILE_LANES);
+                hdr = lo | (hi << 10) | ((uint32_t)sl << 20) | ((uint32_t)il->jser << 21);
+            }
+#endif
+#ifdef EFD_EXP_COUNT
+            int nev = 0;
+            if (c > 0 && tid == 0) {
+                int mx = 0, sm = 0;
+                for (int w = 0; w < NWAVE; ++w) { mx = max(mx, wimb[(c - 1) & 1][w]); sm += wimb[(c - 1) & 1][w]; }
+                atomicAdd(&g_exp_count[24], (unsigned long long)mx);
+                atomicAdd(&g_exp_count[25], (unsigned long long)sm);
+                atomicAdd(&g_exp_count[26], 1ull);
             }
 #endif
             for (int ii = 0; ii < nin; ++ii) {
 #if EFD_UNIFIED_BODY
-                const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane((int)hdr_a, ii);
-                const int s = (int)((ha >> 28) & 1u);
-                const int32_t klo = (int32_t)(ha & 0x0fffffffu);
-                const int32_t khi = __builtin_amdgcn_readlane((int)hdr_b, ii);
+                const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane((int)hdr, ii);
+                const int s = (int)((ha >> 20) & 1u);
+                const int32_t klo = tlo + (int32_t)(ha & 1023u);
+                const int32_t khi = tlo + (int32_t)((ha >> 10) & 1023u);
                 const Item* it = stg + ii;
 #else
                 const uint32_t key = rfl(keys[c * NC + ii]);
@@ -2034,6 +2121,7 @@ __device__ __forceinline__ void modesum_tile(
                     continue;
                 }
 #ifdef EFD_EXP_COUNT
+                ++nev;
                 if (lane == 0) {
                     atomicAdd(&g_exp_count[0], 1ull);
                     if (tile < 16384) atomicAdd(&g_exp_tile[tile], 1u);
@@ -2120,7 +2208,7 @@ __device__ __forceinline__ void modesum_tile(
                     // wave-uniform values
 #ifdef EFD_EXP_JDIST   // records by series length [0..3], sub-branch flips [4], records [5]
                     if (lane == 0) {
-                        atomicAdd(&g_exp_count[min((int)(ha >> 29), 4) - 1], 1ull);
+                        atomicAdd(&g_exp_count[min((int)(ha >> 21), 4) - 1], 1ull);
                         atomicAdd(&g_exp_count[5], 1ull);
                         if (s != s_cur) atomicAdd(&g_exp_count[4], 1ull);
                     }
@@ -2138,11 +2226,24 @@ __device__ __forceinline__ void modesum_tile(
 #ifdef EFD_EXP_JFIX   // experiment: every record takes the FAST_J-term series (no J dispatch)
                     const int J = FAST_J;
 #else
-                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)(ha >> 29) : FAST_J;
+                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)(ha >> 21) : FAST_J;
 #endif
                     const double* xo = &it->b[s][0][0];
                     const double* xm = &it->b[1 - s][0][0];
                     double wr[BPL], wi[BPL], w[BPL];
+#if EFD_SALU_MASKS
+                    uint64_t needm[BPL], needany = 0;
+#pragma unroll
+                    for (int i = 0; i < BPL; ++i) {
+                        const int32_t base = w_lo + 64 * i;
+                        spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], J,
+                                            lane_range_mask(klo - base, khi - base), sctab, wr[i],
+                                            wi[i], w[i], needm[i]);
+                        need[i] = __builtin_amdgcn_inverse_ballot_w64(needm[i]);
+                        needany |= needm[i];
+                    }
+                    anyneed = needany != 0;
+#else
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t k = w_lo + 64 * i + lane;
@@ -2151,6 +2252,7 @@ __device__ __forceinline__ void modesum_tile(
                                              need[i]);
                         anyneed = anyneed | need[i];
                     }
+#endif
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
@@ -2162,7 +2264,11 @@ __device__ __forceinline__ void modesum_tile(
 #ifdef EFD_EXP_NOSLOW
                     anyneed = false;
 #endif
+#if EFD_SALU_MASKS
+                    if (__builtin_expect(anyneed, 0)) {   // cold: general path, some lanes
+#else
                     if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
+#endif
 #ifdef EFD_EXP_COUNT
                         {
                             unsigned long long nl_ = 0;
@@ -2194,6 +2300,9 @@ __device__ __forceinline__ void modesum_tile(
                 else by_j(I1{});
 #endif
             }
+#ifdef EFD_EXP_COUNT
+            if (lane == 0) wimb[c & 1][wave] = nev;
+#endif
             // retire this wave's LDS-DMA pieces, then the barrier publishes chunk c+1's stage
             __builtin_amdgcn_s_waitcnt(0x0f70);
             __syncthreads();
@@ -2703,8 +2812,6 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         return fail(EFD_ERR_ARG, "efd_modesum: unknown caustic mode");
     const int paired = a->grid_symmetric ? 1 : 0;
     const Layout L = make_layout(a->nt, a->K, a->nf, paired);
-    if (L.nlanes >= MAX_LANES)   // k_modesum packs a record's lane bound into 28 bits
-        return fail(EFD_ERR_ARG, "efd_modesum: more than 2^28 - 1 bins per side of the grid");
     if (workspace_bytes < L.total)
         return fail(EFD_ERR_WORKSPACE, "efd_modesum: workspace too small (see efd_modesum_workspace_bytes)");
 

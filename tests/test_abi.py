@@ -89,8 +89,7 @@ def test_header_constants_match_python():
 
 def test_argument_errors_are_host_side():
     """Shape errors return EFD_ERR_ARG with a message before anything touches the device, e.g.
-    a grid with more than 2^28 - 1 bins per side (k_modesum packs a record's lane bound into 28
-    bits of its chunk header)."""
+    a grid of 2^31 - 1 bins or more (lane indices are 32-bit)."""
     lib = _lib.load()
     fake = ctypes.c_void_p(16)   # never dereferenced: validation fails first
     a = _lib.ModesumArgs()
@@ -100,10 +99,10 @@ def test_argument_errors_are_host_side():
     a.nt, a.K, a.caustic, a.scale_re = 100, 3000, 1, 1.0
     a.grid_symmetric = 1
     buf = ctypes.create_string_buffer(256)
-    a.nf = 2 ** 29 + 1
+    a.nf = 2 ** 31 - 1
     assert lib.efd_modesum(ctypes.byref(a), fake, ctypes.c_size_t(1 << 40), None) == -1
     lib.efd_last_error(buf, 256)
-    assert b"2^28" in buf.value
+    assert b"nf out of range" in buf.value
     a.nf = 1000
     a.nt = 1
     assert lib.efd_modesum(ctypes.byref(a), fake, ctypes.c_size_t(1 << 40), None) == -1

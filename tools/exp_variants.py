@@ -22,6 +22,9 @@ SRC = os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc", "emrifd.hi
 sys.path.insert(0, ROOT)
 
 
+NWAVE = 4   # waves per k_modesum workgroup
+
+
 def lib_path(name):
     if name == "base":
         return os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "libemrifd.so")
@@ -122,7 +125,12 @@ def child(name, ref_path):
             ("record_evals", "cold_evals", "cold_lanes", "skips", "lanes_overshoot",
              "lanes_y_mid", "lanes_y_small", "unused", "y_ge153", "y_ge75", "y_ge48",
              "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18", "cold_wave_evals", "cold_wave_lanes",
-             "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1"))}
+             "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1",
+             "chunk_max_wave_evals", "chunk_wave_evals", "chunks"))}
+        c = out["counters_per_launch"]
+        if c["chunk_wave_evals"] > 0:
+            # wave-time lost at the chunk barriers if every record evaluation cost the same
+            out["barrier_idle_frac"] = 1.0 - c["chunk_wave_evals"] / (NWAVE * c["chunk_max_wave_evals"])
     print("EXPRESULT " + json.dumps(out), flush=True)
 
 
