@@ -128,6 +128,8 @@ struct __attribute__((aligned(16))) Item {
 };
 static_assert(sizeof(Item) == 288, "Item must be 288 B");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
+constexpr int B_PIECE = (int)offsetof(Item, b) / 16;   // first piece of b (b[0]: 4, b[1]: 4)
+static_assert(offsetof(Item, b) % 16 == 0 && sizeof(Item::b) == 8 * 16, "b: 8 whole pieces");
 #ifndef EFD_STAGE_ROUNDS
 #define EFD_STAGE_ROUNDS 2
 #endif
@@ -1394,54 +1396,6 @@ __device__ __forceinline__ double cubic(const double* __restrict__ c, double w) 
     return fma(fma(fma(c[0], w, c[1]), w, c[2]), w, c[3]);
 }
 
-// Branch-free SPA evaluation of interval record `it` on sub-branch S (g = -f for S = 0, +f for
-// S = 1) at the lane's bin: returns the group-independent factor
-//   W = Q e^{i(2 pi g t - Phi)}   (Q-factor notes above; arg Q_spa folded into the phase)
-// and w = t - t_j for the amplitude cubics, for lanes with `act` set. need_general is set for
-// active lanes the general path must redo (t(g) overshot the record's knot interval, F' = 0, or
-// |y| < FAST_Y in the uniform mode); W is 0 for those and for inactive lanes. Everything is
-// computed unconditionally and masked once (selects, no divergent branches).
-template <int S, int CAUSTIC, int J>
-__device__ __forceinline__ void spa_fast(const Item* __restrict__ it, double fk, double tfk,
-                                         bool act, const double2* __restrict__ sct, double& wr,
-                                         double& wi, double& w, bool& need_general) {
-    // g = +-fk (tfk = 2 pi fk): the sign is a source modifier, free
-    const double u = (S ? fk : -fk) - it->gx;
-    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
-    w = tt - it->tj;
-    // 0 <= w < dtj as one unsigned compare of the bit patterns (negative w and NaN fail)
-    bool good = (unsigned long long)__double_as_longlong(w) <
-                (unsigned long long)__double_as_longlong(it->dtj);
-    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
-    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-    const double afd = fabs(fd);
-    good = good & (afd > 0.0);
-    const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
-    // psi = 2 pi g t - Phi + sgn(F') 3 pi/4; the 3 pi/4 (192 table steps) goes in as an index
-    const double psi0 = fma(S ? tfk : -tfk, tt, -ph);
-    const int shift = fd > 0.0 ? 192 : -192;
-    double R = 1.0, I = 0.0;
-    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
-        // w = 3 F''^2 / (2 pi F'^3) = (fdd_scaled * |F'|^-3/2)^2 with the sign of F'
-        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
-        const double a3 = amp * amp * amp;
-        const double t3 = fdds * a3;
-        const double ww = copysign(t3 * t3, fd);
-        // J < FAST_J: the record's |y| bound covers every in-interval lane, no per-lane test
-        if (J == FAST_J) good = good & (fabs(ww) <= 1.0 / FAST_Y);
-        kseries<J>(ww, R, I);
-    }
-    // W = 0 unless this lane finishes here (the general path adds the others' terms)
-    const double a = (act & good) ? amp : 0.0;
-    R *= a;
-    I *= a;
-    double sn, cs;
-    sincos_tab(psi0, shift, sct, sn, cs);
-    wr = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, cs, -I * sn) : R * cs;
-    wi = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, sn, I * cs) : R * sn;
-    need_general = act & !good;
-}
-
 // The same factor in polar form, G = rho e^{i theta} (fast path, EFD_POLAR): log G of the
 // Hankel series, re-expanded as rho = sum_j RH_j u^j and theta = w sum_j TH_j u^j (y > 0; theta
 // is odd in y), u = w^2, TH = {-0.069444444444444444444, 0.035525977366255144033,
@@ -1494,12 +1448,17 @@ __device__ __forceinline__ void kseries_rt(int J, double ww, double& R, double& 
     }
 }
 
-// spa_fast with the sub-branch and the series length as wave-uniform runtime values: sfk, stfk
-// are g = +-fk, 2 pi g (the tile keeps them signed for the current sub-branch), J the record's
-// series length.
-// Same operations in the same order as spa_fast<S, CAUSTIC, J>, so bitwise the same result; one
-// body instead of 2 x 4 compiled copies, so the accumulators stay in place across records (the
-// copies' merge points cost 8 v_mov_b64 per record and the copies 8x the code).
+// Branch-free SPA evaluation of interval record `it` at the lane's bin: returns the
+// group-independent factor
+//   W = Q e^{i(2 pi g t - Phi)}   (Q-factor notes above; arg Q_spa folded into the phase)
+// and w = t - t_j for the amplitude cubics, for lanes with `act` set. need_general is set for
+// active lanes the general path must redo (t(g) overshot the record's knot interval, F' = 0, or
+// |y| < FAST_Y in the uniform mode); W is 0 for those and for inactive lanes. Everything is
+// computed unconditionally and masked once (selects, no divergent branches). The sub-branch
+// (g = -f or +f) and the series length are wave-uniform runtime values: sfk, stfk are g = +-fk,
+// 2 pi g (the tile keeps them signed for the current sub-branch), J the record's series length.
+// One body for every (sub-branch, J): round 1's 2 x 4 compiled copies merged the accumulators
+// through 8 v_mov_b64 per record and took 8x the code, for bitwise the same result.
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double sfk, double stfk,
                                             int J, bool act, const double2* __restrict__ sct,
@@ -1619,8 +1578,11 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         double rho, thn;
         kpolar_rt(J, ww, rho, thn);
         const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
-        // theta is odd in y and thn > 0 where ok: the sign of F' (= sign of y) by a copysign
-        const double ths = ok ? copysign(thn, fd) : 0.0;
+        // theta is odd in y and thn > 0 where ok: the sign of F' (= sign of y) by a copysign.
+        // Not masked: where ok, 0 < thn < 1/153; elsewhere min(|thn|, 1) keeps the angle finite
+        // (a NaN thn becomes 1; far outside the series' range thn is large of either sign), so
+        // sin/cos stay finite and the zero amplitude below zeroes W. |.| is a source modifier.
+        const double ths = copysign(fmin(fabs(thn), 1.0), fd);
         const double am = ok ? amp * rho : 0.0;
         sincos_tab(psi0, shift, sct, sn, cs, ths, true, KTH0);   // theta = KTH0 * thn
         wr = am * cs;
@@ -1648,12 +1610,14 @@ __device__ unsigned long long g_exp_tclk[16384];  // wall clock (s_memrealtime) 
 #endif
 
 // General (cold) path: scipy interval selection for t(g) and the full K_{1/3} evaluation.
-// Returns W and both group amplitudes at t(g).
+// Returns W and both group amplitudes at t(g), the own bin's first (b[0], b[1]: the staged
+// record's b[0]; from the spline coefficients, Bp for s = 0 and Bm for s = 1).
 struct ColdEval {
     double wr, wi, b[4];
 };
 template <int CAUSTIC>
-__device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double g, int h, int jrec,
+__device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double g, int s, int h,
+                                             int jrec,
                                              const double* __restrict__ t, int nt, int K,
                                              const int32_t* __restrict__ gm,
                                              const int32_t* __restrict__ gn,
@@ -1686,7 +1650,7 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
         }
 #endif
         const FwdEval fe = forward_generic(tt, t, nt, jrec, h, K, gm[h], gn[h], coefA, coefT);
-        for (int q = 0; q < 4; ++q) c.b[q] = fe.b[q];
+        for (int q = 0; q < 4; ++q) c.b[q] = fe.b[s ? q ^ 2 : q];
         ph = fe.ph; fd = fe.fd; fdd = fe.fdd;
     }
     const double amp = fd != 0.0 ? rsqrt(fabs(fd)) : 0.0;
@@ -1770,13 +1734,6 @@ template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
 // 5 waves with a one-round stage: 1.07 ms)
 #ifndef EFD_WAVES_PER_EU
 #define EFD_WAVES_PER_EU 4
-#endif
-// 1: one evaluation body with the sub-branch sign and series length as wave-uniform runtime
-// values (spa_fast_rt); 0: the compile-time (S, J) instantiations (kept for the EFD_EXP_*
-// experiments). Bitwise-identical results and the same speed (1.13 vs 1.15 ms at config 2); the
-// runtime form is 2.3x less code and has no VGPR spills.
-#ifndef EFD_UNIFIED_BODY
-#define EFD_UNIFIED_BODY 1
 #endif
 // 1: the tiles' record lists are built by a lists-only k_modesum instance in the preparation
 // phase (k_tile_lists role) and DMA'd in by the sum; tiles whose list needs more than one
@@ -1888,7 +1845,6 @@ __device__ __forceinline__ void modesum_tile(
         tfk[i] = TWO_PI * fk[i];
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
-#if EFD_UNIFIED_BODY
     // Sub-branch sign state (wave-uniform): fk, tfk hold g = -+f, 2 pi g of the sub-branch s_cur
     // and own_i, mir_i hold sg * (the true sums), sg = -1 for s_cur = 1. A record of the other
     // sub-branch flips the 4 BPL registers in place (one v_xor each) instead of making signed
@@ -1897,7 +1853,6 @@ __device__ __forceinline__ void modesum_tile(
     int s_cur = 0;
 #pragma unroll
     for (int i = 0; i < BPL; ++i) { fk[i] = -fk[i]; tfk[i] = -tfk[i]; }   // s = 0: g = -f
-#endif
 
     // staging: a record is PIECES pieces of 16 B; NC records take at most ROUNDS pieces per thread.
     // The pieces go global -> LDS directly (gfx950 global_load_lds_dwordx4: no VGPR staging,
@@ -1912,8 +1867,12 @@ __device__ __forceinline__ void modesum_tile(
             const int p_ = rd_ * TILE + tid;                                                  \
             const int r_ = p_ / PIECES, q_ = p_ - r_ * PIECES;                                \
             if (r_ < NC && (c) * NC + r_ < cnt) {                                             \
-                const uint4* src_ =                                                           \
-                    reinterpret_cast<const uint4*>(items + (keys[(c) * NC + r_] >> 1)) + q_;  \
+                const uint32_t key_ = keys[(c) * NC + r_];                                    \
+                /* sub-branch 1: b[0] and b[1] trade places in the stage, so the own bin's */ \
+                /* amplitudes are always at b[0] (fixed LDS offsets in the hot loop) */       \
+                const int qs_ = ((key_ & 1u) && q_ >= B_PIECE && q_ < B_PIECE + 8)            \
+                                    ? ((q_ - B_PIECE + 4) & 7) + B_PIECE : q_;                \
+                const uint4* src_ = reinterpret_cast<const uint4*>(items + (key_ >> 1)) + qs_; \
                 uint4* dst_ = reinterpret_cast<uint4*>(&stage[(buf)][0]) + rd_ * TILE + wave * 64; \
                 glds16(src_, dst_);                                                           \
             }                                                                                 \
@@ -2069,7 +2028,6 @@ __device__ __forceinline__ void modesum_tile(
             if (c + 1 < nchunk) EFD_GLDS(c + 1, (c + 1) & 1);
             const int nin = (int)rfl((uint32_t)min(NC, cnt - c * NC));   // loop bound in an SGPR
             const Item* stg = stage[c & 1];
-#if EFD_UNIFIED_BODY
             // the chunk's record headers, one lane per record, read from LDS once per chunk and
             // packed into one word: the sub-branch's lane range clamped to the tile, relative
             // to its first lane (10 bits each), s and the series length: hdr = lo | hi << 10 |
@@ -2087,7 +2045,6 @@ __device__ __forceinline__ void modesum_tile(
                 const uint32_t hi = (uint32_t)min(max(il->khi[sl] - tlo, 0), TILE_LANES);
                 hdr = lo | (hi << 10) | ((uint32_t)sl << 20) | ((uint32_t)il->jser << 21);
             }
-#endif
 #ifdef EFD_EXP_COUNT
             int nev = 0;
             if (c > 0 && tid == 0) {
@@ -2099,21 +2056,11 @@ __device__ __forceinline__ void modesum_tile(
             }
 #endif
             for (int ii = 0; ii < nin; ++ii) {
-#if EFD_UNIFIED_BODY
                 const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane((int)hdr, ii);
                 const int s = (int)((ha >> 20) & 1u);
                 const int32_t klo = tlo + (int32_t)(ha & 1023u);
                 const int32_t khi = tlo + (int32_t)((ha >> 10) & 1023u);
                 const Item* it = stg + ii;
-#else
-                const uint32_t key = rfl(keys[c * NC + ii]);
-                // S = 0: g = -f (parent at the own bin, partner at the mirror); S = 1: g = +f
-                // (partner at the own bin, parent at the mirror). Bm is zero for m = 0 groups.
-                const int s = (int)(key & 1);
-                const Item* it = stg + ii;
-                const int32_t klo = (int32_t)rfl((uint32_t)it->klo[s]);
-                const int32_t khi = (int32_t)rfl((uint32_t)it->khi[s]);
-#endif
                 if (khi <= w_lo || klo >= w_hi) {              // misses this wave's chunk
 #ifdef EFD_EXP_COUNT
                     if (lane == 0) atomicAdd(&g_exp_count[3], 1ull);
@@ -2129,80 +2076,6 @@ __device__ __forceinline__ void modesum_tile(
 #endif
                 bool anyneed = false;
                 bool need[BPL];
-                auto body = [&](auto Sc, auto Jc) {
-                    constexpr int S = decltype(Sc)::value;
-                    constexpr int J = decltype(Jc)::value;
-                    const double* xo = &it->b[S][0][0];       // own bin: b[S] (re 0..3, im 4..7)
-                    const double* xm = &it->b[1 - S][0][0];   // mirror: b[1-S]
-#pragma unroll
-                    for (int i = 0; i < BPL; ++i) {
-                        const int32_t k = w_lo + 64 * i + lane;
-                        const bool act = (k >= klo) & (k < khi);
-                        double wr, wi, w;
-                        spa_fast<S, CAUSTIC, J>(it, fk[i], tfk[i], act, sctab, wr, wi, w, need[i]);
-#ifdef EFD_EXP_DOUBLE   // timing experiment: the fast path's marginal cost (evaluated twice)
-                        {
-                            double wr2, wi2, w2;
-                            bool n2;
-                            spa_fast<S, CAUSTIC, J>(it, fk[i] * (1.0 + 1e-17 * wr), tfk[i], act,
-                                                 sctab, wr2, wi2, w2, n2);
-                            wr = 0.5 * (wr + wr2);
-                            wi = 0.5 * (wi + wi2);
-                            w = 0.5 * (w + w2);
-                        }
-#endif
-                        anyneed = anyneed | need[i];
-                        const double xr = cubic(xo, w), xi = cubic(xo + 4, w);
-                        const double zr = PAIRED ? cubic(xm, w) : 0.0;
-                        const double zi = PAIRED ? cubic(xm + 4, w) : 0.0;
-                        accumulate<S, PAIRED>(wr, wi, xr, xi, zr, zi, own_r[i], own_i[i],
-                                              mir_r[i], mir_i[i]);
-                    }
-#ifdef EFD_EXP_NOSLOW
-                    anyneed = false;
-#endif
-                    if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
-#ifdef EFD_EXP_COUNT
-                        {
-                            const unsigned long long nl_ = __popcll(__ballot(need[0])) +
-                                (BPL > 1 ? __popcll(__ballot(need[BPL - 1])) : 0);
-                            if (lane == 0) {
-                                atomicAdd(&g_exp_count[1], 1ull);
-                                atomicAdd(&g_exp_count[2], nl_);
-                            }
-                        }
-#endif
-                        const uint32_t kc = rfl(keys[c * NC + ii]);
-                        const int hg = (int)((kc >> 1) / (uint32_t)ni);   // the record's group
-                        const int jr = (int)((kc >> 1) - (uint32_t)hg * (uint32_t)ni);   // interval
-#pragma unroll
-                        for (int i = 0; i < BPL; ++i) {
-                            if (need[i]) {
-                                const ColdEval ce = spa_general<CAUSTIC>(
-                                    it, S ? fk[i] : -fk[i], hg, jr, t, nt, K, gm, gn, coefA, coefT);
-                                accumulate<S, PAIRED>(ce.wr, ce.wi, ce.b[2 * S], ce.b[2 * S + 1],
-                                                      ce.b[2 - 2 * S], ce.b[3 - 2 * S], own_r[i],
-                                                      own_i[i], mir_r[i], mir_i[i]);
-                            }
-                        }
-                    }
-                };
-                // wave-uniform dispatch on (S, series length J of the record)
-                using I0 = std::integral_constant<int, 0>;
-                using I1 = std::integral_constant<int, 1>;
-                auto by_j = [&](auto Sc) {
-                    if (CAUSTIC != EFD_CAUSTIC_UNIFORM) {
-                        body(Sc, std::integral_constant<int, FAST_J>{});
-                        return;
-                    }
-                    switch ((int)rfl((uint32_t)it->jser)) {
-                        case 1: body(Sc, std::integral_constant<int, 1>{}); break;
-                        case 2: body(Sc, std::integral_constant<int, 2>{}); break;
-                        case 3: body(Sc, std::integral_constant<int, 3>{}); break;
-                        default: body(Sc, std::integral_constant<int, FAST_J>{}); break;
-                    }
-                };
-#if EFD_UNIFIED_BODY
                 {
                     // one body: sub-branch sign (the register state above) and series length as
                     // wave-uniform values
@@ -2228,8 +2101,9 @@ __device__ __forceinline__ void modesum_tile(
 #else
                     const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)(ha >> 21) : FAST_J;
 #endif
-                    const double* xo = &it->b[s][0][0];
-                    const double* xm = &it->b[1 - s][0][0];
+                    // the stage holds b[s] at b[0] (EFD_GLDS swaps the halves for s = 1)
+                    const double* xo = &it->b[0][0][0];
+                    const double* xm = &it->b[1][0][0];
                     double wr[BPL], wi[BPL], w[BPL];
 #if EFD_SALU_MASKS
                     uint64_t needm[BPL], needany = 0;
@@ -2287,18 +2161,14 @@ __device__ __forceinline__ void modesum_tile(
                         for (int i = 0; i < BPL; ++i) {
                             if (need[i]) {
                                 const ColdEval ce = spa_general<CAUSTIC>(
-                                    it, fk[i], hg, jr, t, nt, K, gm, gn, coefA, coefT);
-                                accumulate<0, PAIRED>(ce.wr, ce.wi, ce.b[2 * s], ce.b[2 * s + 1],
-                                                      ce.b[2 - 2 * s], ce.b[3 - 2 * s], own_r[i],
-                                                      own_i[i], mir_r[i], mir_i[i]);
+                                    it, fk[i], s, hg, jr, t, nt, K, gm, gn, coefA, coefT);
+                                accumulate<0, PAIRED>(ce.wr, ce.wi, ce.b[0], ce.b[1], ce.b[2],
+                                                      ce.b[3], own_r[i], own_i[i], mir_r[i],
+                                                      mir_i[i]);
                             }
                         }
                     }
                 }
-#else
-                if (s == 0) by_j(I0{});
-                else by_j(I1{});
-#endif
             }
 #ifdef EFD_EXP_COUNT
             if (lane == 0) wimb[c & 1][wave] = nev;
@@ -2311,11 +2181,9 @@ __device__ __forceinline__ void modesum_tile(
         if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
-#if EFD_UNIFIED_BODY
     if (s_cur)
 #pragma unroll
         for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
-#endif
 
     // S is written when out != NULL; on a symmetric grid h+ and hx of bins [k0, nf) are written
     // straight from the registers when hp != NULL (the lane holds S(k) and S(nf-1-k), the two
