@@ -121,6 +121,9 @@ def main():
     ap.add_argument("--slots", type=int, default=2,
                     help="overlap pipeline depth: workspaces in flight (preparation runs up to "
                          "slots - 1 waveforms ahead of the sum)")
+    ap.add_argument("--diag-sum-only", action="store_true",
+                    help="diagnostic, not the metric: each slot is prepared once in the warm-up, "
+                         "then every step runs only the mode sum (the sum-stream ceiling)")
     args = ap.parse_args()
 
     import torch
@@ -167,13 +170,14 @@ def main():
         eng = sl["eng"]
         pe = (ev[0].cuda_event, ev[1].cuda_event) if ev is not None else (None, None)
         if overlap:
-            if sl["sum_done"] is not None:        # the slot's previous sum has read its workspace
-                s_prep.wait_event(sl["sum_done"])
-            eng.launch(inp, freq, None, True, w["prefactor"], stream=s_prep.cuda_stream,
-                       phase="prepare")
-            sl["prep_done"].record(s_prep)
             ss = s_sums[i % len(s_sums)]
-            ss.wait_event(sl["prep_done"])
+            if not (args.diag_sum_only and i >= len(slots)):
+                if sl["sum_done"] is not None:    # the slot's previous sum has read its workspace
+                    s_prep.wait_event(sl["sum_done"])
+                eng.launch(inp, freq, None, True, w["prefactor"], stream=s_prep.cuda_stream,
+                           phase="prepare")
+                sl["prep_done"].record(s_prep)
+                ss.wait_event(sl["prep_done"])
             eng.launch(inp, freq, None, True, w["prefactor"], stream=ss.cuda_stream,
                        prof_events=pe, hp=sl["fhp"], hc=sl["fhc"], k0=k0, phase="sum")
             done = torch.cuda.Event()
@@ -270,7 +274,8 @@ def main():
                        "harmonics": K, "mn_groups": n_groups, "N_t": nt, "N_f": nf,
                        "contributions": C, "spa_evaluations": n_eval,
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
-                       "pipeline": args.pipeline,
+                       "pipeline": args.pipeline + (" (diagnostic: sum only)"
+                                                    if args.diag_sum_only else ""),
                        "slots": len(slots), "sum_streams": len(s_sums)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -69,7 +69,7 @@ constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds 
 #endif
 constexpr int KEYCAP = EFD_KEYCAP;  // record keys per tile pass held in LDS
 constexpr int SEGWIN = EFD_SEGWIN_F * TILE;  // segments examined per window (tile list build)
-constexpr int MAX_K = 8192;         // harmonics per call (k_group sorts them in LDS)
+constexpr int MAX_K = 8192;         // harmonics per call
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
@@ -150,6 +150,7 @@ static_assert(sizeof(Header) == 64, "Header must be 64 B");
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
         seginfo, nseg, slotlh, slotinfo, slotcnt, slottiles, segbase, stb0, stb1, gm, gn, gstart,
+        gkeys,
         gmem, gamp, sctab, tkeys, tcnt, tperm, total;
     int64_t stbcap;
     int64_t ntiles, nlanes;
@@ -191,6 +192,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.gn = take(sizeof(int32_t) * K);
     L.gstart = take(sizeof(int32_t) * (K + 1));
     L.gmem = take(sizeof(int32_t) * K);
+    L.gkeys = take(sizeof(unsigned long long) * (size_t)MAX_K);   // k_group's general-case sort
     L.gamp = take(sizeof(double) * nt * 4 * K);
     L.sctab = take(sizeof(double) * 2 * 512);
     L.tkeys = take(sizeof(uint32_t) * (size_t)L.ntiles * KEYCAP);   // prebuilt tile lists
@@ -318,67 +320,167 @@ __device__ __forceinline__ double dcubic(const double* c, double w) {
 //   gm[g], gn[g]; members gmem[gstart[g] .. gstart[g+1]); G = hdr->groups.
 // The order is a function of (m, n) alone, so everything downstream is deterministic.
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ marr,
-                                                const int32_t* __restrict__ narr, int K,
-                                                int32_t* __restrict__ gm, int32_t* __restrict__ gn,
-                                                int32_t* __restrict__ gstart,
-                                                int32_t* __restrict__ gmem,
-                                                Header* __restrict__ hdr,
-                                                double2* __restrict__ sctab_g) {
-    __shared__ unsigned long long key[MAX_K];
+// K0: (m, n) groups. Groups ascend in (m, n), members in harmonic index h (the order every later
+// kernel and the oracle's grouping use). One 256-thread workgroup with a small LDS footprint: it
+// runs while the previous waveform's mode sum holds the GPU, so it must fit where one k_modesum
+// workgroup has left a CU (round 1's 1024-thread, 68 KB-LDS bitonic sort needed two to leave the
+// same CU at once and waited up to the end of that sum's dispatch, delaying the whole
+// preparation chain). Counting sort over the (m, n) box the harmonics span when it has at most
+// GB_CAP cells (FEW's l <= 10, |n| <= 30: 21 x 61); otherwise a bitonic sort of (m, n, h) keys
+// in the global scratch gkeys. Both give the same groups and member order.
+constexpr int GB_CAP = 2048;
+__device__ __forceinline__ void group_minmax(int& v_lo, int& v_hi, int* red, int slot) {
+    for (int o = 32; o > 0; o >>= 1) {
+        v_lo = min(v_lo, __shfl_xor(v_lo, o));
+        v_hi = max(v_hi, __shfl_xor(v_hi, o));
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { red[wave * 4 + slot] = v_lo; red[16 + wave * 4 + slot] = v_hi; }
+}
+__global__ __launch_bounds__(256) void k_group(const int32_t* __restrict__ marr,
+                                               const int32_t* __restrict__ narr, int K,
+                                               int32_t* __restrict__ gm, int32_t* __restrict__ gn,
+                                               int32_t* __restrict__ gstart,
+                                               int32_t* __restrict__ gmem,
+                                               Header* __restrict__ hdr,
+                                               double2* __restrict__ sctab_g,
+                                               unsigned long long* __restrict__ gkeys) {
+    constexpr int NTH = 256, NW = NTH / 64;
+    __shared__ int bcnt[GB_CAP], boff[GB_CAP];
+    __shared__ int red[32];
+    __shared__ int wsum[2 * NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // k_modesum's (sin, cos)(k pi/256) table, computed once per waveform here and copied into
     // each tile's LDS by LDS-DMA (cheaper than 512 sincospi per tile at small harmonic counts)
-    if (sctab_g != nullptr && threadIdx.x < 512) {
-        double sv, cv;
-        sincospi((double)threadIdx.x / 256.0, &sv, &cv);
-        sctab_g[threadIdx.x] = make_double2(sv, cv);
+    if (sctab_g != nullptr)
+        for (int i = tid; i < 512; i += NTH) {
+            double sv, cv;
+            sincospi((double)i / 256.0, &sv, &cv);
+            sctab_g[i] = make_double2(sv, cv);
+        }
+    auto mval = [&](int i) { return min(max(marr[i], -256), 255); };
+    auto nval = [&](int i) { return min(max(narr[i], -1024), 1023); };
+    int mlo = INT32_MAX, mhi = INT32_MIN, nlo = INT32_MAX, nhi = INT32_MIN;
+    for (int i = tid; i < K; i += NTH) {
+        const int m = marr[i], n = narr[i];
+        if (m < -256 || m > 255 || n < -1024 || n > 1023) atomicOr(&hdr->bad_mn, 1);
+        mlo = min(mlo, mval(i)); mhi = max(mhi, mval(i));
+        nlo = min(nlo, nval(i)); nhi = max(nhi, nval(i));
     }
-    __shared__ int part[1024];
-    const int tid = threadIdx.x;
+    group_minmax(mlo, mhi, red, 0);
+    group_minmax(nlo, nhi, red, 1);
+    __syncthreads();
+    mlo = red[0]; mhi = red[16]; nlo = red[1]; nhi = red[17];
+    for (int w = 1; w < NW; ++w) {
+        mlo = min(mlo, red[w * 4]); mhi = max(mhi, red[16 + w * 4]);
+        nlo = min(nlo, red[w * 4 + 1]); nhi = max(nhi, red[16 + w * 4 + 1]);
+    }
+    const int nbn = nhi - nlo + 1;
+    const int64_t nb = (int64_t)(mhi - mlo + 1) * nbn;
+    if (nb <= GB_CAP) {
+        // ---- counting sort over the (m, n) cells: counts, then one pass over the cells (per
+        // thread a block of consecutive cells) writes the groups and the cells' offsets
+        const int NB = (int)nb;
+        auto cell = [&](int i) { return (mval(i) - mlo) * nbn + (nval(i) - nlo); };
+        for (int b = tid; b < NB; b += NTH) bcnt[b] = 0;
+        __syncthreads();
+        for (int i = tid; i < K; i += NTH) atomicAdd(&bcnt[cell(i)], 1);
+        __syncthreads();
+        const int per = (NB + NTH - 1) / NTH;
+        const int b0 = min(NB, tid * per), b1 = min(NB, b0 + per);
+        int cm = 0, gmine = 0;
+        for (int b = b0; b < b1; ++b) { cm += bcnt[b]; gmine += bcnt[b] > 0; }
+        int ci = cm, gi = gmine;   // inclusive wave scans, then across waves
+        for (int o = 1; o < 64; o <<= 1) {
+            const int vc = __shfl_up(ci, o, 64), vg = __shfl_up(gi, o, 64);
+            if (lane >= o) { ci += vc; gi += vg; }
+        }
+        if (lane == 63) { wsum[wave] = ci; wsum[NW + wave] = gi; }
+        __syncthreads();
+        int off = ci - cm, g = gi - gmine, G = 0;
+        for (int w = 0; w < NW; ++w) {
+            if (w < wave) { off += wsum[w]; g += wsum[NW + w]; }
+            G += wsum[NW + w];
+        }
+        for (int b = b0; b < b1; ++b) {
+            const int c = bcnt[b];
+            boff[b] = off;
+            if (c > 0) {
+                gm[g] = mlo + b / nbn;
+                gn[g] = nlo + b % nbn;
+                gstart[g] = off;
+                ++g;
+            }
+            off += c;
+        }
+        __syncthreads();
+        // members into their cells (any order), then each cell sorted by h (l values of one
+        // (m, n): a handful of members)
+        for (int i = tid; i < K; i += NTH) gmem[atomicAdd(&boff[cell(i)], 1)] = i;
+        __syncthreads();
+        for (int b = b0; b < b1; ++b) {
+            const int c = bcnt[b];
+            if (c < 2) continue;
+            int32_t* mem = gmem + (boff[b] - c);
+            for (int x = 1; x < c; ++x) {
+                const int32_t v = mem[x];
+                int y = x - 1;
+                while (y >= 0 && mem[y] > v) { mem[y + 1] = mem[y]; --y; }
+                mem[y + 1] = v;
+            }
+        }
+        if (tid == 0) {
+            gstart[G] = K;
+            hdr->groups = G;
+        }
+        return;
+    }
+    // ---- general (m, n) ranges: bitonic sort of ((m, n) << 32 | h) keys in global scratch
     int P = 1;
     while (P < K) P <<= 1;
-    for (int i = tid; i < P; i += 1024) {
+    for (int i = tid; i < P; i += NTH) {
         unsigned long long k = ~0ull;
         if (i < K) {
-            const int m = marr[i], n = narr[i];
-            if (m < -256 || m > 255 || n < -1024 || n > 1023) atomicOr(&hdr->bad_mn, 1);
-            const unsigned gk = ((unsigned)(m + 256) & 511u) << 11 | ((unsigned)(n + 1024) & 2047u);
+            const unsigned gk = ((unsigned)(mval(i) + 256) << 11) | (unsigned)(nval(i) + 1024);
             k = ((unsigned long long)gk << 32) | (unsigned)i;
         }
-        key[i] = k;
+        gkeys[i] = k;
     }
     __syncthreads();
     for (int size = 2; size <= P; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = tid; t < P / 2; t += 1024) {
+            for (int t = tid; t < P / 2; t += NTH) {
                 const int lo = 2 * t - (t & (stride - 1));   // index with bit `stride` clear
                 const int hi = lo + stride;
                 const bool up = (lo & size) == 0;
-                const unsigned long long a = key[lo], b = key[hi];
-                if ((a > b) == up) { key[lo] = b; key[hi] = a; }
+                const unsigned long long a = gkeys[lo], b = gkeys[hi];
+                if ((a > b) == up) { gkeys[lo] = b; gkeys[hi] = a; }
             }
             __syncthreads();
         }
     }
     // group starts: position p starts a group if its (m, n) differs from p - 1; exclusive scan
     // of the start flags over per-thread blocks of consecutive positions
-    const int per = (K + 1023) / 1024;
+    const int per = (K + NTH - 1) / NTH;
     const int p0 = min(K, tid * per), p1 = min(K, p0 + per);
     int mine = 0;
-    for (int p = p0; p < p1; ++p) mine += (p == 0 || (key[p] >> 32) != (key[p - 1] >> 32));
-    part[tid] = mine;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = tid >= o ? part[tid - o] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    for (int p = p0; p < p1; ++p) mine += (p == 0 || (gkeys[p] >> 32) != (gkeys[p - 1] >> 32));
+    int incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
     }
-    int g = part[tid] - mine;   // groups started before p0
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int g = incl - mine, G = 0;
+    for (int w = 0; w < NW; ++w) {
+        if (w < wave) g += wsum[w];
+        G += wsum[w];
+    }
     for (int p = p0; p < p1; ++p) {
-        const unsigned long long k = key[p];
+        const unsigned long long k = gkeys[p];
         gmem[p] = (int32_t)(unsigned)(k & 0xffffffffu);
-        if (p == 0 || (k >> 32) != (key[p - 1] >> 32)) {
+        if (p == 0 || (k >> 32) != (gkeys[p - 1] >> 32)) {
             const unsigned gk = (unsigned)(k >> 32);
             gm[g] = (int32_t)(gk >> 11) - 256;
             gn[g] = (int32_t)(gk & 2047u) - 1024;
@@ -386,9 +488,9 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ marr
             ++g;
         }
     }
-    if (tid == 1023) {
-        gstart[part[1023]] = K;
-        hdr->groups = part[1023];
+    if (tid == 0) {
+        gstart[G] = K;
+        hdr->groups = G;
     }
 }
 
@@ -2255,7 +2357,12 @@ __device__ __forceinline__ void modesum_tile(
 
 // K8: the mode sum (one workgroup per tile; prebuilt lists when tcnt is given)
 template <bool PAIRED, int CAUSTIC, int BPL>
+#ifdef EFD_MODESUM_VGPRS   // experiment: a VGPR cap below 128 leaves room for other waves
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
+__attribute__((amdgpu_num_vgpr(EFD_MODESUM_VGPRS)))
+#else
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
+#endif
 void k_modesum(EFD_MODESUM_PARAMS) {
     modesum_tile<PAIRED, CAUSTIC, BPL, false>(EFD_MODESUM_ARGS);
 }
@@ -2718,8 +2825,8 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
 
     // K0: (m, n) groups
-    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
-                       hdr, sctab_g);
+    hipLaunchKernelGGL(k_group, dim3(1), dim3(256), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
+                       hdr, sctab_g, (unsigned long long*)(ws + L.gkeys));
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
                        a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
@@ -2774,6 +2881,10 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     {
         const int64_t gq = 8 * XCD_GROUP;
         const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
+#ifdef EFD_EXP_SKIP_TL   // diagnostic: after the warm-up, reuse the lists (same inputs only)
+        static int exp_calls = 0;
+        if (++exp_calls > 8) {} else
+#endif
         if (paired)
             hipLaunchKernelGGL((k_tile_lists<true>), grid, block, 0, st,
                                items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
@@ -2876,7 +2987,7 @@ int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* ev
 
 // TD workspace: the FD layout's grouping and spline buffers only (no records, no tile lists)
 struct TdLayout {
-    size_t header, coefA, coefT, kslope, tscratch, gm, gn, gstart, gmem, gamp, total;
+    size_t header, coefA, coefT, kslope, tscratch, gm, gn, gstart, gmem, gkeys, gamp, total;
 };
 static TdLayout make_td_layout(int32_t nt, int32_t K) {
     TdLayout L{};
@@ -2892,6 +3003,7 @@ static TdLayout make_td_layout(int32_t nt, int32_t K) {
     L.gn = take(sizeof(int32_t) * K);
     L.gstart = take(sizeof(int32_t) * (K + 1));
     L.gmem = take(sizeof(int32_t) * K);
+    L.gkeys = take(sizeof(unsigned long long) * (size_t)MAX_K);
     L.gamp = take(sizeof(double) * nt * 4 * K);
     L.total = off;
     return L;
@@ -2932,8 +3044,8 @@ int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes
     const int nt = a->nt, K = a->K;
 
     HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
-    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
-                       hdr, (double2*)nullptr);
+    hipLaunchKernelGGL(k_group, dim3(1), dim3(256), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
+                       hdr, (double2*)nullptr, (unsigned long long*)(ws + L.gkeys));
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
                        a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);

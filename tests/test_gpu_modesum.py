@@ -242,3 +242,20 @@ def test_fused_polarizations_and_two_phase_api(multimode):
     with pytest.raises(_lib.EFDError):   # fused outputs need a symmetric grid
         eng.launch(inp, freq, None, False, d["prefactor"], hp=torch.view_as_real(hp),
                    hc=torch.view_as_real(hc), k0=0)
+
+
+def test_wide_mn_range_grouping(multimode):
+    """k_group's two paths: the counting sort over the (m, n) box the harmonics span (at most
+    2048 cells, every other test) and, past that, the bitonic sort of (m, n, h) keys. Shifting n
+    of every third harmonic by 250 widens the box to > 2048 cells (those harmonics then lie
+    beyond the grid's Nyquist frequency); the spectrum of the others, grouped by the second
+    path, must still match the oracle (which takes the harmonics one by one)."""
+    d = dict(multimode)
+    n = np.array(d["n"]).copy()
+    n[::3] += 250
+    d["n"] = n
+    m = np.asarray(d["m"])
+    assert (m.max() - m.min() + 1) * (n.max() - n.min() + 1) > 2048
+    S, eng = _gpu(d, d["freq"])
+    R = _oracle(d, d["freq"])
+    assert _relerr(S, R) < RTOL
