@@ -1829,7 +1829,7 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst) {
 // term in a cold block. The sub-branch S of a record is wave-uniform: each S has its own copy of
 // the evaluation (compile-time signs and LDS offsets).
 // ----------------------------------------------------------------------------------------
-template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
+template <bool PAIRED, int CAUSTIC, int BPL>
 // 4 waves per SIMD (<= 128 VGPRs, 19 spilled, all outside the fast path's FMA chains): with
 // 37.6 KB of LDS per workgroup 4 workgroups fit a CU, and the fourth wave hides more FP64
 // latency than the spills cost (config 2: 1.00 ms against 1.09 ms at 3 waves / 147 VGPRs;
@@ -1837,9 +1837,9 @@ template <bool PAIRED, int CAUSTIC, int BPL, bool LISTS>
 #ifndef EFD_WAVES_PER_EU
 #define EFD_WAVES_PER_EU 4
 #endif
-// 1: the tiles' record lists are built by a lists-only k_modesum instance in the preparation
-// phase (k_tile_lists role) and DMA'd in by the sum; tiles whose list needs more than one
-// KEYCAP pass (tcnt = -1) build it in the sum as before. 0: always in the sum.
+// 1: the tiles' record lists are built by k_tile_keys in the preparation phase and DMA'd in by
+// the sum; tiles whose list needs more than one KEYCAP pass or has more than TK_HITS segments
+// (tcnt = -1) build it in the sum as before. 0: always in the sum.
 #ifndef EFD_PREBUILT_LISTS
 #define EFD_PREBUILT_LISTS 1
 #endif
@@ -1854,8 +1854,8 @@ __device__ __forceinline__ void modesum_tile(
     int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,
     const int32_t* __restrict__ gn, const double* __restrict__ t,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
-    const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,
-    int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,
+    const double2* __restrict__ sctab_g, const uint32_t* __restrict__ tkeys,
+    const int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,
     const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,
     const int32_t* __restrict__ stb1, Header* __restrict__ hdr, int accumulate_out,
     double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
@@ -1901,11 +1901,11 @@ __device__ __forceinline__ void modesum_tile(
     const int lane = tid & 63;
     const int ni = nt - 1;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
-    // Prebuilt record list (LISTS = false with tkeys set): k_tile_lists, launched in the
-    // preparation phase, ran this tile's list build below and stored its keys when they fit in
-    // one KEYCAP pass (tcnt >= 0); they come in by LDS-DMA with the sin/cos table and the build is
-    // skipped. Same keys in the same order, so the sum is bitwise the in-kernel build's.
-    const int pre = (!LISTS && tcnt != nullptr) ? tcnt[tile] : -1;
+    // Prebuilt record list: k_tile_keys, launched in the preparation phase, stored this tile's
+    // keys when they fit in one KEYCAP pass (tcnt >= 0); they come in by LDS-DMA with the sin/cos
+    // table and the build below is skipped. Same keys in the same order as the build below, so
+    // the sum is bitwise the in-kernel build's.
+    const int pre = tcnt != nullptr ? tcnt[tile] : -1;
     if (pre > 0) {
         static_assert(KEYCAP % (4 * TILE) == 0, "key copy: whole rounds of 16-B pieces");
 #pragma unroll
@@ -1916,7 +1916,7 @@ __device__ __forceinline__ void modesum_tile(
                        reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
         }
     }
-    if (!LISTS) {
+    {
         // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces)
         static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
 #pragma unroll
@@ -2103,14 +2103,6 @@ __device__ __forceinline__ void modesum_tile(
             nkeys += take;
             wdone += take;
             __syncthreads();
-        }
-        if (LISTS) {
-            // lists-only instance (k_tile_lists): store the first pass when it is the whole list
-            const bool whole = (wdone == wtotal) && (win >= nseg);
-            if (tid == 0) tcnt[tile] = whole ? nkeys : -1;
-            if (whole)
-                for (int i = tid; i < nkeys; i += TILE) tkeys[(size_t)tile * KEYCAP + i] = keys[i];
-            return;
         }
         if (nkeys == 0) break;
 #ifdef EFD_EXP_NOEVAL
@@ -2345,8 +2337,8 @@ __device__ __forceinline__ void modesum_tile(
         int64_t nlanes, int64_t ntiles, int nt, int K, const int32_t* __restrict__ gm,        \
         const int32_t* __restrict__ gn, const double* __restrict__ t,                         \
         const double* __restrict__ coefA, const double* __restrict__ coefT,                   \
-        const double2* __restrict__ sctab_g, uint32_t* __restrict__ tkeys,                    \
-        int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,                        \
+        const double2* __restrict__ sctab_g, const uint32_t* __restrict__ tkeys,              \
+        const int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,                  \
         const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,                \
         const int32_t* __restrict__ stb1, Header* __restrict__ hdr, int accumulate_out,       \
         double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0
@@ -2364,19 +2356,182 @@ __attribute__((amdgpu_num_vgpr(EFD_MODESUM_VGPRS)))
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 #endif
 void k_modesum(EFD_MODESUM_PARAMS) {
-    modesum_tile<PAIRED, CAUSTIC, BPL, false>(EFD_MODESUM_ARGS);
+    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS);
 }
 
-// K6: the tiles' record lists only (the same build, run in the preparation phase)
-template <bool PAIRED>
-__global__ __launch_bounds__(TILE) void k_tile_lists(EFD_MODESUM_PARAMS) {
-    modesum_tile<PAIRED, EFD_CAUSTIC_SPA, BPL, true>(EFD_MODESUM_ARGS);
+// K6: the tiles' record lists, built in the preparation phase (k_modesum DMAs them in). The same
+// keys in the same order as the sum's own build (segments in table order; each segment's records
+// reaching the tile, [p0, p1) from the segment-tile boundaries or by bisection; the keys of each
+// SEGWIN window of segment ids scattered by x -> P x mod n over that window), computed in one
+// pass over the tile's hits instead of window by window: the segment table is read in batches
+// of 8 windows per barrier, the hits' boundaries and counts in one round of loads, one block
+// scan places them, and each thread then writes keys found by bisection over the hit offsets.
+// The sum's build waits for every window's loads, scans and barriers in turn (~7.7 us per tile
+// alone at config 2, 37 us for the launch); this kernel shares the GPU with the previous
+// waveform's sum, so its resident time is what it costs. Tiles with more than TK_HITS hits or
+// KEYCAP keys get tcnt = -1 and build in the sum.
+constexpr int TK_HITS = TILE;
+constexpr int TK_ROWS = 8;   // windows of the segment table per barrier
+__global__ __launch_bounds__(TILE) void k_tile_keys(
+    const int4* __restrict__ ranges, const int2* __restrict__ seglh,
+    const int4* __restrict__ seginfo, const int32_t* __restrict__ nsegp,
+    const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,
+    const int32_t* __restrict__ stb1, int64_t ntiles, uint32_t* __restrict__ tkeys,
+    int32_t* __restrict__ tcnt) {
+    static_assert(SEGWIN == TILE, "one segment per thread and window row");
+    __shared__ int hits[TK_HITS], hp0[TK_HITS], hcnt[TK_HITS], hoff[TK_HITS], hws[TK_HITS],
+        hwt[TK_HITS];
+    __shared__ int4 hinfo[TK_HITS];
+    __shared__ int wcnt[TK_ROWS * NWAVE];
+    __shared__ int part[NWAVE];
+    const int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
+    const int nseg = *nsegp;
+#ifdef EFD_EXP_COUNT   // segment table size [27], hits per tile summed [28]
+    if (tile == 0 && tid == 0) atomicAdd(&g_exp_count[27], (unsigned long long)nseg);
+#endif
+    // (1) the segments overlapping the tile, in table order
+    int nhit = 0;
+    for (int base = 0; base < nseg; base += TK_ROWS * TILE) {
+        unsigned long long bal[TK_ROWS];
+#pragma unroll
+        for (int r = 0; r < TK_ROWS; ++r) {
+            const int sgi = base + r * TILE + tid;
+            bool hit = false;
+            if (sgi < nseg) {
+                const int2 lh = seglh[sgi];
+                hit = lh.y > tlo && lh.x < thi;
+            }
+            bal[r] = __ballot(hit);
+            if (lane == 0) wcnt[r * NWAVE + wave] = __popcll(bal[r]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < TK_ROWS; ++r) {
+            int before = nhit;
+            for (int w = 0; w < wave; ++w) before += wcnt[r * NWAVE + w];
+            if ((bal[r] >> lane) & 1ull) {
+                const int pos = before + __popcll(bal[r] & ((1ull << lane) - 1ull));
+                if (pos < TK_HITS) hits[pos] = base + r * TILE + tid;
+            }
+#pragma unroll
+            for (int w = 0; w < NWAVE; ++w) nhit += wcnt[r * NWAVE + w];
+        }
+        __syncthreads();
+    }
+#ifdef EFD_EXP_COUNT
+    if (tid == 0) atomicAdd(&g_exp_count[28], (unsigned long long)nhit);
+#endif
+    if (nhit > TK_HITS) {
+        if (tid == 0) tcnt[tile] = -1;
+        return;
+    }
+    // (2) each hit's records reaching into the tile: [p0, p1)
+    int c = 0;
+    if (tid < nhit) {
+        const int sg = hits[tid];
+        const int32_t sbase = segbase[sg];
+        const int4 info = seginfo[sg];
+        int p0 = 0;
+        if (sbase != SEG_NO_STB) {
+            p0 = stb0[sbase + tile];
+            c = max(stb1[sbase + tile] - p0, 0);
+        } else {
+            const int base = info.x, n = info.y, dir = info.z, sb = info.w;
+            int lo = 0, hi = n;            // first p (lane order) with khi > tlo
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const int4 rg = ranges[base + (dir > 0 ? mid : n - 1 - mid)];
+                if ((sb ? rg.w : rg.y) > tlo) hi = mid; else lo = mid + 1;
+            }
+            p0 = lo;
+            hi = n;                        // first p with klo >= thi
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const int4 rg = ranges[base + (dir > 0 ? mid : n - 1 - mid)];
+                if ((sb ? rg.z : rg.x) >= thi) hi = mid; else lo = mid + 1;
+            }
+            c = lo - p0;
+        }
+        hp0[tid] = p0;
+        hcnt[tid] = c;
+        hinfo[tid] = info;
+    }
+    // (3) exclusive scan of the counts
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) part[wave] = incl;
+    __syncthreads();
+    int total = 0, woff = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) {
+        woff += w < wave ? part[w] : 0;
+        total += part[w];
+    }
+    if (total > KEYCAP) {
+        if (tid == 0) tcnt[tile] = -1;
+        return;
+    }
+    if (tid < nhit) hoff[tid] = woff + incl - c;
+    __syncthreads();
+    // (4) each hit's SEGWIN window: where its keys start and how many it holds (the scatter's
+    // range). Hits are in table order, so a window's hits are consecutive: the window's start
+    // is a max-scan of the offsets at window starts, its end a min-scan from the right of the
+    // offsets past window ends
+    {
+        const int w = tid < nhit ? hits[tid] / SEGWIN : INT32_MAX;
+        const bool first = tid < nhit && (tid == 0 || hits[tid - 1] / SEGWIN != w);
+        const bool last = tid < nhit && (tid == nhit - 1 || hits[tid + 1] / SEGWIN != w);
+        int st = first ? woff + incl - c : INT32_MIN;       // this hit's offset = hoff[tid]
+        int en = last ? woff + incl : INT32_MAX;            // hoff[tid] + hcnt[tid]
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int vs = __shfl_up(st, o, 64), ve = __shfl_down(en, o, 64);
+            if (lane >= o) st = max(st, vs);
+            if (lane + o < 64) en = min(en, ve);
+        }
+        if (lane == 63) hws[wave] = st;   // wave carries (hws, hwt reused as scratch)
+        if (lane == 0) hwt[wave] = en;
+        __syncthreads();
+        for (int v = 0; v < wave; ++v) st = max(st, hws[v]);
+        for (int v = NWAVE - 1; v > wave; --v) en = min(en, hwt[v]);
+        __syncthreads();
+        if (tid < nhit) {
+            hws[tid] = st;
+            hwt[tid] = en - st;
+        }
+    }
+    __syncthreads();
+    // (5) the keys: position g of the list lies in hit i (bisection over the offsets)
+    uint32_t* out = tkeys + (size_t)tile * KEYCAP;
+    for (int g = tid; g < total; g += TILE) {
+        int lo = 0, hi = nhit - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (hoff[mid] <= g) lo = mid; else hi = mid - 1;
+        }
+        const int4 info = hinfo[lo];
+        const int p = hp0[lo] + (g - hoff[lo]);
+        const int j = info.z > 0 ? p : info.y - 1 - p;
+        const int ws = hws[lo], take = hwt[lo];
+        const int P = (take % 97) ? 97 : 101;
+        out[ws + (int)(((unsigned)(g - ws) * (unsigned)P) % (unsigned)take)] =
+            ((uint32_t)(info.x + j) << 1) | (uint32_t)info.w;
+    }
+    if (tid == 0) tcnt[tile] = total;
 }
 #undef EFD_MODESUM_PARAMS
 #undef EFD_MODESUM_ARGS
 
 // K7: dispatch order for the sum, most expensive tiles first (longest-processing-time list
-// scheduling). Cost = the tile's record count from k_tile_lists (tcnt; -1, a list over one
+// scheduling). Cost = the tile's record count from k_tile_keys (tcnt; -1, a list over one
 // KEYCAP pass, is the most expensive class), bucketed at quarter octaves: a counting sort in
 // LDS by one workgroup. The order within a bucket follows LDS atomics and may vary from run to
 // run; it changes only which block runs a tile, never a tile's arithmetic, so the spectrum is
@@ -2875,26 +3030,17 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     }
     HIP_TRY(hipGetLastError());
 #if EFD_PREBUILT_LISTS
-    // K6: the tiles' record lists (k_modesum's own list build, lists-only instance): moves the
-    // latency-bound build out of the mode sum into the preparation phase, which overlaps the
-    // previous waveform's sum in a two-stream pipeline
+    // K6: the tiles' record lists (k_tile_keys): moves the latency-bound build out of the mode
+    // sum into the preparation phase, which overlaps the previous waveform's sum in a two-stream
+    // pipeline
     {
-        const int64_t gq = 8 * XCD_GROUP;
-        const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
+        const dim3 block(TILE);
 #ifdef EFD_EXP_SKIP_TL   // diagnostic: after the warm-up, reuse the lists (same inputs only)
         static int exp_calls = 0;
         if (++exp_calls > 8) {} else
 #endif
-        if (paired)
-            hipLaunchKernelGGL((k_tile_lists<true>), grid, block, 0, st,
-                               items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, segbase,
-                               stb0, stb1, hdr, 0, nullptr, nullptr, nullptr, (int64_t)0);
-        else
-            hipLaunchKernelGGL((k_tile_lists<false>), grid, block, 0, st,
-                               items, ranges, seglh, seginfo, nseg, a->freq, nf, nl, L.ntiles, nt,
-                               K, gm, gn, a->t, coefA, coefT, sctab_g, tkeys, tcnt, nullptr, segbase,
-                               stb0, stb1, hdr, 0, nullptr, nullptr, nullptr, (int64_t)0);
+        hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)L.ntiles), block, 0, st, ranges, seglh,
+                           seginfo, nseg, segbase, stb0, stb1, L.ntiles, tkeys, tcnt);
         HIP_TRY(hipGetLastError());
 #if EFD_COST_ORDER
         if (L.ntiles > resident_tile_slots()) {

@@ -126,7 +126,8 @@ def child(name, ref_path):
              "lanes_y_mid", "lanes_y_small", "unused", "y_ge153", "y_ge75", "y_ge48",
              "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18", "cold_wave_evals", "cold_wave_lanes",
              "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1",
-             "chunk_max_wave_evals", "chunk_wave_evals", "chunks"))}
+             "chunk_max_wave_evals", "chunk_wave_evals", "chunks", "segments",
+             "tile_hits"))}
         c = out["counters_per_launch"]
         if c["chunk_wave_evals"] > 0:
             # wave-time lost at the chunk barriers if every record evaluation cost the same
