@@ -10,25 +10,32 @@
 // (:579-584), amplitude spline (:587-594), K_{1/3} factor (:599-613), phases (:615-616).
 // The oracle (oracle/fd_oracle.py) states the same maths in numpy; tests pin them together.
 //
-// Pipeline (all on one stream, no host sync, no allocation):
+// Pipeline (one stream per phase, no host sync, no allocation). Preparation
+// (efd_modesum_prepare, latency-bound kernels on few CUs, overlapping the previous sum):
+//   K0 k_group, k_group_amp  (m, n) groups of the harmonics; per knot, the group amplitudes
+//                            Bp = sum_l y0_l A_l, Bm = sum_l y1_l A_l
 //   K1-K3 k_prep          one launch, three independent roles by workgroup:
 //                         - 1 wave: not-a-knot splines of Phi_phi, Phi_r, f_phi, f_r and of the
 //                           knot derivatives f_phi'(t_i), f_r'(t_i) (for F'' as notebook :583)
-//                         - 1 lane per amplitude interpolant (Re/Im A_k, 2K lanes), sharing one
-//                           LDS factorisation of the knot matrix
-//                         - 1 lane per harmonic: F knots, monotonic runs, inverse spline per run
-//   K4 k_items            1 thread per (harmonic, knot interval): gathers every cubic the SPA
-//                         needs for that interval into one 256-B record + its bin (lane) ranges
-//   K5 k_segment_slots    1 thread per (harmonic, run, sub-branch): its segment of records,
-//      k_segment_compact  trimmed of clamped empty records; then compacted in slot order
-//   K6 k_modesum          OUTPUT-STATIONARY: one 4-wave workgroup per tile of 256*BPL bins;
+//                         - 1 lane per group amplitude interpolant (4G lanes), sharing one LDS
+//                           factorisation of the knot matrix
+//                         - 1 lane per group: F knots, monotonic runs, inverse spline per run
+//   K4 k_items            1 thread per (group, knot interval): gathers every cubic the SPA
+//                         needs for that interval into one 288-B record + its bin (lane) ranges
+//   K5 k_segment_slots    1 thread per (group, run, sub-branch): its segment of records,
+//      k_segment_compact  trimmed of clamped empty records; then compacted in slot order;
+//      k_seg_tiles        per (segment, tile it covers) the record sub-range reaching the tile
+//   K6 k_tile_keys        per tile, its ordered record list (prebuilt keys)
+//   K7 k_tile_order       tiles by cost, most expensive first (the sum's dispatch order)
+// Mode sum (efd_modesum_sum):
+//   K8 k_modesum          OUTPUT-STATIONARY: one 4-wave workgroup per tile of 256*BPL bins;
 //                         each lane owns BPL bins (and their mirrors -f when the grid is
 //                         symmetric: the +m branch and its -m partner share t(g), the
 //                         amplitude/phase splines and sin/cos, so one evaluation feeds two
-//                         bins); each tile builds its own record list in LDS from the segment
-//                         table (bisection, fixed order -> bitwise reproducible), streams the
-//                         records through a double-buffered LDS stage, and writes its bins once
-//                         -- no atomics, no global lists, no host synchronisation.
+//                         bins); the tile's record list comes by LDS-DMA from K6 (or is built
+//                         in LDS from the segment table, fixed order -> bitwise reproducible),
+//                         records stream through a double-buffered LDS stage, and the tile
+//                         writes its bins (or h+/hx) once -- no atomics, no host sync.
 // The SPA evaluation is FP64 VALU work (phases reach ~1e7 rad); MFMA is not applicable.
 
 #include <hip/hip_runtime.h>
@@ -315,13 +322,9 @@ __device__ __forceinline__ double dcubic(const double* c, double w) {
 }
 
 // ----------------------------------------------------------------------------------------
-// K0: (m, n) groups. One workgroup sorts the K harmonics by (m, n, h) in LDS (bitonic, 64-bit
-// keys) and writes the groups in (m, n) order with their members in ascending h:
-//   gm[g], gn[g]; members gmem[gstart[g] .. gstart[g+1]); G = hdr->groups.
-// The order is a function of (m, n) alone, so everything downstream is deterministic.
-// ----------------------------------------------------------------------------------------
-// K0: (m, n) groups. Groups ascend in (m, n), members in harmonic index h (the order every later
-// kernel and the oracle's grouping use). One 256-thread workgroup with a small LDS footprint: it
+// K0: (m, n) groups: gm[g], gn[g]; members gmem[gstart[g] .. gstart[g+1]); G = hdr->groups.
+// Groups ascend in (m, n), members in harmonic index h (the order every later kernel and the
+// oracle's grouping use; a function of (m, n) alone, so everything downstream is deterministic). One 256-thread workgroup with a small LDS footprint: it
 // runs while the previous waveform's mode sum holds the GPU, so it must fit where one k_modesum
 // workgroup has left a CU (round 1's 1024-thread, 68 KB-LDS bitonic sort needed two to leave the
 // same CU at once and waited up to the end of that sum's dispatch, delaying the whole
