@@ -214,6 +214,25 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
 #define EFD_SPLINE_PF 8   // 16: same, 32: slower (k_prep 110 -> 177 us)
 #endif
 
+// 1/x for the spline solves: the hardware reciprocal estimate and two Newton steps (5 dependent
+// operations, within an ulp) instead of the IEEE division sequence (~10, with the scale and
+// fixup steps) on the serial Thomas chains, whose latency sets the preparation's length; the
+// coefficients stay within 1e-11 of scipy's (tests/test_gpu_modesum.py), their rounding level
+#ifndef EFD_SPLINE_RCP
+#define EFD_SPLINE_RCP 1
+#endif
+__device__ __forceinline__ double spl_rcp(double x) {
+#if EFD_SPLINE_RCP
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+#else
+    return 1.0 / x;
+#endif
+}
+
 // ----------------------------------------------------------------------------------------
 // Not-a-knot cubic spline solve (scipy.interpolate.CubicSpline semantics)
 // ----------------------------------------------------------------------------------------
@@ -261,7 +280,7 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
         // row i: a = dx_i, b = 2(dx_{i-1} + dx_i), c = dx_{i-1}, r = 3(dx_i sl_{i-1} + dx_{i-1} sl_i)
         const double a = dxi, b = 2.0 * (dxm + dxi), c = dxm;
         const double r = 3.0 * (dxi * slm + dxm * sli);
-        const double inv = 1.0 / (b - a * cpm);   // one division on the serial chain
+        const double inv = spl_rcp(b - a * cpm);   // one reciprocal on the serial chain
         cpm = c * inv;
         dpm = (r - a * dpm) * inv;
         CP(i) = cpm;
@@ -269,7 +288,7 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
         if (i + 2 <= n - 1) {
             const double xn = X(i + 2), yn = Y(i + 2);
             dxm = dxi; slm = sli;
-            dxi = xn - xi; sli = (yn - yi) / dxi;
+            dxi = xn - xi; sli = (yn - yi) * spl_rcp(dxi);
             xi = xn; yi = yn;
         }
     }
@@ -303,11 +322,13 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
             if (i < 0) break;
             const double xl = X(i), yl = Y(i);
             const double s_i = dpb[k] - cpb[k] * s_next;
-            const double dx = xr - xl;
-            const double sl = (yr - yl) / dx;
-            const double tt = (s_i + s_next - 2.0 * sl) / dx;
-            OUT(i, 0, tt / dx);
-            OUT(i, 1, (sl - s_i) / dx - tt);
+            // one reciprocal for the interval's four quotients (an FP64 division is a ~10-op
+            // sequence; x * (1/dx) differs from x / dx by at most an ulp)
+            const double rdx = spl_rcp(xr - xl);
+            const double sl = (yr - yl) * rdx;
+            const double tt = (s_i + s_next - 2.0 * sl) * rdx;
+            OUT(i, 0, tt * rdx);
+            OUT(i, 1, (sl - s_i) * rdx - tt);
             OUT(i, 2, s_i);
             OUT(i, 3, yl);
             s_next = s_i;
@@ -607,8 +628,10 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
     double* cpl = lds + n;
     double* iml = lds + 2 * n;
     double* all = lds + 3 * n;
+    double* ridx = lds + 4 * n;   // 1 / (x_{i+1} - x_i): every lane's quotients by dx_i
     for (int i = threadIdx.x; i < n; i += blockDim.x) xs[i] = x[i];
     __syncthreads();
+    for (int i = threadIdx.x; i < n - 1; i += blockDim.x) ridx[i] = spl_rcp(xs[i + 1] - xs[i]);
     if (threadIdx.x == 0 && n >= 4) {
         double dxm = xs[1] - xs[0], dxi = xs[2] - xs[1];
         double d = xs[2] - xs[0];
@@ -617,7 +640,8 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
             dxm = xs[i] - xs[i - 1];
             dxi = xs[i + 1] - xs[i];
             const double mm = 2.0 * (dxm + dxi) - dxi * cpl[i - 1];
-            cpl[i] = dxm / mm; iml[i] = 1.0 / mm; all[i] = dxi;
+            const double rm = spl_rcp(mm);
+            cpl[i] = dxm * rm; iml[i] = rm; all[i] = dxi;
         }
         const double dl = xs[n - 1] - xs[n - 3];
         const double mm = (xs[n - 2] - xs[n - 3]) - dl * cpl[n - 2];
@@ -646,7 +670,7 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
     const double y0 = Y(0), y1 = Y(1);
     double yprev = Y(2);
     double dxm = xs[1] - xs[0], dxi = xs[2] - xs[1];
-    double slm = (y1 - y0) / dxm, sli = (yprev - y1) / dxi;
+    double slm = (y1 - y0) * ridx[0], sli = (yprev - y1) * ridx[1];
     double dp;
     {
         const double d = xs[2] - xs[0];
@@ -671,7 +695,7 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
             if (i + 2 <= n - 1) {
                 dxm = dxi; slm = sli;
                 dxi = xs[i + 2] - xs[i + 1];
-                sli = (yb[k] - yprev) / dxi;
+                sli = (yb[k] - yprev) * ridx[i + 1];
                 yprev = yb[k];
             }
         }
@@ -698,11 +722,11 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
             if (i < 0) break;
             const double yl = ylb[k];
             const double s_i = dpb[k] - cpl[i] * s_next;
-            const double dx = xs[i + 1] - xs[i];
-            const double sl = (yr - yl) / dx;
-            const double tt = (s_i + s_next - 2.0 * sl) / dx;
-            OUT(i, 0, tt / dx);
-            OUT(i, 1, (sl - s_i) / dx - tt);
+            const double rdx = ridx[i];
+            const double sl = (yr - yl) * rdx;
+            const double tt = (s_i + s_next - 2.0 * sl) * rdx;
+            OUT(i, 0, tt * rdx);
+            OUT(i, 1, (sl - s_i) * rdx - tt);
             OUT(i, 2, s_i);
             OUT(i, 3, yl);
             s_next = s_i;
@@ -2890,7 +2914,7 @@ int efd_spline_build(const double* x, int n, const double* y, int ninterp, doubl
         return fail(EFD_ERR_ARG, "efd_spline_build: bad arguments");
     const int threads = 64;   // spline_shared assumes 64-thread blocks
     const int blocks = (ninterp + threads - 1) / threads;
-    hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), sizeof(double) * 4 * n,
+    hipLaunchKernelGGL(k_spline_shared, dim3(blocks), dim3(threads), sizeof(double) * 5 * n,
                        (hipStream_t)stream, x, n, y, ninterp, coef, (int64_t)4 * ninterp);
     HIP_TRY(hipGetLastError());
     return EFD_OK;
