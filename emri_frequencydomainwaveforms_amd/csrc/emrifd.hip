@@ -127,8 +127,10 @@ struct __attribute__((aligned(16))) Item {
     double fd[3];     // F'(t)
     double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
     int32_t jser;     // K_{1/3} series terms the fast path needs on this interval (1..FAST_J)
-    int32_t pad;      // b starts 16-B aligned, so its cubics come out of LDS by ds_read_b128
-                      // (8 ds_read2_b64 -> ds_read_b128 per record: k_modesum -3%)
+    int32_t fdneg;    // F' < 0 at the interval's midpoint: the sign the fast path assumes for
+                      // every lane (lanes of the other sign, at a turning point, take the general
+                      // path). Also keeps b 16-B aligned, so its cubics come out of LDS by
+                      // ds_read_b128 (8 ds_read2_b64 -> ds_read_b128 per record: k_modesum -3%)
     double b[2][2][4];  // b[0] = Bp (re, im cubics), b[1] = Bm: sub-branch s reads b[s] for its
                         // own bin and b[1-s] for the mirror
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
@@ -963,6 +965,7 @@ __device__ void build_item(
     }
     const int partner = (m != 0) ? 1 : 0;
     evals = 0;
+    it.fdneg = 0;
     if (run < 0) {  // flat interval (F_{j+1} == F_j): no support; place empty ranges at 0
         it.klo[0] = it.khi[0] = it.klo[1] = it.khi[1] = 0;
         ranges[(size_t)h * ni + j] = make_int4(0, 0, 0, 0);
@@ -1000,6 +1003,7 @@ __device__ void build_item(
         const double dt = it.dtj;
         auto qv = [](double a, double b, double c, double x) { return (a * x + b) * x + c; };
         const double fa = it.fd[2], fb = qv(it.fd[0], it.fd[1], it.fd[2], dt);
+        it.fdneg = qv(it.fd[0], it.fd[1], it.fd[2], 0.5 * dt) < 0.0 ? 1 : 0;
         double fdmin = fmin(fabs(fa), fabs(fb));
         if ((fa > 0.0) != (fb > 0.0) || fa == 0.0 || fb == 0.0) fdmin = 0.0;
         if (it.fd[0] != 0.0) {
@@ -1286,6 +1290,10 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 // cos to r^4: < 1e-16) and the angle-sum formula: ~13 FP64 operations
 // instead of ~26 plus the quadrant logic of sincos_big. `shift` (an integer number of table
 // steps) is added to the angle exactly, through the table index. Valid for |x| < 2^31 pi/256.
+// The reduction is one FMA against the leading 53 bits of the step: the dropped q * STEP_2 is
+// < 3.9e-17 |x|, below half an ulp of x itself (the rounding every phase already carries), and
+// one FMA less on the longest dependency chain of an evaluation (k_modesum +1.2-1.6%, the
+// spectrum moves by 8e-12 of max|S| at config 2; -DEFD_CW_TWO_PART restores the second term).
 constexpr int SCTAB = 512;
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
                                            double& s, double& c, double extra = 0.0,
@@ -1299,7 +1307,11 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     const double qs = fma(x, INV_STEP, SHIFTER);
     const double q = qs - SHIFTER;
     double r = fma(-q, STEP_1, x);
+#ifdef EFD_CW_TWO_PART
     r = fma(-q, STEP_2, r);
+#else
+    (void)STEP_2;
+#endif
     // a small angle (|extra_scale * extra| < 1e-3) added after the reduction
     if (use_extra) r = fma(extra_scale, extra, r);
     const int qi = __double2loint(qs);
@@ -1677,11 +1689,38 @@ __device__ __forceinline__ uint64_t lane_range_mask(int32_t lo, int32_t hi) {
     return lanes_below(hi) & ~lanes_below(lo);
 }
 // spa_fast_rt with the active lanes given as a mask and the general-path lanes returned as one;
-// the same arithmetic (bitwise the same W and w)
+// the same arithmetic (bitwise the same W and w). EFD_REC_SIGN: the sign of F' is the record's
+// (Item::fdneg, wave-uniform), so the table shift and the angle's sign are scalar values: one
+// v_cmp_class (F' of the record's sign, nonzero) replaces the |F'| > 0 compare, and the per-lane
+// sign compare, shift select and copysign go (lanes whose F' has the other sign, at turning
+// points, take the general path). The class test is inline asm: the builtin's boolean is turned
+// into a VGPR and compared back (2 VALU) before a ballot.
+#ifndef EFD_REC_SIGN
+#define EFD_REC_SIGN 1
+#endif
+struct RecSign {
+    int32_t fdcls;   // v_cmp_class mask: F' normal or subnormal of the record's sign
+    int32_t shift;   // sign(F') 3 pi / 4 in table steps
+    double kth;      // theta = kth * min(|thn|, 1): KTH0 with the sign of F'
+};
+__device__ __forceinline__ RecSign rec_sign(bool fdneg) {
+    RecSign r;
+    r.fdcls = fdneg ? 0x018 : 0x180;
+    r.shift = fdneg ? -192 : 192;
+    r.kth = fdneg ? -KTH0 : KTH0;
+    return r;
+}
+// lanes where v_cmp_class_f64(x, cls) holds, as a wave mask
+__device__ __forceinline__ uint64_t class_mask(double x, int32_t cls) {
+    uint64_t m;
+    asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(m) : "v"(x), "s"(cls));
+    return m;
+}
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            int J, uint64_t actm, const double2* __restrict__ sct,
-                                           double& wr, double& wi, double& w, uint64_t& needm) {
+                                           const RecSign& rs, double& wr, double& wi, double& w,
+                                           uint64_t& needm) {
     static_assert(EFD_POLAR, "mask form of the polar fast path");
     const double u = sfk - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
@@ -1691,11 +1730,15 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
     const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
+#if EFD_REC_SIGN
+    goodm &= class_mask(fd, rs.fdcls);
+#else
     goodm &= __builtin_amdgcn_ballot_w64(afd > 0.0);
+    const int shift = fd > 0.0 ? 192 : -192;
+#endif
     // F' = 0 gives amp = NaN here; every quantity it reaches is selected away below
     const double amp = rsqrt_pos(afd);
     const double psi0 = fma(stfk, tt, -ph);
-    const int shift = fd > 0.0 ? 192 : -192;
     double sn, cs;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
         const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
@@ -1711,15 +1754,24 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         // Not masked: where ok, 0 < thn < 1/153; elsewhere min(|thn|, 1) keeps the angle finite
         // (a NaN thn becomes 1; far outside the series' range thn is large of either sign), so
         // sin/cos stay finite and the zero amplitude below zeroes W. |.| is a source modifier.
+#if EFD_REC_SIGN
+        const double am = ok ? amp * rho : 0.0;
+        sincos_tab(psi0, rs.shift, sct, sn, cs, fmin(fabs(thn), 1.0), true, rs.kth);
+#else
         const double ths = copysign(fmin(fabs(thn), 1.0), fd);
         const double am = ok ? amp * rho : 0.0;
         sincos_tab(psi0, shift, sct, sn, cs, ths, true, KTH0);   // theta = KTH0 * thn
+#endif
         wr = am * cs;
         wi = am * sn;
     } else {
         const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
         const double am = ok ? amp : 0.0;
+#if EFD_REC_SIGN
+        sincos_tab(psi0, rs.shift, sct, sn, cs);
+#else
         sincos_tab(psi0, shift, sct, sn, cs);
+#endif
         wr = am * cs;
         wi = am * sn;
     }
@@ -2164,7 +2216,8 @@ __device__ __forceinline__ void modesum_tile(
                 const Item* il = stg + lane;
                 const uint32_t lo = (uint32_t)min(max(il->klo[sl] - tlo, 0), TILE_LANES);
                 const uint32_t hi = (uint32_t)min(max(il->khi[sl] - tlo, 0), TILE_LANES);
-                hdr = lo | (hi << 10) | ((uint32_t)sl << 20) | ((uint32_t)il->jser << 21);
+                hdr = lo | (hi << 10) | ((uint32_t)sl << 20) | ((uint32_t)il->jser << 21) |
+                      ((uint32_t)il->fdneg << 24);
             }
 #ifdef EFD_EXP_COUNT
             int nev = 0;
@@ -2202,7 +2255,7 @@ __device__ __forceinline__ void modesum_tile(
                     // wave-uniform values
 #ifdef EFD_EXP_JDIST   // records by series length [0..3], sub-branch flips [4], records [5]
                     if (lane == 0) {
-                        atomicAdd(&g_exp_count[min((int)(ha >> 21), 4) - 1], 1ull);
+                        atomicAdd(&g_exp_count[min((int)((ha >> 21) & 7u), 4) - 1], 1ull);
                         atomicAdd(&g_exp_count[5], 1ull);
                         if (s != s_cur) atomicAdd(&g_exp_count[4], 1ull);
                     }
@@ -2220,7 +2273,7 @@ __device__ __forceinline__ void modesum_tile(
 #ifdef EFD_EXP_JFIX   // experiment: every record takes the FAST_J-term series (no J dispatch)
                     const int J = FAST_J;
 #else
-                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)(ha >> 21) : FAST_J;
+                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)((ha >> 21) & 7u) : FAST_J;
 #endif
                     // the stage holds b[s] at b[0] (EFD_GLDS swaps the halves for s = 1)
                     const double* xo = &it->b[0][0][0];
@@ -2228,12 +2281,13 @@ __device__ __forceinline__ void modesum_tile(
                     double wr[BPL], wi[BPL], w[BPL];
 #if EFD_SALU_MASKS
                     uint64_t needm[BPL], needany = 0;
+                    const RecSign rs = rec_sign((ha >> 24) & 1u);
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t base = w_lo + 64 * i;
                         spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], J,
-                                            lane_range_mask(klo - base, khi - base), sctab, wr[i],
-                                            wi[i], w[i], needm[i]);
+                                            lane_range_mask(klo - base, khi - base), sctab, rs,
+                                            wr[i], wi[i], w[i], needm[i]);
                         need[i] = __builtin_amdgcn_inverse_ballot_w64(needm[i]);
                         needany |= needm[i];
                     }
