@@ -9,18 +9,22 @@ p0 solved so the inspiral lasts 0.99 * Tobs (README's p0 = 12 is overwritten lik
 emri_pe.py:623-635), Tobs = 2 yr, dt = 10 s (N_f = 6,311,631 two-sided bins), eps = 1e-5
 (~3000 harmonics), K_{1/3} uniform SPA (the reference notebook's form). Inputs (sparse
 trajectory, amplitudes, Ylm; host stand-ins, NOT FEW physics) are resident in HBM before timing.
-One step = one full FD waveform on the device: spline build -> inverse splines -> interval
-records -> tile lists -> mode sum -> h+/hx over f >= 0 (the Likelihood path, emri_pe.py:241).
-With --pipeline overlap (default) waveform i+1's preparation (grouping, splines, records:
-latency-bound kernels on few CUs; efd_modesum_prepare) runs on a second stream beside waveform
-i's mode sum (efd_modesum_sum), and the sum writes h+/hx itself (fused polarisations).
+One step = a batch of B (--batch, default 4) full FD waveforms on the device, each with its own
+workspace and outputs: spline build -> inverse splines -> interval records -> tile lists -> mode
+sum -> h+/hx over f >= 0 (the Likelihood path, emri_pe.py:241, for a batch of walkers). With
+--pipeline overlap (default) batch i+1's preparation (grouping, splines, records: latency-bound
+kernels on few CUs; efd_modesum_prepare per waveform) runs on a second stream beside batch i's
+mode sums, which run as one launch (efd_modesum_sum_batch: the B waveforms' tiles in one
+longest-first dispatch) and write h+/hx themselves (fused polarisations). value counts
+waveforms (B per step); --batch 1 runs one efd_modesum_sum per waveform.
 
 Multi-GPU: one process per GPU; each rank generates its own waveforms (the walker batch of
 emri_pe.py shards with no data-path exchange: weak scaling); value = all ranks' waveforms / the
 max over ranks of the timed region.
 
-roofline: the mode-sum kernel (k_modesum) timed with HIP events recorded on its own stream
-around each launch of that kernel in the timed region; achieved = B_alg / t with B_alg = 32 C + 32 n_interp N_t + 16 N_f
+roofline: the mode-sum kernel (k_modesum_batch, or k_modesum at --batch 1) timed with HIP events
+recorded on its own stream around each launch in the timed region; t = launch time / B per
+waveform; achieved = B_alg / t with B_alg = 32 C + 32 n_interp N_t + 16 N_f
 (32 B per SPA contribution of the reference's scatter formulation),
 peak 8.0 TB/s (MI355X_MICROARCH.md). traffic: HBM bytes per launch from the committed rocprofv3
 PMC pass (profiles/), or null.
@@ -119,8 +123,11 @@ def main():
                     help="overlap pipeline: consecutive mode sums alternate over this many streams "
                          "(> 1 lets sum i+1 start during sum i's tail)")
     ap.add_argument("--slots", type=int, default=2,
-                    help="overlap pipeline depth: workspaces in flight (preparation runs up to "
-                         "slots - 1 waveforms ahead of the sum)")
+                    help="overlap pipeline depth: batches in flight (preparation runs up to "
+                         "slots - 1 batches ahead of the sum)")
+    ap.add_argument("--batch", type=int, default=4,
+                    help="overlap pipeline: waveforms per step, their mode sums in one launch "
+                         "(efd_modesum_sum_batch; 1 = one efd_modesum_sum per waveform)")
     ap.add_argument("--diag-sum-only", action="store_true",
                     help="diagnostic, not the metric: each slot is prepared once in the warm-up, "
                          "then every step runs only the mode sum (the sum-stream ceiling)")
@@ -138,7 +145,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from emri_frequencydomainwaveforms_amd import _lib
-    from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine
+    from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine, sum_batch
 
     w = build_workload(T=args.T, eps=args.eps)
     inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
@@ -147,47 +154,62 @@ def main():
     nf = int(freq.numel())
     k0 = int(np.searchsorted(w["freq"], 0.0))
     overlap = args.pipeline == "overlap"
-    # Two slots (workspace + h+/hx outputs). "overlap": waveform i+1's preparation (grouping,
-    # splines, records: latency-bound kernels on few CUs) runs on the prep stream while waveform
-    # i's mode sum runs on the sum stream; the sum writes h+/hx directly (fused polarisations).
+    B = args.batch if overlap else 1
+    if not 1 <= B <= _lib.EFD_BATCH_MAX:
+        raise SystemExit(f"--batch must be in [1, {_lib.EFD_BATCH_MAX}]")
+    # Slots of B waveforms (a workspace + h+/hx outputs each). "overlap": batch i+1's
+    # preparation (grouping, splines, records: latency-bound kernels on few CUs) runs on the prep
+    # stream while batch i's mode sums run on the sum stream, all B in one launch
+    # (efd_modesum_sum_batch: one ramp, one tail, no gaps between the B sums); the sums write
+    # h+/hx directly (fused polarisations). Every waveform is prepared and summed in full.
     # "serial": one stream, efd_modesum then efd_polarizations (the unfused path).
     slots = []
     for _ in range(max(2, args.slots) if overlap else 1):
-        hp = torch.empty(nf - k0, dtype=torch.complex128, device=dev)
-        slots.append(dict(eng=ModeSumEngine(caustic=args.caustic), fhp=torch.view_as_real(hp),
-                          fhc=torch.view_as_real(torch.empty_like(hp)),
-                          fS=None if overlap else torch.view_as_real(
-                              torch.empty(nf, dtype=torch.complex128, device=dev)),
-                          prep_done=torch.cuda.Event(), sum_done=None))
+        wf = []
+        for _ in range(B):
+            hp = torch.empty(nf - k0, dtype=torch.complex128, device=dev)
+            wf.append(dict(eng=ModeSumEngine(caustic=args.caustic), fhp=torch.view_as_real(hp),
+                           fhc=torch.view_as_real(torch.empty_like(hp)),
+                           fS=None if overlap else torch.view_as_real(
+                               torch.empty(nf, dtype=torch.complex128, device=dev))))
+        slots.append(dict(wf=wf, prep_done=torch.cuda.Event(), sum_done=None))
     s_prep = torch.cuda.Stream(dev)
     s_sums = [torch.cuda.Stream(dev) for _ in range(max(1, args.sum_streams))] if overlap \
         else [s_prep]
     s_sum = s_sums[0]
-    lib = slots[0]["eng"].lib
+    lib = slots[0]["wf"][0]["eng"].lib
 
     def step(i, ev=None):
         sl = slots[i % len(slots)]
-        eng = sl["eng"]
         pe = (ev[0].cuda_event, ev[1].cuda_event) if ev is not None else (None, None)
         if overlap:
             ss = s_sums[i % len(s_sums)]
             if not (args.diag_sum_only and i >= len(slots)):
-                if sl["sum_done"] is not None:    # the slot's previous sum has read its workspace
+                if sl["sum_done"] is not None:    # the slot's previous sums have read it
                     s_prep.wait_event(sl["sum_done"])
-                eng.launch(inp, freq, None, True, w["prefactor"], stream=s_prep.cuda_stream,
-                           phase="prepare")
+                for x in sl["wf"]:
+                    x["eng"].launch(inp, freq, None, True, w["prefactor"],
+                                    stream=s_prep.cuda_stream, phase="prepare")
                 sl["prep_done"].record(s_prep)
                 ss.wait_event(sl["prep_done"])
-            eng.launch(inp, freq, None, True, w["prefactor"], stream=ss.cuda_stream,
-                       prof_events=pe, hp=sl["fhp"], hc=sl["fhc"], k0=k0, phase="sum")
+            if B == 1:
+                x = sl["wf"][0]
+                x["eng"].launch(inp, freq, None, True, w["prefactor"], stream=ss.cuda_stream,
+                                prof_events=pe, hp=x["fhp"], hc=x["fhc"], k0=k0, phase="sum")
+            else:
+                sum_batch([(x["eng"], dict(inp=inp, freq=freq, out=None, grid_symmetric=True,
+                                           scale=w["prefactor"], hp=x["fhp"], hc=x["fhc"],
+                                           k0=k0)) for x in sl["wf"]],
+                          stream=ss.cuda_stream, prof_events=pe)
             done = torch.cuda.Event()
             done.record(ss)
             sl["sum_done"] = done
         else:
             st = s_prep.cuda_stream
-            eng.launch(inp, freq, sl["fS"], True, w["prefactor"], stream=st, prof_events=pe)
-            _lib.check(lib.efd_polarizations(sl["fS"].data_ptr(), nf, k0, sl["fhp"].data_ptr(),
-                                             sl["fhc"].data_ptr(), st), "efd_polarizations", lib)
+            x = sl["wf"][0]
+            x["eng"].launch(inp, freq, x["fS"], True, w["prefactor"], stream=st, prof_events=pe)
+            _lib.check(lib.efd_polarizations(x["fS"].data_ptr(), nf, k0, x["fhp"].data_ptr(),
+                                             x["fhc"].data_ptr(), st), "efd_polarizations", lib)
 
     evs = []
     for i in range(args.steps):
@@ -209,8 +231,9 @@ def main():
     if world > 1:
         dist.barrier()
     for sl in slots:
-        if not sl["eng"].status(s_sum.cuda_stream):
-            raise RuntimeError(f"efd_modesum reported a device error: {_lib.last_error(lib)}")
+        for x in sl["wf"]:
+            if not x["eng"].status(s_sum.cuda_stream):
+                raise RuntimeError(f"efd_modesum reported a device error: {_lib.last_error(lib)}")
     # per-launch k_modesum duration, live over the timed region (HIP events on the sum stream;
     # with the overlap pipeline the next waveform's preparation kernels share the GPU with it)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
@@ -218,7 +241,7 @@ def main():
     # its preparation and for the launch): what the pipeline loses beside the kernel itself
     gaps = [evs[i][1].elapsed_time(evs[i + 1][0]) for i in range(len(evs) - 1)]
     gap_ms = float(np.mean(gaps)) if gaps else 0.0
-    C, n_eval, n_groups = slots[0]["eng"].stats(s_sum.cuda_stream)
+    C, n_eval, n_groups = slots[0]["wf"][0]["eng"].stats(s_sum.cuda_stream)
 
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -230,7 +253,8 @@ def main():
         nt = int(len(w["t"]))
         n_interp = 2 * K + 4
         b_alg = 32.0 * C + 32.0 * n_interp * nt + 16.0 * nf
-        achieved = b_alg / (kern_ms * 1e-3) / 1e9
+        wf_ms = kern_ms / B   # one launch sums B waveforms
+        achieved = b_alg / (wf_ms * 1e-3) / 1e9
         traffic = None
         fp64 = None
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -241,7 +265,7 @@ def main():
                     traffic = pj.get("hbm_bytes_per_launch")
                     f = pj.get("fp64")
                     if f:
-                        tf = f["flops_per_launch"] / (kern_ms * 1e-3) / 1e12
+                        tf = f["flops_per_launch"] / (wf_ms * 1e-3) / 1e12
                         fp64 = {"achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                                 "frac": tf / FP64_VALU_PEAK_TFLOPS,
                                 "valu_busy": f["valu_busy"],
@@ -255,7 +279,7 @@ def main():
                 cpu = cpu_baseline(w, seconds=args.cpu_seconds)
             except Exception as exc:  # the baseline must not kill the GPU measurement
                 cpu = {"value": None, "error": repr(exc)}
-        value = world * args.steps / elapsed
+        value = world * args.steps * B / elapsed
         line = {
             "metric": METRIC,
             "value": value,
@@ -264,6 +288,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "waveforms_per_step": B,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -276,13 +301,14 @@ def main():
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
                        "pipeline": args.pipeline + (" (diagnostic: sum only)"
                                                     if args.diag_sum_only else ""),
-                       "slots": len(slots), "sum_streams": len(s_sums)},
+                       "slots": len(slots), "sum_streams": len(s_sums), "batch": B},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_modesum", "kernel_ms": kern_ms,
+                         "kernel": "k_modesum_batch" if B > 1 else "k_modesum",
+                         "kernel_ms": kern_ms, "kernel_ms_per_waveform": wf_ms,
                          "kernel_timing": "HIP events around each k_modesum launch in the timed "
                                           "region (sum stream), mean",
-                         "contributions_per_s": C / (kern_ms * 1e-3),
+                         "contributions_per_s": C / (wf_ms * 1e-3),
                          "sum_gap_ms": gap_ms,
                          "sum_gap_ms_min_max": [min(gaps, default=0.0), max(gaps, default=0.0)],
                          "fp64_valu": fp64},

@@ -18,6 +18,7 @@ EFD_CAUSTIC_SPA = 0
 EFD_CAUSTIC_UNIFORM = 1
 EFD_LOGLIKE_SCRATCH = 1024
 EFD_INNER_SCRATCH = 2048
+EFD_BATCH_MAX = 16
 
 # every symbol include/emrifd.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = (
@@ -28,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum",
     "efd_modesum_prepare",
     "efd_modesum_sum",
+    "efd_modesum_sum_batch",
     "efd_modesum_status",
     "efd_modesum_contributions",
     "efd_modesum_stats",
@@ -139,6 +141,10 @@ def load(path=None):
         if hasattr(lib, name):   # absent only in older experiment builds
             getattr(lib, name).restype = ctypes.c_int
             getattr(lib, name).argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
+    if hasattr(lib, "efd_modesum_sum_batch"):
+        lib.efd_modesum_sum_batch.restype = ctypes.c_int
+        lib.efd_modesum_sum_batch.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
+                                              ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
     lib.efd_modesum_status.argtypes = [vp, vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int

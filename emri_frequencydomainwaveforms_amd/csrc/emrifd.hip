@@ -1957,7 +1957,8 @@ __device__ __forceinline__ void modesum_tile(
     const int32_t* __restrict__ tcnt, const int32_t* __restrict__ tperm,
     const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,
     const int32_t* __restrict__ stb1, Header* __restrict__ hdr, int accumulate_out,
-    double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0) {
+    double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0,
+    int64_t b) {   // b: this workgroup's place in the waveform's dispatch order
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -1976,7 +1977,6 @@ __device__ __forceinline__ void modesum_tile(
     // With a cost order (tperm, k_tile_order) block b takes the b-th most expensive tile instead:
     // longest-first dispatch, so the launch does not end on expensive tiles started late;
     // consecutive blocks (similar cost) land on different XCDs.
-    const int64_t b = blockIdx.x;
     int64_t tile;
     if (tperm != nullptr) {
         if (b >= ntiles) return;   // grid padding
@@ -1988,9 +1988,11 @@ __device__ __forceinline__ void modesum_tile(
             return;
         }
     } else {
+        // (the padded per-waveform grid, not gridDim: a batched launch holds several)
+        const int64_t gq = 8 * XCD_GROUP, ngrid = (ntiles + gq - 1) / gq * gq;
         const int64_t r = b >> 3, grp = r / XCD_GROUP;
         const int64_t lin = (grp * 8 + (b & 7)) * XCD_GROUP + (r % XCD_GROUP);
-        tile = (int64_t)gridDim.x - 1 - lin;
+        tile = ngrid - 1 - lin;
         if (tile >= ntiles) return;
     }
 #ifdef EFD_EXP_TCLK
@@ -2462,7 +2464,62 @@ __attribute__((amdgpu_num_vgpr(EFD_MODESUM_VGPRS)))
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 #endif
 void k_modesum(EFD_MODESUM_PARAMS) {
-    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS);
+    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, (int64_t)blockIdx.x);
+}
+
+// K8 over a batch of prepared waveforms in one launch (efd_modesum_sum_batch): workgroup g takes
+// waveform g mod n at place g / n of that waveform's dispatch order, so the waveforms' tiles
+// interleave longest-first and one launch's ramp, tail and inter-launch gap are shared by n
+// waveforms. Each waveform keeps its own workspace and outputs; its tiles run exactly the code of
+// a single launch (bitwise the same spectrum). The per-waveform pointers travel in the kernel
+// arguments (n <= EFD_BATCH_MAX), read with wave-uniform scalar loads. Config 2 (bench.py, 2
+// rounds): 1,238 waveforms/s one sum per launch; 2 / 4 / 8 / 16 per launch 1,311 / 1,331 /
+// 1,291 / 1,288 (k_modesum 0.781 -> 0.742 ms per waveform at 4; past 4 the concurrent
+// waveforms' records outgrow the caches). Waveform-major order (each waveform's longest-first
+// order in turn) measured 1,288 / 1,290 / 1,226 / 1,187.
+struct BatchDesc {
+    const Item* items;
+    const int4* ranges;
+    const int2* seglh;
+    const int4* seginfo;
+    const int32_t* nseg;
+    const double* freq;
+    const int32_t* gm;
+    const int32_t* gn;
+    const double* t;
+    const double* coefA;
+    const double* coefT;
+    const double2* sctab;
+    const uint32_t* tkeys;
+    const int32_t* tcnt;
+    const int32_t* tperm;
+    const int32_t* segbase;
+    const int32_t* stb0;
+    const int32_t* stb1;
+    Header* hdr;
+    double* out;
+    double* hp;
+    double* hc;
+    int64_t k0;
+    int32_t nt, K;
+};
+struct SumBatch {
+    BatchDesc d[EFD_BATCH_MAX];
+    int32_t n;
+};
+static_assert(sizeof(SumBatch) <= 3584, "batch descriptors must fit the kernel arguments");
+template <bool PAIRED, int CAUSTIC, int BPL>
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
+void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t ntiles,
+                     int accumulate_out) {
+    const int n = batch.n;
+    const int w = (int)(blockIdx.x % (unsigned)n);
+    const int64_t pos = blockIdx.x / (unsigned)n;
+    const BatchDesc& d = batch.d[w];
+    modesum_tile<PAIRED, CAUSTIC, BPL>(
+        d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt, d.K,
+        d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm, d.segbase, d.stb0,
+        d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, pos);
 }
 
 // K6: the tiles' record lists, built in the preparation phase (k_modesum DMAs them in). The same
@@ -3027,9 +3084,8 @@ static int64_t resident_tile_slots() {
     return v;
 }
 
-// phase: 1 = prepare (K0-K5), 2 = sum (K8), 3 = both
-static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
-                        void* stream, int phase) {
+// argument checks of efd_modesum / _prepare / _sum (phase as in modesum_impl)
+static int check_modesum_args(const efd_modesum_args* a, const void* workspace, int phase) {
     if (!a || !workspace) return fail(EFD_ERR_ARG, "efd_modesum: NULL argument");
     if (!a->t || !a->phi_phi || !a->phi_r || !a->f_phi || !a->f_r || !a->amp || !a->m ||
         !a->n || !a->ylm_p || !a->ylm_m || !a->freq)
@@ -3046,6 +3102,16 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         return fail(EFD_ERR_ARG, "efd_modesum: nf out of range");
     if (a->caustic != EFD_CAUSTIC_SPA && a->caustic != EFD_CAUSTIC_UNIFORM)
         return fail(EFD_ERR_ARG, "efd_modesum: unknown caustic mode");
+    return EFD_OK;
+}
+
+// phase: 1 = prepare (K0-K5), 2 = sum (K8), 3 = both
+static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                        void* stream, int phase) {
+    {
+        const int rc = check_modesum_args(a, workspace, phase);
+        if (rc != EFD_OK) return rc;
+    }
     const int paired = a->grid_symmetric ? 1 : 0;
     const Layout L = make_layout(a->nt, a->K, a->nf, paired);
     if (workspace_bytes < L.total)
@@ -3199,6 +3265,81 @@ int efd_modesum_prepare(const efd_modesum_args* a, void* workspace, size_t works
 int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
                     void* stream) {
     return modesum_impl(a, workspace, workspace_bytes, stream, 2);
+}
+
+int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspace,
+                          const size_t* workspace_bytes, int32_t count, void* stream) {
+    if (!a || !workspace || !workspace_bytes)
+        return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: NULL argument");
+    if (count < 1 || count > EFD_BATCH_MAX)
+        return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: count out of range [1, EFD_BATCH_MAX]");
+    SumBatch batch{};
+    batch.n = count;
+    Layout L0{};
+    for (int i = 0; i < count; ++i) {
+        const efd_modesum_args* ai = a[i];
+        const int rc = check_modesum_args(ai, workspace[i], 2);
+        if (rc != EFD_OK) return rc;
+        if (ai->nf != a[0]->nf || (ai->grid_symmetric != 0) != (a[0]->grid_symmetric != 0) ||
+            ai->caustic != a[0]->caustic || (ai->accumulate != 0) != (a[0]->accumulate != 0))
+            return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: nf, grid_symmetric, caustic and "
+                                     "accumulate must agree across the batch");
+        const int paired = ai->grid_symmetric ? 1 : 0;
+        const Layout L = make_layout(ai->nt, ai->K, ai->nf, paired);
+        if (workspace_bytes[i] < L.total)
+            return fail(EFD_ERR_WORKSPACE, "efd_modesum_sum_batch: workspace too small (see "
+                                           "efd_modesum_workspace_bytes)");
+        if (i == 0) L0 = L;
+        char* ws = (char*)workspace[i];
+        BatchDesc& d = batch.d[i];
+        d.items = (const Item*)(ws + L.items);
+        d.ranges = (const int4*)(ws + L.ranges);
+        d.seglh = (const int2*)(ws + L.seglh);
+        d.seginfo = (const int4*)(ws + L.seginfo);
+        d.nseg = (const int32_t*)(ws + L.nseg);
+        d.freq = ai->freq;
+        d.gm = (const int32_t*)(ws + L.gm);
+        d.gn = (const int32_t*)(ws + L.gn);
+        d.t = ai->t;
+        d.coefA = (const double*)(ws + L.coefA);
+        d.coefT = (const double*)(ws + L.coefT);
+        d.sctab = (const double2*)(ws + L.sctab);
+        d.tkeys = (const uint32_t*)(ws + L.tkeys);
+        d.tcnt = EFD_PREBUILT_LISTS ? (const int32_t*)(ws + L.tcnt) : nullptr;
+        d.tperm = (EFD_PREBUILT_LISTS && EFD_COST_ORDER && L.ntiles > resident_tile_slots())
+                      ? (const int32_t*)(ws + L.tperm) : nullptr;
+        d.segbase = (const int32_t*)(ws + L.segbase);
+        d.stb0 = (const int32_t*)(ws + L.stb0);
+        d.stb1 = (const int32_t*)(ws + L.stb1);
+        d.hdr = (Header*)(ws + L.header);
+        d.out = ai->out;
+        d.hp = ai->hp;
+        d.hc = ai->hc;
+        d.k0 = ai->k0;
+        d.nt = ai->nt;
+        d.K = ai->K;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t gq = 8 * XCD_GROUP;
+    const int64_t nblk = (L0.ntiles + gq - 1) / gq * gq * count;
+    if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: grid too large");
+    const dim3 grid((unsigned)nblk), block(TILE);
+    const int acc = a[0]->accumulate ? 1 : 0;
+    if (a[0]->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a[0]->prof_begin, st));
+#define EFD_LAUNCH(P, C)                                                                      \
+    hipLaunchKernelGGL((k_modesum_batch<P, C, BPL>), grid, block, 0, st, batch, a[0]->nf,       \
+                       L0.nlanes, L0.ntiles, acc)
+    if (a[0]->grid_symmetric) {
+        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
+        else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
+    } else {
+        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(false, EFD_CAUSTIC_UNIFORM);
+        else EFD_LAUNCH(false, EFD_CAUSTIC_SPA);
+    }
+#undef EFD_LAUNCH
+    HIP_TRY(hipGetLastError());
+    if (a[0]->prof_end) HIP_TRY(hipEventRecord((hipEvent_t)a[0]->prof_end, st));
+    return EFD_OK;
 }
 
 int efd_modesum_status(const void* workspace, void* stream) {

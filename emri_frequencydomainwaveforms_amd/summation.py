@@ -168,6 +168,17 @@ class ModeSumEngine:
         waveform's preparation with the previous one's sum on another stream).
         """
         torch = _torch()
+        a, ws = self._args(inp, freq, out, grid_symmetric, scale, accumulate, prof_events, hp,
+                           hc, k0)
+        st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
+        fn = {"all": "efd_modesum", "prepare": "efd_modesum_prepare",
+              "sum": "efd_modesum_sum"}[phase]
+        _lib.check(getattr(self.lib, fn)(a, ws.data_ptr(), ws.numel(), st), fn, self.lib)
+        return ws
+
+    def _args(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
+              prof_events=(None, None), hp=None, hc=None, k0=0):
+        """(efd_modesum_args, workspace) of one launch."""
         nf = int(freq.numel())
         ws = self._workspace(inp.nt, inp.K, nf, freq.device)
         ptr = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
@@ -181,11 +192,7 @@ class ModeSumEngine:
             caustic=CAUSTIC_MODES[self.caustic], accumulate=1 if accumulate else 0,
             out=ptr(out), prof_begin=prof_events[0], prof_end=prof_events[1],
             hp=ptr(hp), hc=ptr(hc), k0=int(k0))
-        st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
-        fn = {"all": "efd_modesum", "prepare": "efd_modesum_prepare",
-              "sum": "efd_modesum_sum"}[phase]
-        _lib.check(getattr(self.lib, fn)(a, ws.data_ptr(), ws.numel(), st), fn, self.lib)
-        return ws
+        return a, ws
 
     def status(self, stream=None):
         """Synchronise; True when the last launch reported no device-side error."""
@@ -226,6 +233,37 @@ class ModeSumEngine:
             if not self.status():
                 raise _lib.EFDError(f"efd_modesum: {_lib.last_error(self.lib)}")
         return out
+
+
+def sum_batch(jobs, stream=None, prof_events=(None, None)):
+    """The mode sums of several prepared waveforms in one launch (efd_modesum_sum_batch).
+
+    jobs: sequence of (engine, launch_kwargs) pairs; each engine was prepared with
+    `launch(..., phase="prepare")` and launch_kwargs are the keyword arguments its
+    `launch(..., phase="sum")` would take (inp, freq, out, grid_symmetric, and optionally scale,
+    accumulate, hp, hc, k0). Every waveform's outputs are bitwise those of its own sum; the
+    waveforms' tiles share one longest-first dispatch (one ramp, one tail, no launch gaps).
+    prof_events bracket the launch. At most EFD_BATCH_MAX waveforms.
+    """
+    import ctypes
+    torch = _torch()
+    jobs = list(jobs)
+    if not 1 <= len(jobs) <= _lib.EFD_BATCH_MAX:
+        raise ValueError(f"sum_batch takes 1..{_lib.EFD_BATCH_MAX} waveforms")
+    args, wss = [], []
+    for i, (eng, kw) in enumerate(jobs):
+        a, ws = eng._args(prof_events=prof_events if i == 0 else (None, None), **kw)
+        args.append(a)
+        wss.append(ws)
+    n = len(jobs)
+    pa = (ctypes.POINTER(_lib.ModesumArgs) * n)(*[ctypes.pointer(a) for a in args])
+    pw = (ctypes.c_void_p * n)(*[ws.data_ptr() for ws in wss])
+    pb = (ctypes.c_size_t * n)(*[ws.numel() for ws in wss])
+    lib = jobs[0][0].lib
+    freq = jobs[0][1]["freq"]
+    st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
+    _lib.check(lib.efd_modesum_sum_batch(pa, pw, pb, n, st), "efd_modesum_sum_batch", lib)
+    return wss
 
 
 class WaveformPipeline:

@@ -126,6 +126,20 @@ int efd_modesum_prepare(const efd_modesum_args* a, void* workspace, size_t works
 int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
                     void* stream);
 
+/*
+ * _sum for `count` prepared waveforms in one kernel launch (1 <= count <= EFD_BATCH_MAX): the
+ * waveforms' tiles interleave in one longest-first dispatch, so the launch's ramp, tail and the
+ * gap between launches are shared (a batch of walkers in a likelihood, or of templates). a[i] and
+ * workspace[i] are exactly what efd_modesum_sum would take for waveform i (each prepared by
+ * efd_modesum_prepare on its own workspace); every a[i] must agree on nf, grid_symmetric, caustic
+ * and accumulate. Each waveform's outputs are bitwise those of its own efd_modesum_sum. The
+ * profiling events of a[0] bracket the launch; efd_modesum_status / _stats work per workspace.
+ * Not part of the reference's interface: an extension for its batched callers.
+ */
+#define EFD_BATCH_MAX 16
+int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspace,
+                          const size_t* workspace_bytes, int32_t count, void* stream);
+
 /* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
  * this workspace: a harmonic with more than 8 monotonic frequency runs, or |m| > 255 or
  * |n| > 1023 -> EFD_ERR_ARG; a tile dispatch-order entry out of range in the sum (its bins left

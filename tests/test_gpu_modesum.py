@@ -259,3 +259,72 @@ def test_wide_mn_range_grouping(multimode):
     S, eng = _gpu(d, d["freq"])
     R = _oracle(d, d["freq"])
     assert _relerr(S, R) < RTOL
+
+
+def _dev_inputs(d):
+    return DeviceInputs.from_host(d["t"], np.asarray(d["amp"]).T, d["phi_phi"], d["phi_r"],
+                                  d["f_phi"], d["f_r"], d["m"], d["n"], d["ylm_p"], d["ylm_m"])
+
+
+def test_sum_batch_matches_single_sums(multimode):
+    """efd_modesum_sum_batch: three different waveforms (different trajectories, harmonic
+    counts and amplitudes) on one grid, summed in one launch, give bitwise the spectra (and fused
+    h+/hx) of their own efd_modesum_sum, on the paired and the unpaired kernel; mismatched grids
+    and bad counts are rejected."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.summation import sum_batch
+    d1 = multimode
+    d2 = source_inputs(M=3e5, mu=10.0, e0=0.2, T=0.02, dt=20.0, eps=1e-2)
+    assert np.array_equal(d2["freq"], d1["freq"])
+    d3 = dict(d1)
+    keep = np.arange(len(d1["m"])) % 2 == 0
+    for k in ("m", "n", "ylm_p", "ylm_m"):
+        d3[k] = np.asarray(d1[k])[keep]
+    d3["amp"] = 0.5 * np.asarray(d1["amp"])[keep]
+    freq = torch.as_tensor(d1["freq"], device="cuda")
+    nf = len(d1["freq"])
+    k0 = int(np.searchsorted(d1["freq"], 0.0))
+    cases = [(d, _dev_inputs(d), ModeSumEngine()) for d in (d1, d2, d3)]
+    for sym in (True, False):
+        single, outs, jobs = [], [], []
+        for d, inp, eng in cases:
+            eng.launch(inp, freq, None, sym, d["prefactor"], phase="prepare")
+            S = torch.full((nf,), np.nan, dtype=torch.complex128, device="cuda")
+            eng.launch(inp, freq, torch.view_as_real(S), sym, d["prefactor"], phase="sum")
+            single.append(S)
+            B = torch.full_like(S, np.nan)
+            outs.append(B)
+            jobs.append((eng, dict(inp=inp, freq=freq, out=torch.view_as_real(B),
+                                   grid_symmetric=sym, scale=d["prefactor"])))
+        sum_batch(jobs)
+        for (d, inp, eng), S, B in zip(cases, single, outs):
+            assert eng.status()
+            assert torch.equal(S, B)
+    # fused h+/hx (symmetric grid, f >= 0) in a batch == each waveform's own fused sum
+    ref, jobs, outs = [], [], []
+    for d, inp, eng in cases:
+        eng.launch(inp, freq, None, True, d["prefactor"], phase="prepare")
+        hp = torch.empty(nf - k0, dtype=torch.complex128, device="cuda")
+        hc = torch.empty_like(hp)
+        eng.launch(inp, freq, None, True, d["prefactor"], phase="sum",
+                   hp=torch.view_as_real(hp), hc=torch.view_as_real(hc), k0=k0)
+        ref.append((hp, hc))
+        bp, bc = torch.full_like(hp, np.nan), torch.full_like(hc, np.nan)
+        outs.append((bp, bc))
+        jobs.append((eng, dict(inp=inp, freq=freq, out=None, grid_symmetric=True,
+                               scale=d["prefactor"], hp=torch.view_as_real(bp),
+                               hc=torch.view_as_real(bc), k0=k0)))
+    sum_batch(jobs)
+    for (hp, hc), (bp, bc) in zip(ref, outs):
+        assert torch.equal(hp, bp) and torch.equal(hc, bc)
+    # every member must share the grid size, kind, caustic mode and accumulate flag
+    short = freq[1:]
+    bad = [jobs[0], (cases[1][2], dict(inp=cases[1][1], freq=short, out=torch.view_as_real(
+        torch.empty(nf - 1, dtype=torch.complex128, device="cuda")), grid_symmetric=False,
+        scale=1.0))]
+    with pytest.raises(_lib.EFDError):
+        sum_batch(bad)
+    with pytest.raises(ValueError):
+        sum_batch([jobs[0]] * (_lib.EFD_BATCH_MAX + 1))
+    with pytest.raises(ValueError):
+        sum_batch([])
