@@ -625,6 +625,9 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
     // (cp_i, 1/m_i, a_i of the Thomas sweep), then every lane runs the two division-free
     // recurrences for its right-hand side. DP(i) lives in the c1 slot of interval i of the
     // output (read back, one row ahead, by the back substitution before that row is written).
+    // grids are sized for the harmonic count K before the device knows the group count: blocks
+    // past the interpolants leave before the shared factorisation (a serial chain of ~n steps)
+    if (block * (int)blockDim.x >= count) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* xs = lds;
     double* cpl = lds + n;
@@ -754,6 +757,7 @@ __device__ void inverse_splines(const double* __restrict__ t, const double* __re
                                   int32_t* __restrict__ runs, Item* __restrict__ items,
                                   double* __restrict__ cpbuf, double* __restrict__ dpbuf,
                                   int32_t* __restrict__ err, int block) {
+    if (block * (int)blockDim.x >= G) return;   // grid sized for K >= G
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* ts = lds;              // t, f_phi, f_r staged in LDS for the serial chains
     double* fps = lds + nt;
@@ -922,6 +926,8 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
                         Header* __restrict__ hdr) {
     const int ni = nt - 1;
     const int G = hdr->groups;
+    // the grid is sized for K >= G groups: whole blocks past the records leave at once
+    if ((int64_t)blockIdx.x * blockDim.x >= (int64_t)ni * G) return;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     __shared__ unsigned long long red[2][4];
     unsigned long long ev = 0, contrib = 0;
@@ -3149,6 +3155,15 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     const int64_t nl1 = paired ? ((nf % 2) ? nl - 1 : nl) : nf;
 
     if (phase & 1) {
+#ifdef EFD_EXP_SKIP   // diagnostic: after the warm-up, skip preparation kernels (bit mask: 1 groups,
+    // 2 k_prep, 4 k_items, 8 segment table, 16 k_tile_keys, 32 k_tile_order); valid only when
+    // every call repeats the same inputs on workspaces that already hold their results
+    static int exp_calls = 0;
+    const int skip = ++exp_calls > 16 ? EFD_EXP_SKIP : 0;
+#else
+    constexpr int skip = 0;
+#endif
+    if (!(skip & 1)) {
     HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
 
     // K0: (m, n) groups
@@ -3158,9 +3173,10 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
                        a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
     HIP_TRY(hipGetLastError());
+    }
     // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
     // grids sized for G = K, blocks past the device-side G return at once)
-    {
+    if (!(skip & 2)) {
         const int nb_amp = (4 * K + 63) / 64;
         const int nb_inv = (K + 63) / 64;
         hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp + nb_inv), dim3(64), sizeof(double) * 7 * nt, st,
@@ -3173,7 +3189,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
 #endif
     }
     // K4: interval records
-    {
+    if (!(skip & 4)) {
         const int64_t total = (int64_t)(nt - 1) * K;
         const int threads = 256;
         const int64_t blocks = (total + threads - 1) / threads;
@@ -3183,7 +3199,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         HIP_TRY(hipGetLastError());
     }
     // K5: segment table
-    {
+    if (!(skip & 8)) {
         const int nslot = K * MAXRUNS * 2;
         int2* slot_lh = (int2*)(ws + L.slotlh);
         int4* slot_info = (int4*)(ws + L.slotinfo);
@@ -3207,15 +3223,12 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     // pipeline
     {
         const dim3 block(TILE);
-#ifdef EFD_EXP_SKIP_TL   // diagnostic: after the warm-up, reuse the lists (same inputs only)
-        static int exp_calls = 0;
-        if (++exp_calls > 8) {} else
-#endif
+        if (!(skip & 16))
         hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)L.ntiles), block, 0, st, ranges, seglh,
                            seginfo, nseg, segbase, stb0, stb1, L.ntiles, tkeys, tcnt);
         HIP_TRY(hipGetLastError());
 #if EFD_COST_ORDER
-        if (L.ntiles > resident_tile_slots()) {
+        if (L.ntiles > resident_tile_slots() && !(skip & 32)) {
             hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
                                (int32_t*)(ws + L.tperm));
             HIP_TRY(hipGetLastError());
