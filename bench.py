@@ -24,10 +24,10 @@ max over ranks of the timed region.
 
 roofline: the mode-sum kernel (k_modesum_batch, or k_modesum at --batch 1) timed with HIP events
 recorded on its own stream around each launch in the timed region; t = launch time / B per
-waveform; achieved = B_alg / t with B_alg = 32 C + 32 n_interp N_t + 16 N_f
+waveform; achieved = B * B_alg per launch / launch time, B_alg = 32 C + 32 n_interp N_t + 16 N_f
 (32 B per SPA contribution of the reference's scatter formulation),
 peak 8.0 TB/s (MI355X_MICROARCH.md). traffic: HBM bytes per launch from the committed rocprofv3
-PMC pass (profiles/), or null.
+PMC pass (profiles/) when it was taken at the same batch, or null.
 
 cpu_baseline: the oracle's C restatement (oracle/fd_oracle_c.c, OpenMP, kind "port") timed on a
 bounded sample of the same workload (a subset of its harmonics) on this host, extrapolated to
@@ -254,18 +254,19 @@ def main():
         n_interp = 2 * K + 4
         b_alg = 32.0 * C + 32.0 * n_interp * nt + 16.0 * nf
         wf_ms = kern_ms / B   # one launch sums B waveforms
-        achieved = b_alg / (wf_ms * 1e-3) / 1e9
+        achieved = B * b_alg / (kern_ms * 1e-3) / 1e9   # algorithmic bytes per launch / launch
         traffic = None
         fp64 = None
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof):
             try:
                 pj = json.load(open(prof))
-                if pj.get("workload") == "config2" and pj.get("caustic") == args.caustic:
+                if (pj.get("workload") == "config2" and pj.get("caustic") == args.caustic
+                        and int(pj.get("batch", 1)) == B):
                     traffic = pj.get("hbm_bytes_per_launch")
                     f = pj.get("fp64")
                     if f:
-                        tf = f["flops_per_launch"] / (wf_ms * 1e-3) / 1e12
+                        tf = f["flops_per_launch"] / (kern_ms * 1e-3) / 1e12
                         fp64 = {"achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                                 "frac": tf / FP64_VALU_PEAK_TFLOPS,
                                 "valu_busy": f["valu_busy"],
@@ -304,6 +305,7 @@ def main():
                        "slots": len(slots), "sum_streams": len(s_sums), "batch": B},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_alg_per_launch": B * b_alg, "waveforms_per_launch": B,
                          "kernel": "k_modesum_batch" if B > 1 else "k_modesum",
                          "kernel_ms": kern_ms, "kernel_ms_per_waveform": wf_ms,
                          "kernel_timing": "HIP events around each k_modesum launch in the timed "

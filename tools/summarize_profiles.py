@@ -4,7 +4,8 @@
 
 writes profiles/<tag>_kernel_stats.csv (the --kernel-trace --stats summary as produced),
 profiles/<tag>_bench.json (the bench line of the same round), profiles/<tag>_pmc.json
-(per-launch counter values of k_modesum) and profiles/pmc_traffic.json, which bench.py reads
+(per-launch counter values of the mode-sum kernel: k_modesum_batch when the bench line's
+config.batch > 1, one launch per batch of waveforms) and profiles/pmc_traffic.json, which bench.py reads
 for roofline.traffic. HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (kB units from
 rocprofv3): MI355X_MICROARCH.md, section HBM: on gfx950 FETCH_SIZE reports half of the bytes
 of wide coalesced reads, WRITE_SIZE reads exactly for 16-B stores.
@@ -69,19 +70,22 @@ def main(tag):
                                              + pmc["SQ_INSTS_VALU_ADD_F64"]
                                              + pmc["SQ_INSTS_VALU_TRANS_F64"])
                 / pmc["SQ_INSTS_VALU"]}
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    # one launch sums `batch` waveforms (k_modesum_batch; 1 = k_modesum)
+    batch = int(bench["config"].get("batch", 1))
+    kernel = "k_modesum_batch" if batch > 1 else "k_modesum"
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-        if "k_modesum" in r["Name"]:
+        if kernel in r["Name"] and (batch > 1 or "k_modesum_batch" not in r["Name"]):
             stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
-    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
-    summary = {"tag": tag, "kernel": "k_modesum", "workload": "config2",
+    summary = {"tag": tag, "kernel": kernel, "workload": "config2", "batch": batch,
                "caustic": "uniform", "counters_per_launch": pmc, "dispatches": ndisp,
-               "hbm_bytes_per_launch": hbm, "fp64": fp64,
+               "hbm_bytes_per_launch": hbm, "hbm_bytes_per_waveform": hbm / batch, "fp64": fp64,
                "hbm_formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (kB; gfx950 FETCH_SIZE x2)",
                "rocprof_avg_ms": stats.get("avg_ns", 0.0) / 1e6,
                "bench_event_ms": bench["roofline"]["kernel_ms"]}
     json.dump(summary, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
-    json.dump({"workload": "config2", "caustic": "uniform", "kernel": "k_modesum",
+    json.dump({"workload": "config2", "caustic": "uniform", "kernel": kernel, "batch": batch,
                "hbm_bytes_per_launch": hbm, "fp64": fp64, "source": f"profiles/{tag}_pmc.json"},
               open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
