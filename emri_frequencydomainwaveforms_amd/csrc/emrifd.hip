@@ -1565,16 +1565,27 @@ __constant__ double KRH[4] = {1.0, -0.034722222222222222222, 0.05509741512345679
 constexpr double KTH0 = -0.069444444444444444444;   // TH_0
 __constant__ double KTHN[4] = {1.0, -0.51157407407407407407, 1.5977044753086419754,
                                -12.267136107513349990};   // TH_j / TH_0
+// EFD_J34: records of series length 3 take the fourth terms too (below 1e-17 on their
+// intervals, by the choice of J), so J = 3 and J = 4 share one branch: the compiler otherwise
+// if-converts the J >= 4 increments and merges the two results with 4 v_cndmask per evaluation.
+#ifndef EFD_J34
+#define EFD_J34 1
+#endif
 __device__ __forceinline__ void kpolar_rt(int J, double ww, double& rho, double& thn) {
     static_assert(FAST_J == 4, "kpolar_rt: increments up to 4 terms");
     const double uu = ww * ww;
     double r = fma(KRH[1], uu, 1.0);   // KRH[0] == 1
     double t = fma(KTHN[1], uu, 1.0);
     if (J >= 3) {   // wave-uniform
+#if EFD_J34
+        // a real branch: without it the compiler computes the 4-term form for every record and
+        // selects (6 FP64 operations + 4 v_cndmask per evaluation for the 82% of J <= 2)
+        asm volatile("");
+#endif
         const double u2 = uu * uu;
         r = fma(KRH[2], u2, r);
         t = fma(KTHN[2], u2, t);
-        if (J >= 4) {
+        if (EFD_J34 || J >= 4) {
             const double u3 = u2 * uu;
             r = fma(KRH[3], u3, r);
             t = fma(KTHN[3], u3, t);
@@ -1722,6 +1733,21 @@ __device__ __forceinline__ uint64_t class_mask(double x, int32_t cls) {
     asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(m) : "v"(x), "s"(cls));
     return m;
 }
+// Masking the fast path's amplitude (EFD_FTZ_SELECT): k_modesum runs with FP64 denormals
+// flushed (modesum_tile sets the MODE register; no value of the sum comes near 1e-308), so
+// clearing the high word alone turns any amp -- inf and NaN included -- into a denormal that
+// every later FP64 operation reads as +0: one v_cndmask_b32 instead of two for the 64-bit
+// select, with bitwise the same W (+0 either way).
+#ifndef EFD_FTZ_SELECT
+#define EFD_FTZ_SELECT 1
+#endif
+__device__ __forceinline__ double ftz_select(bool ok, double v) {
+#if EFD_FTZ_SELECT
+    return __hiloint2double(ok ? __double2hiint(v) : 0, __double2loint(v));
+#else
+    return ok ? v : 0.0;
+#endif
+}
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            int J, uint64_t actm, const double2* __restrict__ sct,
@@ -1761,7 +1787,7 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         // (a NaN thn becomes 1; far outside the series' range thn is large of either sign), so
         // sin/cos stay finite and the zero amplitude below zeroes W. |.| is a source modifier.
 #if EFD_REC_SIGN
-        const double am = ok ? amp * rho : 0.0;
+        const double am = ftz_select(ok, amp * rho);
         sincos_tab(psi0, rs.shift, sct, sn, cs, fmin(fabs(thn), 1.0), true, rs.kth);
 #else
         const double ths = copysign(fmin(fabs(thn), 1.0), fd);
@@ -1772,7 +1798,7 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         wi = am * sn;
     } else {
         const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
-        const double am = ok ? amp : 0.0;
+        const double am = ftz_select(ok, amp);
 #if EFD_REC_SIGN
         sincos_tab(psi0, rs.shift, sct, sn, cs);
 #else
@@ -2003,6 +2029,11 @@ __device__ __forceinline__ void modesum_tile(
     }
 #ifdef EFD_EXP_TCLK
     const unsigned long long t_start = wall_clock64();
+#endif
+#if EFD_FTZ_SELECT
+    // MODE.FP_DENORM[3:2] (FP64/FP16) = 0: flush denormal inputs and outputs (ftz_select). The
+    // mode is per wave and set from the kernel descriptor at every wave launch.
+    __builtin_amdgcn_s_setreg(1 | (6 << 6) | (1 << 11), 0);   // hwreg(HW_REG_MODE, 6, 2)
 #endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;

@@ -81,3 +81,36 @@ def test_config2_linearity_and_determinism(cfg2):
             accumulate=True)
     err = (P - S).abs().max().item() / S.abs().max().item()
     assert err <= 1e-12, err
+
+
+def test_config2_batched_sum_bitwise(cfg2):
+    """The bench's path at full size: several prepared config-2 waveforms (the full harmonic set
+    and two subsets, so the batch mixes tile costs and record counts) summed by one
+    efd_modesum_sum_batch launch with fused h+/hx give bitwise each waveform's own fused
+    efd_modesum_sum, which test_config2_full_spectrum_vs_c_oracle holds to the oracle."""
+    from emri_frequencydomainwaveforms_amd.summation import sum_batch
+    w = cfg2
+    freq = torch.as_tensor(w["freq"], device="cuda")
+    nf = len(w["freq"])
+    k0 = int(np.searchsorted(w["freq"], 0.0))
+    idx = np.arange(len(w["m"]))
+    sels = [None, idx[idx % 3 == 0], idx[idx % 2 == 1], None]
+    ref, outs, jobs = [], [], []
+    for sel in sels:
+        inp, eng = _inputs(w, sel), ModeSumEngine(caustic="uniform")
+        eng.launch(inp, freq, None, True, w["prefactor"], phase="prepare")
+        hp = torch.empty(nf - k0, dtype=torch.complex128, device="cuda")
+        hc = torch.empty_like(hp)
+        eng.launch(inp, freq, None, True, w["prefactor"], phase="sum",
+                   hp=torch.view_as_real(hp), hc=torch.view_as_real(hc), k0=k0)
+        ref.append((hp, hc))
+        bp, bc = torch.full_like(hp, np.nan), torch.full_like(hc, np.nan)
+        outs.append((bp, bc))
+        jobs.append((eng, dict(inp=inp, freq=freq, out=None, grid_symmetric=True,
+                               scale=w["prefactor"], hp=torch.view_as_real(bp),
+                               hc=torch.view_as_real(bc), k0=k0)))
+    sum_batch(jobs)
+    for (eng, _), (hp, hc), (bp, bc) in zip(jobs, ref, outs):
+        assert eng.status()
+        assert torch.equal(hp, bp) and torch.equal(hc, bc)
+    assert not torch.equal(ref[0][0], ref[1][0])
