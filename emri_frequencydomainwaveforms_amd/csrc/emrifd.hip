@@ -1344,6 +1344,25 @@ __device__ __forceinline__ double rsqrt_pos(double x) {
     return fma(y * e, 0.5, y);
 }
 
+// The same inside k_modesum with the halving on the FMA's output modifier (EFD_OMOD): e/2 comes
+// straight out of v_fma_f64 ... div:2, one FP64 operation fewer. The output modifiers apply only
+// with IEEE mode off and FP64 denormals flushed (tools/rsq_omod_check.hip: otherwise the
+// modifier is silently ignored), which modesum_tile sets in the MODE register; the compiler never
+// emits them itself in IEEE mode, hence the inline asm. Only for k_modesum's mode.
+#ifndef EFD_OMOD
+#define EFD_OMOD 1
+#endif
+__device__ __forceinline__ double rsqrt_pos_sum(double x) {
+#if EFD_OMOD
+    const double y = __builtin_amdgcn_rsq(x);
+    double h;
+    asm("v_fma_f64 %0, -%1, %2, 1.0 div:2" : "=v"(h) : "v"(x * y), "v"(y));
+    return fma(y, h, y);
+#else
+    return rsqrt_pos(x);
+#endif
+}
+
 // Q factor. The mirror-convention term of one branch is A Y Q e^{i(2 pi g t - Phi)} with
 //   SPA:      Q_spa = e^{i sgn(F') 3 pi/4} / sqrt|F'|
 //   uniform:  Q = i F'/|F''| K_{1/3}(z) e^{z} 2/sqrt(3),  z = -i y,  y = 2 pi F'^3 / (3 F''^2)
@@ -1769,7 +1788,7 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
     const int shift = fd > 0.0 ? 192 : -192;
 #endif
     // F' = 0 gives amp = NaN here; every quantity it reaches is selected away below
-    const double amp = rsqrt_pos(afd);
+    const double amp = rsqrt_pos_sum(afd);
     const double psi0 = fma(stfk, tt, -ph);
     double sn, cs;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
@@ -2034,6 +2053,12 @@ __device__ __forceinline__ void modesum_tile(
     // MODE.FP_DENORM[3:2] (FP64/FP16) = 0: flush denormal inputs and outputs (ftz_select). The
     // mode is per wave and set from the kernel descriptor at every wave launch.
     __builtin_amdgcn_s_setreg(1 | (6 << 6) | (1 << 11), 0);   // hwreg(HW_REG_MODE, 6, 2)
+#endif
+#if EFD_OMOD
+    // MODE.IEEE = 0 (rsqrt_pos_sum's output modifier). Nothing here depends on IEEE mode's NaN
+    // rules: the one min (fmin(|thn|, 1)) sees quiet NaNs at most and returns 1 in either mode.
+    static_assert(EFD_FTZ_SELECT, "output modifiers need FP64 denormals flushed");
+    __builtin_amdgcn_s_setreg(1 | (9 << 6), 0);               // hwreg(HW_REG_MODE, 9, 1)
 #endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;

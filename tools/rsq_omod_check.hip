@@ -1,9 +1,14 @@
-// Checks whether v_fma_f64 honours the div:2 output modifier (it does not on gfx950 with FP64
-// denormals enabled): hipcc --offload-arch=gfx950 -O3 tools/rsq_omod_check.hip -o /tmp/rsq_omod
+// Checks whether v_fma_f64 honours the div:2 output modifier, without and with FP64 denormals
+// flushed by s_setreg (MODE.FP_DENORM[3:2]). MI355X: it does not in either mode (eh/e = 1; the
+// kernels run in IEEE mode, where the output modifiers are not applied):
+// hipcc --offload-arch=gfx950 -O3 tools/rsq_omod_check.hip -o /tmp/rsq_omod
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cmath>
+template <int FTZ>
 __global__ void k(const double* x, double* out, int n) {
+    if (FTZ >= 1) __builtin_amdgcn_s_setreg(1 | (6 << 6) | (1 << 11), 0);
+    if (FTZ >= 2) __builtin_amdgcn_s_setreg(1 | (9 << 6), 0);   // MODE.IEEE = 0
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double xv = x[i];
@@ -22,7 +27,10 @@ int main() {
     hipMallocManaged(&x, n * sizeof(double));
     hipMallocManaged(&o, 4 * n * sizeof(double));
     for (int i = 0; i < n; ++i) x[i] = std::ldexp(1.0 + (double)i / n, (i % 97) - 48);
-    hipLaunchKernelGGL(k, dim3(n / 256), dim3(256), 0, 0, x, o, n);
+  for (int ftz = 0; ftz < 3; ++ftz) {
+    if (ftz == 2) hipLaunchKernelGGL(k<2>, dim3(n / 256), dim3(256), 0, 0, x, o, n);
+    else if (ftz == 1) hipLaunchKernelGGL(k<1>, dim3(n / 256), dim3(256), 0, 0, x, o, n);
+    else hipLaunchKernelGGL(k<0>, dim3(n / 256), dim3(256), 0, 0, x, o, n);
     hipDeviceSynchronize();
     double m0 = 0, m1 = 0, my = 0, rmin = 1e9, rmax = -1e9;
     for (int i = 0; i < n; ++i) {
@@ -32,6 +40,8 @@ int main() {
         my = fmax(my, (double)fabsl((o[4 * i + 2] - ex) / ex));
         if (std::isfinite(o[4 * i + 3])) { rmin = fmin(rmin, o[4 * i + 3]); rmax = fmax(rmax, o[4 * i + 3]); }
     }
-    printf("rel err: newton %.3e  omod %.3e  rsq %.3e  eh/e in [%.6f, %.6f]\n", m0, m1, my, rmin, rmax);
+    printf("ftz %d rel err: newton %.3e  omod %.3e  rsq %.3e  eh/e in [%.6f, %.6f]\n", ftz, m0, m1,
+           my, rmin, rmax);
+  }
     return 0;
 }
