@@ -69,7 +69,7 @@ constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the disp
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
 #ifndef EFD_KEYCAP
-#define EFD_KEYCAP (EFD_TILE >= 256 ? 2048 : 1024)
+#define EFD_KEYCAP (EFD_TILE >= 512 ? 4096 : EFD_TILE >= 256 ? 2048 : 1024)
 #endif
 #ifndef EFD_SEGWIN_F
 #define EFD_SEGWIN_F 1   // 256 segments per window: 4 KB of LDS instead of 16 (4 workgroups/CU)
@@ -2287,12 +2287,14 @@ __device__ __forceinline__ void modesum_tile(
             const Item* stg = stage[c & 1];
             // the chunk's record headers, one lane per record, read from LDS once per chunk and
             // packed into one word: the sub-branch's lane range clamped to the tile, relative
-            // to its first lane (10 bits each), s and the series length: hdr = lo | hi << 10 |
-            // s << 20 | jser << 21. Each record then takes one v_readlane (a VALU instruction,
+            // to its first lane (HB bits each), s and the series length: hdr = lo | hi << HB |
+            // s << 2 HB | jser << (2 HB + 1) | fdneg << (2 HB + 4). Each record then takes one v_readlane (a VALU instruction,
             // as costly as an FMA) instead of an LDS round trip and 5 address / readfirstlane
             // operations (round 1), or two readlanes of absolute bounds (round 2 first form).
             static_assert(FAST_J < 8, "header: jser in 3 bits");
-            static_assert(TILE_LANES < 1024, "header: tile-relative lane bounds in 10 bits");
+            constexpr int HB = TILE_LANES < 1024 ? 10 : 11;   // bits of a tile-relative bound
+            constexpr uint32_t HM = (1u << HB) - 1u;
+            static_assert(TILE_LANES < 2048 && 2 * HB + 5 <= 32, "header: one 32-bit word");
             uint32_t hdr = 0;
             if (lane < nin) {
                 const uint32_t kl = keys[c * NC + lane];
@@ -2300,8 +2302,8 @@ __device__ __forceinline__ void modesum_tile(
                 const Item* il = stg + lane;
                 const uint32_t lo = (uint32_t)min(max(il->klo[sl] - tlo, 0), TILE_LANES);
                 const uint32_t hi = (uint32_t)min(max(il->khi[sl] - tlo, 0), TILE_LANES);
-                hdr = lo | (hi << 10) | ((uint32_t)sl << 20) | ((uint32_t)il->jser << 21) |
-                      ((uint32_t)il->fdneg << 24);
+                hdr = lo | (hi << HB) | ((uint32_t)sl << (2 * HB)) |
+                      ((uint32_t)il->jser << (2 * HB + 1)) | ((uint32_t)il->fdneg << (2 * HB + 4));
             }
 #ifdef EFD_EXP_COUNT
             int nev = 0;
@@ -2315,9 +2317,9 @@ __device__ __forceinline__ void modesum_tile(
 #endif
             for (int ii = 0; ii < nin; ++ii) {
                 const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane((int)hdr, ii);
-                const int s = (int)((ha >> 20) & 1u);
-                const int32_t klo = tlo + (int32_t)(ha & 1023u);
-                const int32_t khi = tlo + (int32_t)((ha >> 10) & 1023u);
+                const int s = (int)((ha >> (2 * HB)) & 1u);
+                const int32_t klo = tlo + (int32_t)(ha & HM);
+                const int32_t khi = tlo + (int32_t)((ha >> HB) & HM);
                 const Item* it = stg + ii;
                 if (khi <= w_lo || klo >= w_hi) {              // misses this wave's chunk
 #ifdef EFD_EXP_COUNT
@@ -2339,7 +2341,7 @@ __device__ __forceinline__ void modesum_tile(
                     // wave-uniform values
 #ifdef EFD_EXP_JDIST   // records by series length [0..3], sub-branch flips [4], records [5]
                     if (lane == 0) {
-                        atomicAdd(&g_exp_count[min((int)((ha >> 21) & 7u), 4) - 1], 1ull);
+                        atomicAdd(&g_exp_count[min((int)((ha >> (2 * HB + 1)) & 7u), 4) - 1], 1ull);
                         atomicAdd(&g_exp_count[5], 1ull);
                         if (s != s_cur) atomicAdd(&g_exp_count[4], 1ull);
                     }
@@ -2357,7 +2359,7 @@ __device__ __forceinline__ void modesum_tile(
 #ifdef EFD_EXP_JFIX   // experiment: every record takes the FAST_J-term series (no J dispatch)
                     const int J = FAST_J;
 #else
-                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)((ha >> 21) & 7u) : FAST_J;
+                    const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)((ha >> (2 * HB + 1)) & 7u) : FAST_J;
 #endif
                     // the stage holds b[s] at b[0] (EFD_GLDS swaps the halves for s = 1)
                     const double* xo = &it->b[0][0][0];
@@ -2365,7 +2367,7 @@ __device__ __forceinline__ void modesum_tile(
                     double wr[BPL], wi[BPL], w[BPL];
 #if EFD_SALU_MASKS
                     uint64_t needm[BPL], needany = 0;
-                    const RecSign rs = rec_sign((ha >> 24) & 1u);
+                    const RecSign rs = rec_sign((ha >> (2 * HB + 4)) & 1u);
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t base = w_lo + 64 * i;
