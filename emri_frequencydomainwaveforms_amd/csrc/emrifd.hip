@@ -1303,7 +1303,8 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 constexpr int SCTAB = 512;
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
                                            double& s, double& c, double extra = 0.0,
-                                           bool use_extra = false, double extra_scale = 1.0) {
+                                           bool use_extra = false, double extra_scale = 1.0,
+                                           double c0 = 1.0) {
     constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
     constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
     constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
@@ -1330,7 +1331,9 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
 #else
     const double sr = fma(r * z, -1.6666666666666666e-01, r);
 #endif
-    const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), 1.0);
+    // c0: the cosine polynomial's constant term (1, or a factor 1 + O(1e-9) folded in by the
+    // caller: rho (1 + d) E to within |d| |sr| < 3e-12, see EFD_EARLY_MASK)
+    const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), c0);
     s = fma(t.x, cr, t.y * sr);
     c = fma(t.y, cr, -t.x * sr);
 }
@@ -1790,6 +1793,9 @@ __device__ __forceinline__ double ftz_select(bool ok, double v) {
     return ok ? v : 0.0;
 #endif
 }
+#ifndef EFD_EARLY_MASK
+#define EFD_EARLY_MASK 1
+#endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            int J, uint64_t actm, const double2* __restrict__ sct,
@@ -1815,6 +1821,46 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
     const double psi0 = fma(stfk, tt, -ph);
     double sn, cs;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
+#if EFD_EARLY_MASK
+        static_assert(EFD_REC_SIGN && EFD_FTZ_SELECT && EFD_THETA_TRUNC && FAST_J == 4,
+                      "early mask: record sign, flushed denormals, truncated theta");
+        // The amplitude is masked before it enters 1/|y|: masked lanes get amp = +0 (inf and
+        // NaN included), so w = 0, theta = 0 and rho = 1 there and the angle stays finite with no
+        // clamp; for J <= 3 records every in-interval lane is within the series' range, so
+        // nothing else needs masking. J <= 2 (82% of records): rho - 1 = KRH_1 w^2 < 4.6e-10
+        // goes into the cosine polynomial's constant term instead of a multiply of the
+        // amplitude (rho E to within |rho - 1| |sr| < 3e-12, a rotation far below the phases'
+        // 1e-9 rad rounding). J >= 3 (18%) tests |y| >= FAST_Y, clamps w for the lanes past it
+        // and masks their amplitude again.
+        const double ampm = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm & goodm), amp);
+        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        const double a3 = ampm * ampm * ampm;
+        const double t3 = fdds * a3;
+        double ww = t3 * t3;   // 1/|y|
+        double am, c0, thn;
+        if (J >= 3) {   // wave-uniform; a real branch (see EFD_J34)
+            asm volatile("");
+            // the |y| >= FAST_Y test only matters for J = 4 (J = 3 lanes pass it by their
+            // record's bound), but a nested J test's condition crossed the join as a per-lane
+            // boolean (v_cndmask + v_cmp for every record)
+            goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
+            ww = fmin(ww, 1.0);
+            const double uu = ww * ww, u2 = uu * uu;
+            double r = fma(KRH[1], uu, 1.0);
+            r = fma(KRH[2], u2, r);
+            r = fma(KRH[3], u2 * uu, r);
+            thn = ww * fma(KTHN[2], u2, fma(KTHN[1], uu, 1.0));
+            am = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm & goodm), ampm * r);
+            c0 = 1.0;
+        } else {
+            c0 = fma(KRH[1], ww * ww, 1.0);
+            thn = ww;
+            am = ampm;
+        }
+        sincos_tab(psi0, rs.shift, sct, sn, cs, thn, true, rs.kth, c0);
+        wr = am * cs;
+        wi = am * sn;
+#else
         const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
         const double a3 = amp * amp * amp;
         const double t3 = fdds * a3;
@@ -1838,6 +1884,7 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
 #endif
         wr = am * cs;
         wi = am * sn;
+#endif
     } else {
         const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
         const double am = ftz_select(ok, amp);
