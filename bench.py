@@ -128,6 +128,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4,
                     help="overlap pipeline: waveforms per step, their mode sums in one launch "
                          "(efd_modesum_sum_batch; 1 = one efd_modesum_sum per waveform)")
+    ap.add_argument("--sum-priority", type=int, default=0,
+                    help="overlap pipeline: torch stream priority of the sum stream (negative = "
+                         "higher; the preparation stream keeps the default)")
     ap.add_argument("--diag-sum-only", action="store_true",
                     help="diagnostic, not the metric: each slot is prepared once in the warm-up, "
                          "then every step runs only the mode sum (the sum-stream ceiling)")
@@ -174,8 +177,8 @@ def main():
                                torch.empty(nf, dtype=torch.complex128, device=dev))))
         slots.append(dict(wf=wf, prep_done=torch.cuda.Event(), sum_done=None))
     s_prep = torch.cuda.Stream(dev)
-    s_sums = [torch.cuda.Stream(dev) for _ in range(max(1, args.sum_streams))] if overlap \
-        else [s_prep]
+    s_sums = [torch.cuda.Stream(dev, priority=args.sum_priority)
+              for _ in range(max(1, args.sum_streams))] if overlap else [s_prep]
     s_sum = s_sums[0]
     lib = slots[0]["wf"][0]["eng"].lib
 

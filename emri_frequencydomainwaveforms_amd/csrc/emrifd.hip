@@ -1845,11 +1845,11 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
             // boolean (v_cndmask + v_cmp for every record)
             goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
             ww = fmin(ww, 1.0);
-            const double uu = ww * ww, u2 = uu * uu;
-            double r = fma(KRH[1], uu, 1.0);
-            r = fma(KRH[2], u2, r);
-            r = fma(KRH[3], u2 * uu, r);
-            thn = ww * fma(KTHN[2], u2, fma(KTHN[1], uu, 1.0));
+            // |w| <= 1/153: rho's KRH_3 term (< 2.2e-14) and theta's KTHN_2 term (< 1.3e-12 rad)
+            // are below the accuracy of the rest of the evaluation
+            const double uu = ww * ww;
+            const double r = fma(KRH[2], uu * uu, fma(KRH[1], uu, 1.0));
+            thn = ww * fma(KTHN[1], uu, 1.0);
             am = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm & goodm), ampm * r);
             c0 = 1.0;
         } else {
