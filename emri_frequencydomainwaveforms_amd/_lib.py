@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_prepare",
     "efd_modesum_sum",
     "efd_modesum_sum_batch",
+    "efd_modesum_sum_loglike",
     "efd_modesum_status",
     "efd_modesum_contributions",
     "efd_modesum_stats",
@@ -145,6 +146,11 @@ def load(path=None):
         lib.efd_modesum_sum_batch.restype = ctypes.c_int
         lib.efd_modesum_sum_batch.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
                                               ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp]
+    if hasattr(lib, "efd_modesum_sum_loglike"):
+        lib.efd_modesum_sum_loglike.restype = ctypes.c_int
+        lib.efd_modesum_sum_loglike.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
+                                                ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp,
+                                                vp, vp, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
     lib.efd_modesum_status.argtypes = [vp, vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int

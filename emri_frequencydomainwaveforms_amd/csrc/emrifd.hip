@@ -160,7 +160,7 @@ struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
         seginfo, nseg, slotlh, slotinfo, slotcnt, slottiles, segbase, stb0, stb1, gm, gn, gstart,
         gkeys,
-        gmem, gamp, sctab, tkeys, tcnt, tperm, total;
+        gmem, gamp, sctab, tkeys, tcnt, tperm, llpart, total;
     int64_t stbcap;
     int64_t ntiles, nlanes;
 };
@@ -207,6 +207,7 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.tkeys = take(sizeof(uint32_t) * (size_t)L.ntiles * KEYCAP);   // prebuilt tile lists
     L.tcnt = take(sizeof(int32_t) * (size_t)L.ntiles);
     L.tperm = take(sizeof(int32_t) * (size_t)L.ntiles);   // cost-ordered dispatch (k_tile_order)
+    L.llpart = take(sizeof(double) * (size_t)L.ntiles);   // fused likelihood: per-tile partials
     L.total = off;
     return L;
 }
@@ -2079,6 +2080,10 @@ __device__ __forceinline__ void modesum_tile(
     const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,
     const int32_t* __restrict__ stb1, Header* __restrict__ hdr, int accumulate_out,
     double* __restrict__ out, double* __restrict__ hp, double* __restrict__ hc, int64_t k0,
+    // fused likelihood (efd_modesum_sum_loglike; paired grids): d complex, w real [2][nf - k0];
+    // the tile writes sum_c sum_j |d[c][j] - h_c[j] w[c][j]|^2 over its bins j >= k0 to
+    // llpart[tile]. lld = NULL: not computed.
+    const double* __restrict__ lld, const double* __restrict__ llw, double* __restrict__ llpart,
     int64_t b) {   // b: this workgroup's place in the waveform's dispatch order
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
@@ -2527,6 +2532,7 @@ __device__ __forceinline__ void modesum_tile(
     double2* o = reinterpret_cast<double2*>(out);
     double2* php = reinterpret_cast<double2*>(hp);
     double2* phc = reinterpret_cast<double2*>(hc);
+    double llacc = 0.0;   // fused likelihood: this lane's sum of |d - h w|^2
 #pragma unroll
     for (int i = 0; i < BPL; ++i) {
         const int64_t k = w_lo + 64 * i + lane;
@@ -2549,12 +2555,26 @@ __device__ __forceinline__ void modesum_tile(
             if (accumulate_out) { const double2 p = o[k]; v.x += p.x; v.y += p.y; }
             o[k] = v;
         }
-        if (PAIRED && php) {
+        if (PAIRED && (php || lld)) {
             // h+ = (a + conj b)/2, hx = i (a - conj b)/2 with a = S(j), b = S(nf-1-j)
             auto put = [&](int64_t j, double2 a, double2 b) {
                 if (j < k0) return;
                 double2 vp = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
                 double2 vc = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+                if (lld) {
+                    // d - h w rounded like efd_loglike (product rounded, then difference: no
+                    // contraction), so a template equal to the injection gives exactly 0
+#pragma clang fp contract(off)
+                    const int64_t q = j - k0, nb = nf - k0;
+                    const double2 d0 = reinterpret_cast<const double2*>(lld)[q];
+                    const double2 d1 = reinterpret_cast<const double2*>(lld)[nb + q];
+                    const double w0 = llw[q], w1 = llw[nb + q];
+                    const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
+                    const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
+                    llacc = fma(r0, r0, fma(i0, i0, llacc));
+                    llacc = fma(r1, r1, fma(i1, i1, llacc));
+                }
+                if (!php) return;
                 if (accumulate_out) {
                     const double2 pp = php[j - k0], pc = phc[j - k0];
                     vp.x += pp.x; vp.y += pp.y; vc.x += pc.x; vc.y += pc.y;
@@ -2564,6 +2584,20 @@ __device__ __forceinline__ void modesum_tile(
             };
             put(km, sm, sk);
             if (km != k) put(k, sk, sm);
+        }
+    }
+    if (PAIRED && lld) {
+        // the tile's partial in a fixed order: a butterfly over each wave, then the waves in turn
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) llacc += __shfl_xor(llacc, o, 64);
+        __shared__ double llw4[NWAVE];
+        if (lane == 0) llw4[wave] = llacc;
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < NWAVE; ++w) t += llw4[w];
+            llpart[tile] = t;
         }
     }
 #ifdef EFD_EXP_TCLK
@@ -2598,7 +2632,8 @@ __attribute__((amdgpu_num_vgpr(EFD_MODESUM_VGPRS)))
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 #endif
 void k_modesum(EFD_MODESUM_PARAMS) {
-    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, (int64_t)blockIdx.x);
+    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, nullptr, nullptr, nullptr,
+                                       (int64_t)blockIdx.x);
 }
 
 // K8 over a batch of prepared waveforms in one launch (efd_modesum_sum_batch): workgroup g takes
@@ -2634,6 +2669,7 @@ struct BatchDesc {
     double* out;
     double* hp;
     double* hc;
+    double* llpart;
     int64_t k0;
     int32_t nt, K;
 };
@@ -2645,7 +2681,8 @@ static_assert(sizeof(SumBatch) <= 3584, "batch descriptors must fit the kernel a
 template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t ntiles,
-                     int accumulate_out) {
+                     int accumulate_out, const double* __restrict__ lld,
+                     const double* __restrict__ llw) {
     const int n = batch.n;
     const int w = (int)(blockIdx.x % (unsigned)n);
     const int64_t pos = blockIdx.x / (unsigned)n;
@@ -2653,7 +2690,29 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
     modesum_tile<PAIRED, CAUSTIC, BPL>(
         d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt, d.K,
         d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm, d.segbase, d.stb0,
-        d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, pos);
+        d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld, llw, d.llpart, pos);
+}
+
+// Fused likelihood, second stage: waveform i's out[i] = -1/2 * 4 * (sum of its tiles' partials),
+// one workgroup per waveform, fixed order (a strided pass per thread, then a tree)
+struct LlBatch {
+    const double* part[EFD_BATCH_MAX];
+    double* out;
+    int64_t ntiles;
+    int32_t n;
+};
+__global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
+    __shared__ double red[256];
+    const double* p = lb.part[blockIdx.x];
+    double acc = 0.0;
+    for (int64_t i = threadIdx.x; i < lb.ntiles; i += 256) acc += p[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) lb.out[blockIdx.x] = -0.5 * 4.0 * red[0];
 }
 
 // K6: the tiles' record lists, built in the preparation phase (k_modesum DMAs them in). The same
@@ -3408,28 +3467,37 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
     return modesum_impl(a, workspace, workspace_bytes, stream, 2);
 }
 
-int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspace,
-                          const size_t* workspace_bytes, int32_t count, void* stream) {
+// efd_modesum_sum_batch, and efd_modesum_sum_loglike when d != NULL (paired grids: the tiles
+// write their likelihood partials, k_ll_final turns each waveform's into out[i])
+int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const* workspace,
+                   const size_t* workspace_bytes, int32_t count, const double* d, const double* w,
+                   double* llout, void* stream) {
+    const std::string F(fn);
     if (!a || !workspace || !workspace_bytes)
-        return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: NULL argument");
+        return fail(EFD_ERR_ARG, F + ": NULL argument");
     if (count < 1 || count > EFD_BATCH_MAX)
-        return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: count out of range [1, EFD_BATCH_MAX]");
+        return fail(EFD_ERR_ARG, F + ": count out of range [1, EFD_BATCH_MAX]");
     SumBatch batch{};
     batch.n = count;
     Layout L0{};
     for (int i = 0; i < count; ++i) {
         const efd_modesum_args* ai = a[i];
-        const int rc = check_modesum_args(ai, workspace[i], 2);
+        // (the fused likelihood needs no written output)
+        const int rc = check_modesum_args(ai, workspace[i], d ? 0 : 2);
         if (rc != EFD_OK) return rc;
         if (ai->nf != a[0]->nf || (ai->grid_symmetric != 0) != (a[0]->grid_symmetric != 0) ||
             ai->caustic != a[0]->caustic || (ai->accumulate != 0) != (a[0]->accumulate != 0))
-            return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: nf, grid_symmetric, caustic and "
-                                     "accumulate must agree across the batch");
+            return fail(EFD_ERR_ARG, F + ": nf, grid_symmetric, caustic and accumulate must agree "
+                                         "across the batch");
+        if (d && (!ai->grid_symmetric || ai->accumulate || ai->k0 != a[0]->k0 || ai->k0 < 0 ||
+                  ai->k0 >= ai->nf))
+            return fail(EFD_ERR_ARG, F + ": the fused likelihood needs a symmetric grid, "
+                                         "accumulate = 0 and one 0 <= k0 < nf for the batch");
         const int paired = ai->grid_symmetric ? 1 : 0;
         const Layout L = make_layout(ai->nt, ai->K, ai->nf, paired);
         if (workspace_bytes[i] < L.total)
-            return fail(EFD_ERR_WORKSPACE, "efd_modesum_sum_batch: workspace too small (see "
-                                           "efd_modesum_workspace_bytes)");
+            return fail(EFD_ERR_WORKSPACE, F + ": workspace too small (see "
+                                               "efd_modesum_workspace_bytes)");
         if (i == 0) L0 = L;
         char* ws = (char*)workspace[i];
         BatchDesc& d = batch.d[i];
@@ -3456,6 +3524,7 @@ int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspa
         d.out = ai->out;
         d.hp = ai->hp;
         d.hc = ai->hc;
+        d.llpart = (double*)(ws + L.llpart);
         d.k0 = ai->k0;
         d.nt = ai->nt;
         d.K = ai->K;
@@ -3463,13 +3532,13 @@ int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspa
     hipStream_t st = (hipStream_t)stream;
     const int64_t gq = 8 * XCD_GROUP;
     const int64_t nblk = (L0.ntiles + gq - 1) / gq * gq * count;
-    if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, "efd_modesum_sum_batch: grid too large");
+    if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, F + ": grid too large");
     const dim3 grid((unsigned)nblk), block(TILE);
     const int acc = a[0]->accumulate ? 1 : 0;
     if (a[0]->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a[0]->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum_batch<P, C, BPL>), grid, block, 0, st, batch, a[0]->nf,       \
-                       L0.nlanes, L0.ntiles, acc)
+                       L0.nlanes, L0.ntiles, acc, d, w)
     if (a[0]->grid_symmetric) {
         if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
         else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
@@ -3479,8 +3548,31 @@ int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspa
     }
 #undef EFD_LAUNCH
     HIP_TRY(hipGetLastError());
+    if (d) {
+        LlBatch lb{};
+        lb.n = count;
+        lb.ntiles = L0.ntiles;
+        for (int i = 0; i < count; ++i) lb.part[i] = batch.d[i].llpart;
+        lb.out = llout;
+        hipLaunchKernelGGL(k_ll_final, dim3((unsigned)count), dim3(256), 0, st, lb);
+        HIP_TRY(hipGetLastError());
+    }
     if (a[0]->prof_end) HIP_TRY(hipEventRecord((hipEvent_t)a[0]->prof_end, st));
     return EFD_OK;
+}
+
+int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspace,
+                          const size_t* workspace_bytes, int32_t count, void* stream) {
+    return sum_batch_impl("efd_modesum_sum_batch", a, workspace, workspace_bytes, count, nullptr,
+                          nullptr, nullptr, stream);
+}
+
+int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* workspace,
+                            const size_t* workspace_bytes, int32_t count, const double* d,
+                            const double* w, double* out, void* stream) {
+    if (!d || !w || !out) return fail(EFD_ERR_ARG, "efd_modesum_sum_loglike: NULL d, w or out");
+    return sum_batch_impl("efd_modesum_sum_loglike", a, workspace, workspace_bytes, count, d, w,
+                          out, stream);
 }
 
 int efd_modesum_status(const void* workspace, void* stream) {

@@ -11,10 +11,13 @@ noise_fn = FDutils.get_sensitivity, f_arr = frequency[frequency >= 0]):
                            channels and bins, skipping bin 0 when w[0][0] is NaN (:268)
   __call__ (:295-334)      parameter transform, transpose_params, `subset` batching
 
-What changes is where the work happens. Data and noise factor live on the device; each
-walker's template is reduced by efd_loglike (HIP) straight from the template buffer into its slot
-of a device result vector, so the batch costs one host synchronisation and the 2 x N_pos
-residual d - h w is never materialised. When the template is this package's
+What changes is where the work happens. Data and noise factor live on the device. On
+symmetric grids (FEW's own and the drivers' downsampled f_arr) the walkers' mode sums run a few
+at a time in one launch with the likelihood fused into the sum's epilogue
+(efd_modesum_sum_loglike): the templates are never written, each walker's logL lands in its slot
+of a device result vector, and the batch costs one host synchronisation. Otherwise (or with
+fused_likelihood = False) each walker's template is reduced by efd_loglike (HIP) straight from
+the template buffer, and the 2 x N_pos residual d - h w is never materialised. When the template is this package's
 get_fd_waveform_fromFD around a GenerateEMRIWaveform (the drivers' case), h+ and hx are written
 by efd_polarizations directly into one reusable [2][N_pos] buffer (the stream orders reuse), and
 non_zero_mask is folded into the template weight (w * mask) instead of zeroing h.
@@ -55,6 +58,11 @@ class Likelihood:
         # walkers whose templates are in flight at once in get_ll (WaveformPipeline slots);
         # one HIP stream each (the box exposes 4 hardware queues per process)
         self.num_streams = 4
+        # pipelined templates on symmetric grids: the walkers' mode sums run FUSED_GROUP at a
+        # time in one launch with the likelihood in its epilogue (efd_modesum_sum_loglike), so
+        # no template is written; False keeps one template buffer + efd_loglike per walker
+        self.fused_likelihood = True
+        self._fused = None
         self._specific_likelihood_setup()
 
     def _specific_likelihood_setup(self):
@@ -175,6 +183,9 @@ class Likelihood:
             for i in range(num_likes):
                 h = self._as_channels(h_all[i])
                 self._red.loglike(h, self._d, self._w, out=out[i:i + 1])
+        elif (getattr(tm, "can_pipeline", False) and self.fused_likelihood
+              and self._get_ll_fused(tm, params, args, kwargs, out)):
+            pass
         elif getattr(tm, "can_pipeline", False):
             # several walkers in flight: each pipeline slot has its own template buffer,
             # stream and reduction scratch; walker i's template and logL run on one slot's
@@ -203,6 +214,63 @@ class Likelihood:
         if self.use_gpu and self.return_cupy:
             return out
         return out.cpu().numpy()
+
+    # walkers per fused launch, and the fused path's WaveformPipeline slots (at least two
+    # groups): small groups keep the next walkers' preparation beside the current sum (one
+    # group of 8 waited for all 8 preparations: config 4 3,222 vs 3,977 logL/s unfused); 3 and
+    # 6 slots measured best (configs 4 / 5: 4,936 / 7,015 vs 4,122 / 3,545 unfused, same box)
+    FUSED_GROUP = 3
+    FUSED_SLOTS = 4
+
+    def _get_ll_fused(self, tm, params, args, kwargs, out):
+        """The pipelined path with the likelihood fused into the mode sum: each walker's upload
+        and preparation on a WaveformPipeline slot, then per group of FUSED_GROUP walkers one
+        efd_modesum_sum_loglike on a sum stream writing their log-likelihoods into out (the
+        templates never reach HBM). Slots are reused only after the sum that read them (an event
+        per group). Returns False, before queueing anything, when the template's grid is not
+        symmetric (the caller takes the per-walker path)."""
+        torch = self.torch
+        from .summation import WaveformPipeline, sum_batch_loglike
+        G = self.FUSED_GROUP
+        caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),
+                                  "create_waveform", None), "caustic", "uniform")
+        F = self._fused
+        ns = max(2 * G, self.FUSED_SLOTS)
+        if F is None or F["pipe"].caustic != caustic or F["pipe"].num_slots != ns:
+            F = self._fused = dict(pipe=WaveformPipeline(ns, caustic=caustic, device=self.device),
+                                   stream=torch.cuda.Stream(self.device), busy=[None] * ns)
+        P, s_sum = F["pipe"], F["stream"]
+        cur = torch.cuda.current_stream(self.device)
+        P.order_after_current()
+        s_sum.wait_stream(cur)
+        n = len(params)
+        for g0 in range(0, n, G):
+            used, jobs = [], []
+            for i in range(g0, min(n, g0 + G)):
+                j = P.next_slot()
+                if F["busy"][j] is not None:   # the slot's previous sum has read its workspace
+                    P.stream(j).wait_event(F["busy"][j])
+                try:
+                    slot = tm.submit(P, None, *params[i], *args, order=False, prepare_only=True,
+                                     **kwargs)
+                except ValueError:
+                    if i == 0:
+                        return False   # not a symmetric grid: nothing queued yet
+                    raise
+                used.append(slot)
+                jobs.append(P.job(slot))
+            for slot in used:
+                s_sum.wait_stream(P.stream(slot))
+            sum_batch_loglike(jobs, self._d, self._w_templ, out[g0:g0 + len(used)],
+                              stream=s_sum.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(s_sum)
+            for slot in used:
+                F["busy"][slot] = ev
+        s_sum.synchronize()
+        P.wait()   # device-side errors of every slot's workspace
+        cur.wait_stream(s_sum)
+        return True
 
     def _pipeline_for(self, tm):
         """The WaveformPipeline (self.num_streams slots) and per-slot buffers of get_ll."""

@@ -266,6 +266,45 @@ def sum_batch(jobs, stream=None, prof_events=(None, None)):
     return wss
 
 
+def sum_batch_loglike(jobs, d, w, out, stream=None):
+    """Mode sums of several prepared waveforms with the likelihood fused into the sum
+    (efd_modesum_sum_loglike): out[i] = -1/2 * 4 * sum |d - h_i w|^2 over both channels, h_i
+    the waveform's [h+, hx] over the f >= 0 bins, never written to HBM.
+
+    jobs: as sum_batch, every one on a symmetric grid with the same k0 (the likelihood's
+    f >= 0 start) and accumulate off. d: complex128 [2][nf - k0], w: float64 [2][nf - k0]
+    (contiguous, on the device), out: float64 [len(jobs)] on the device (written in stream
+    order, no host synchronisation).
+    """
+    import ctypes
+    torch = _torch()
+    jobs = list(jobs)
+    if not 1 <= len(jobs) <= _lib.EFD_BATCH_MAX:
+        raise ValueError(f"sum_batch_loglike takes 1..{_lib.EFD_BATCH_MAX} waveforms")
+    freq = jobs[0][1]["freq"]
+    nb = int(freq.numel()) - int(jobs[0][1].get("k0", 0))
+    if (d.dtype != torch.complex128 or tuple(d.shape) != (2, nb) or not d.is_contiguous()
+            or w.dtype != torch.float64 or tuple(w.shape) != (2, nb) or not w.is_contiguous()
+            or out.dtype != torch.float64 or out.numel() < len(jobs) or not out.is_contiguous()):
+        raise ValueError(f"sum_batch_loglike: d complex128 [2][{nb}], w float64 [2][{nb}] and "
+                         f"out float64 [>= {len(jobs)}], contiguous")
+    args, wss = [], []
+    for eng, kw in jobs:
+        a, ws = eng._args(**kw)
+        args.append(a)
+        wss.append(ws)
+    n = len(jobs)
+    pa = (ctypes.POINTER(_lib.ModesumArgs) * n)(*[ctypes.pointer(a) for a in args])
+    pw = (ctypes.c_void_p * n)(*[ws.data_ptr() for ws in wss])
+    pb = (ctypes.c_size_t * n)(*[ws.numel() for ws in wss])
+    lib = jobs[0][0].lib
+    st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
+    _lib.check(lib.efd_modesum_sum_loglike(pa, pw, pb, n, torch.view_as_real(d).data_ptr(),
+                                           w.data_ptr(), out.data_ptr(), st),
+               "efd_modesum_sum_loglike", lib)
+    return wss
+
+
 class WaveformPipeline:
     """Several FD waveforms in flight on one device.
 
@@ -304,7 +343,7 @@ class WaveformPipeline:
         return self.slots[slot]["stream"]
 
     def submit(self, host, freq, grid_symmetric, scale=1.0 + 0.0j, out=None, hp=None, hc=None,
-               k0=0, accumulate=False, order=True):
+               k0=0, accumulate=False, order=True, prepare_only=False):
         """Queue one waveform; returns its slot index.
 
         host: dict of host arrays t, amp (complex [nt][K]), phi_phi, phi_r, f_phi, f_r, m, n,
@@ -313,6 +352,8 @@ class WaveformPipeline:
         polarisations written by the mode sum itself). Follow-up work on the outputs belongs on
         `stream(slot)` (or after `wait()`). order=False skips making the slot wait for the
         current stream (the caller did it once for the batch: `order_after_current`).
+        prepare_only: upload and efd_modesum_prepare only; the slot keeps the sum's job
+        (`job(slot)`, for sum_batch / sum_batch_loglike on another stream after the slot's).
         """
         torch = _torch()
         i = self._next
@@ -325,10 +366,21 @@ class WaveformPipeline:
         inp = self._upload(sl, host)
         eng = sl["engine"]
         eng._workspace(inp.nt, inp.K, int(freq.numel()), freq.device, stream=st)
-        eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
-                   hp=hp, hc=hc, k0=k0)
+        if prepare_only:
+            eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
+                       hp=hp, hc=hc, k0=k0, phase="prepare")
+            sl["job"] = (eng, dict(inp=inp, freq=freq, out=out, grid_symmetric=grid_symmetric,
+                                   scale=scale, accumulate=accumulate, hp=hp, hc=hc, k0=k0))
+        else:
+            eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
+                       hp=hp, hc=hc, k0=k0)
+            sl["job"] = None
         sl["used"] = True
         return i
+
+    def job(self, slot):
+        """The sum job a prepare_only submit left on `slot` (engine, launch kwargs)."""
+        return self.slots[slot].get("job")
 
     def order_after_current(self):
         """Make every slot wait for the work queued so far on the current stream (once per
@@ -568,7 +620,7 @@ class FDInterpolatedModeSum:
 
     def submit_channels(self, pipeline, out, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr,
                         n_arr, M, p, e, dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j,
-                        f_phi=None, f_r=None, order=True):
+                        f_phi=None, f_r=None, order=True, prepare_only=False):
         """Queue [h+, hx] over f >= 0 into the rows of out (complex128 [2][nf - k0]) on a
         WaveformPipeline slot: no host synchronisation. Symmetric grids (FEW's own and the
         drivers' downsampled f_arr) get the polarisations from the mode sum itself; other grids
@@ -582,6 +634,12 @@ class FDInterpolatedModeSum:
                     m=m_arr, n=n_arr, ylm_p=ylm_p, ylm_m=ylm_m)
         freq, sym = self._grid(T, dt, f_arr)
         nf, k0 = int(freq.numel()), self._k0
+        if prepare_only:
+            # the sum (and the fused likelihood) come later from pipeline.job(slot)
+            if not sym:
+                raise ValueError("submit_channels(prepare_only=True) needs a symmetric grid")
+            return pipeline.submit(host, freq, True, scale, k0=k0, order=order,
+                                   prepare_only=True)
         if (out.dtype != torch.complex128 or tuple(out.shape) != (2, nf - k0)
                 or not out.is_contiguous()):
             raise ValueError(f"submit_channels: out must be contiguous complex128 [2][{nf - k0}]")

@@ -127,8 +127,10 @@ class FastSchwarzschildEccentricFlux:
     def submit_channels(self, pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0,
                         Phi_r0=0.0, dt=10.0, T=1.0, eps=1e-5, mode_selection=None,
                         include_minus_m=True, f_arr=None, extra_scale=1.0 + 0.0j, order=True,
-                        **kwargs):
-        """Queue [h+, hx] over f >= 0 into out on a WaveformPipeline slot (FD only)."""
+                        prepare_only=False, **kwargs):
+        """Queue [h+, hx] over f >= 0 into out on a WaveformPipeline slot (FD only).
+        prepare_only: queue the upload and preparation only and leave the sum's job on the slot
+        (out unused; Likelihood's fused batch path)."""
         if self.output_type != "fd":
             raise ValueError("submit_channels is the FD path")
         d = self.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
@@ -138,7 +140,7 @@ class FastSchwarzschildEccentricFlux:
         return self.create_waveform.submit_channels(
             pipeline, out, d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:], d["Phi_phi"],
             d["Phi_r"], d["m"], d["n"], M, d["p"], d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale,
-            f_phi=d["f_phi"], f_r=d["f_r"], order=order)
+            f_phi=d["f_phi"], f_r=d["f_r"], order=order, prepare_only=prepare_only)
 
     def time_series(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                     T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True,

@@ -140,6 +140,23 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
 int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspace,
                           const size_t* workspace_bytes, int32_t count, void* stream);
 
+/*
+ * efd_modesum_sum_batch with the Gaussian log-likelihood of each waveform fused into the mode
+ * sum's epilogue (Likelihood.get_ll over a batch of walkers, likelihood.py:246-274):
+ *   out[i] = -1/2 * 4 * sum_c sum_j | d[c][j] - h_c,i[j] * w[c][j] |^2,  c in {+, x},
+ *   j over the bins [k0, nf) of the symmetric grid (c = + is h+, c = x is hx, as the fused
+ *   polarisations would write them), d complex [2][nf - k0], w real [2][nf - k0]
+ * (efd_loglike's terms and rounding), without writing the templates: the registers that hold
+ * S(k), S(nf-1-k) feed the reduction, so h+/hx never go through HBM. Every a[i] needs
+ * grid_symmetric = 1, accumulate = 0 and the same k0; hp/hc/out of a[i] are still written when
+ * non-NULL. out: count device doubles. Per-tile partials live in each workspace; the final
+ * reduction has a fixed order (bitwise reproducible; equal to efd_loglike on the written
+ * templates to rounding). An extension for batched likelihood callers.
+ */
+int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* workspace,
+                            const size_t* workspace_bytes, int32_t count, const double* d,
+                            const double* w, double* out, void* stream);
+
 /* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
  * this workspace: a harmonic with more than 8 monotonic frequency runs, or |m| > 255 or
  * |n| > 1023 -> EFD_ERR_ARG; a tile dispatch-order entry out of range in the sum (its bins left

@@ -90,13 +90,19 @@ def test_emri_pe_likelihood_path(setup):
     walkers[1, 0] *= 1.0 + 1e-5
     walkers[2, 4] += 1e-3
     assert fd_gen.can_pipeline
-    ll = like(walkers, **kw)           # pipelined fused path (templates on 4 streams at once)
+    # default: the likelihood fused into the walkers' batched mode sum (no template written);
+    # the injection walker's residual is exactly 0 (same h, same rounding as efd_loglike)
+    llf = like(walkers, **kw)
+    assert llf[0] == 0.0
+    assert np.all(llf[1:] < 0.0)
+    like.fused_likelihood = False      # templates through a buffer + efd_loglike, 4 streams
+    ll = like(walkers, **kw)
     assert ll[0] == 0.0
-    assert np.all(ll[1:] < 0.0)
+    np.testing.assert_allclose(llf, ll, rtol=1e-12, atol=0.0)   # reduction order differs
     like.num_streams, like._pipe = 1, None   # one template in flight at a time: same values
     np.testing.assert_array_equal(like(walkers, **kw), ll)
 
-    # generic path (template returns channels) gives bitwise the same values
+    # generic path (template returns channels) gives bitwise the unfused values
     like_g = Likelihood(lambda *a, **k: fd_gen(*a, **k), 2, f_arr=f_arr, use_gpu=True)
     like_g.inject_signal(data_stream=sig, noise_fn=[get_sensitivity, get_sensitivity],
                          noise_kwargs=[{}, {}])
@@ -117,7 +123,45 @@ def test_emri_pe_likelihood_path(setup):
     like_nzg = Likelihood(lambda *a, **k: fd_nz(*a, **k), 2, f_arr=f_arr, use_gpu=True)
     like_nzg.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2,
                            noise_kwargs=[{}, {}])
+    np.testing.assert_allclose(like_nz.get_ll(walkers, **kw), like_nzg.get_ll(walkers, **kw),
+                               rtol=1e-12, atol=0.0)
+    like_nz.fused_likelihood = False
     np.testing.assert_array_equal(like_nz.get_ll(walkers, **kw), like_nzg.get_ll(walkers, **kw))
+
+
+def test_fused_likelihood_many_walkers(setup):
+    """More walkers than two fused groups (slot reuse across groups, a partial last group):
+    efd_modesum_sum_loglike's values equal the template-buffer path to 1e-12, repeat bitwise,
+    and the fused call rejects bad shapes host-side."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.summation import sum_batch_loglike
+    params, kw, gen, gen_list = setup
+    freq = gen_list.waveform_generator.create_waveform.frequency
+    pos = freq >= 0
+    fd_gen = get_fd_waveform_fromFD(gen_list, pos, DT)
+    sig = fd_gen(*params, **kw)
+    f_arr = freq[pos].cpu().numpy()
+    like = Likelihood(fd_gen, 2, f_arr=f_arr, use_gpu=True)
+    like.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2, noise_kwargs=[{}, {}])
+    rng = np.random.default_rng(5)
+    walkers = np.stack([params] * 19)
+    walkers[1:, 0] *= 1.0 + 1e-5 * rng.standard_normal(18)
+    walkers[1:, 4] += 1e-3 * rng.standard_normal(18)
+    walkers[1:, 11] += 0.1 * rng.standard_normal(18)
+    llf = like.get_ll(walkers, **kw)
+    assert llf[0] == 0.0 and np.all(llf[1:] < 0.0)
+    np.testing.assert_array_equal(like.get_ll(walkers, **kw), llf)
+    like.fused_likelihood = False
+    np.testing.assert_allclose(llf, like.get_ll(walkers, **kw), rtol=1e-12, atol=0.0)
+    # argument errors: wrong data shape (host-side ValueError), unprepared mix of grids (C ABI)
+    P = like._fused["pipe"]
+    jobs = [P.job(s) for s in range(2)]
+    out = torch.empty(2, dtype=torch.float64, device="cuda")
+    with pytest.raises(ValueError):
+        sum_batch_loglike(jobs, like._d[:, 1:].contiguous(), like._w_templ, out)
+    bad = [(jobs[0][0], dict(jobs[0][1], accumulate=True)), jobs[1]]
+    with pytest.raises(_lib.EFDError):
+        sum_batch_loglike(bad, like._d, like._w_templ, out)
 
 
 def test_spectrum_matches_oracle_through_api(setup):

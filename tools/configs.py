@@ -205,9 +205,14 @@ def _likelihood_setup(T, eps, downsample, nwalkers, seed=2601996):
     return few, like, walkers, kw, len(f_like)
 
 
-def config_like(name, T, eps, downsample, nwalkers, reps, slots=4):
+def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, group=None):
     few, like, walkers, kw, nbins = _likelihood_setup(T, eps, downsample, nwalkers)
     like.num_streams = slots
+    like.fused_likelihood = fused
+    if group:
+        like.FUSED_GROUP = group
+    if os.environ.get("FUSED_SLOTS"):
+        like.FUSED_SLOTS = int(os.environ["FUSED_SLOTS"])
     B = len(walkers)
     ll = like.get_ll(walkers, **kw)        # warm-up (also the correctness anchor: ll[0] == 0)
     _sync()
@@ -230,10 +235,17 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4):
             "host_upstream_ms_per_walker": cache.host_s / B * 1e3,
             "ll_truth": float(ll[0]), "ll_min": float(np.min(ll)),
             "ll_bitwise_repeatable": bool(np.array_equal(ll, ll2)), "streams": slots,
+            "fused_likelihood": fused,
             "device_note": "Likelihood.get_ll over the half-step batch with the host upstream "
-                           "memoised: per walker the FD template (input upload, mode sum with "
-                           "h+/hx straight into a slot's buffer) + efd_loglike on one of "
-                           f"{slots} streams (WaveformPipeline); one host sync per batch"}
+                           "memoised: " + (
+                               "per walker the input upload and preparation on a "
+                               "WaveformPipeline slot, per group of 8 walkers one mode-sum "
+                               "launch with the likelihood fused in (no template written)"
+                               if fused else
+                               "per walker the FD template (input upload, mode sum with h+/hx "
+                               "straight into a slot's buffer) + efd_loglike on one of "
+                               f"{slots} streams (WaveformPipeline)") +
+                           "; one host sync per batch"}
 
 
 def main():
@@ -242,6 +254,10 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--slots", type=int, default=4, help="WaveformPipeline slots (config 3) "
                     "and Likelihood.num_streams (configs 4, 5)")
+    ap.add_argument("--unfused", action="store_true", help="configs 4, 5: templates through "
+                    "a buffer + efd_loglike instead of the fused batched likelihood")
+    ap.add_argument("--fused-group", type=int, default=0, help="walkers per fused launch "
+                    "(Likelihood.FUSED_GROUP; 0 = its default)")
     args = ap.parse_args()
     which = set(args.only.split(","))
     out = []
@@ -254,12 +270,12 @@ def main():
     if "4" in which:
         out.append(config_like("config4: emri_pe nwalkers=16 ntemps=1 injectFD=1 template=fd "
                                "Tobs=2yr eps=1e-2 full grid", 2.0, 1e-2, None, 16, args.reps,
-                               args.slots))
+                               args.slots, not args.unfused, args.fused_group))
         print(json.dumps(out[-1]), flush=True)
     if "5" in which:
         out.append(config_like("config5: emri_pe downsample=100 Tobs=4yr eps=1e-2 "
                                "nwalkers=128 (1 GPU)", 4.0, 1e-2, 100, 128, args.reps,
-                               args.slots))
+                               args.slots, not args.unfused, args.fused_group))
         print(json.dumps(out[-1]), flush=True)
 
 
