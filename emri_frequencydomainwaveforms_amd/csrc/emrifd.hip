@@ -377,6 +377,11 @@ __global__ __launch_bounds__(256) void k_group(const int32_t* __restrict__ marr,
     __shared__ int red[32];
     __shared__ int wsum[2 * NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the call's header starts at zero (this is the preparation's first kernel; every later
+    // writer runs after it in stream order): no separate hipMemsetAsync per waveform
+    static_assert(sizeof(Header) == 8 * sizeof(unsigned long long), "header: 8 words");
+    if (tid < 8) reinterpret_cast<unsigned long long*>(hdr)[tid] = 0ull;
+    __syncthreads();
     // k_modesum's (sin, cos)(k pi/256) table, computed once per waveform here and copied into
     // each tile's LDS by LDS-DMA (cheaper than 512 sincospi per tile at small harmonic counts)
     if (sctab_g != nullptr)
@@ -3351,7 +3356,6 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     constexpr int skip = 0;
 #endif
     if (!(skip & 1)) {
-    HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(Header), st));
 
     // K0: (m, n) groups
     hipLaunchKernelGGL(k_group, dim3(1), dim3(256), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,

@@ -139,6 +139,7 @@ class ModeSumEngine:
         self.lib = _lib.load()
         self._ws = None
         self._ws_key = None
+        self._last_args = None
         self.last_contributions = None
 
     def _workspace(self, nt, K, nf, device, stream=None):
@@ -174,6 +175,7 @@ class ModeSumEngine:
         fn = {"all": "efd_modesum", "prepare": "efd_modesum_prepare",
               "sum": "efd_modesum_sum"}[phase]
         _lib.check(getattr(self.lib, fn)(a, ws.data_ptr(), ws.numel(), st), fn, self.lib)
+        self._last_args = a
         return ws
 
     def _args(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
@@ -252,6 +254,7 @@ def sum_batch(jobs, stream=None, prof_events=(None, None)):
         raise ValueError(f"sum_batch takes 1..{_lib.EFD_BATCH_MAX} waveforms")
     args, wss = [], []
     for i, (eng, kw) in enumerate(jobs):
+        kw = {k: v for k, v in kw.items() if k != "_args"}
         a, ws = eng._args(prof_events=prof_events if i == 0 else (None, None), **kw)
         args.append(a)
         wss.append(ws)
@@ -290,7 +293,12 @@ def sum_batch_loglike(jobs, d, w, out, stream=None):
                          f"out float64 [>= {len(jobs)}], contiguous")
     args, wss = [], []
     for eng, kw in jobs:
-        a, ws = eng._args(**kw)
+        kw = dict(kw)
+        a = kw.pop("_args", None)   # the prepare call's own struct (WaveformPipeline jobs)
+        if a is None:
+            a, ws = eng._args(**kw)
+        else:
+            ws = eng._ws
         args.append(a)
         wss.append(ws)
     n = len(jobs)
@@ -369,8 +377,10 @@ class WaveformPipeline:
         if prepare_only:
             eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
                        hp=hp, hc=hc, k0=k0, phase="prepare")
+            # the prepare call's argument struct is the sum's too (same fields, no events)
             sl["job"] = (eng, dict(inp=inp, freq=freq, out=out, grid_symmetric=grid_symmetric,
-                                   scale=scale, accumulate=accumulate, hp=hp, hc=hc, k0=k0))
+                                   scale=scale, accumulate=accumulate, hp=hp, hc=hc, k0=k0,
+                                   _args=eng._last_args))
         else:
             eng.launch(inp, freq, out, grid_symmetric, scale, accumulate, stream=st.cuda_stream,
                        hp=hp, hc=hc, k0=k0)

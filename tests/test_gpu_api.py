@@ -159,7 +159,8 @@ def test_fused_likelihood_many_walkers(setup):
     out = torch.empty(2, dtype=torch.float64, device="cuda")
     with pytest.raises(ValueError):
         sum_batch_loglike(jobs, like._d[:, 1:].contiguous(), like._w_templ, out)
-    bad = [(jobs[0][0], dict(jobs[0][1], accumulate=True)), jobs[1]]
+    kw0 = {k: v for k, v in jobs[0][1].items() if k != "_args"}   # rebuild the struct
+    bad = [(jobs[0][0], dict(kw0, accumulate=True)), jobs[1]]
     with pytest.raises(_lib.EFDError):
         sum_batch_loglike(bad, like._d, like._w_templ, out)
 

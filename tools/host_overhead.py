@@ -44,14 +44,19 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.reps
     # host time up to the batch's synchronisation: time the loop with the final wait stubbed
-    P = like._pipe
+    fused = getattr(like, "_fused", None)
+    P = fused["pipe"] if fused else like._pipe
     real_wait = P.wait
     P.wait = lambda: None
+    real_sync = torch.cuda.Stream.synchronize
+    if fused:   # the fused path also synchronises its sum stream
+        torch.cuda.Stream.synchronize = lambda self: None
     t0 = time.perf_counter()
     like.get_ll(walkers, **kw)
     host = time.perf_counter() - t0
     torch.cuda.synchronize()
     P.wait = real_wait
+    torch.cuda.Stream.synchronize = real_sync
     pr = cProfile.Profile()
     pr.enable()
     like.get_ll(walkers, **kw)
@@ -60,6 +65,7 @@ def main():
     pstats.Stats(pr, stream=s).sort_stats(os.environ.get("HO_SORT", "tottime")).print_stats(int(os.environ.get("HO_N", "18")))
     B = len(walkers)
     print(json.dumps({"config": args.config, "walkers": B, "slots": args.slots,
+                      "fused_likelihood": bool(fused),
                       "wall_ms_per_walker": wall / B * 1e3,
                       "host_ms_per_walker_before_sync": host / B * 1e3}))
     print(s.getvalue())
