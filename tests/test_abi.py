@@ -108,3 +108,37 @@ def test_argument_errors_are_host_side():
     assert lib.efd_modesum(ctypes.byref(a), fake, ctypes.c_size_t(1 << 40), None) == -1
     lib.efd_last_error(buf, 256)
     assert b"nt out of range" in buf.value
+
+
+def test_fused_loglike_argument_errors_are_host_side():
+    """efd_modesum_sum_loglike rejects, before any device work: NULL d/w/out, an asymmetric
+    grid, accumulate = 1, k0 outside [0, nf), and members that disagree on k0."""
+    lib = _lib.load()
+    fake = ctypes.c_void_p(16)
+    a = _lib.ModesumArgs()
+    for f in ("t", "phi_phi", "phi_r", "f_phi", "f_r", "amp", "m", "n", "ylm_p", "ylm_m", "freq"):
+        setattr(a, f, fake)
+    a.nt, a.K, a.caustic, a.scale_re, a.nf, a.k0 = 100, 30, 1, 1.0, 1001, 500
+    a.grid_symmetric = 1
+    b = _lib.ModesumArgs.from_buffer_copy(a)
+    buf = ctypes.create_string_buffer(256)
+    ws = (ctypes.c_void_p * 2)(16, 16)
+    nb = (ctypes.c_size_t * 2)(1 << 40, 1 << 40)
+
+    def call(x, y, d=fake, w=fake, out=fake):
+        pa = (ctypes.POINTER(_lib.ModesumArgs) * 2)(ctypes.pointer(x), ctypes.pointer(y))
+        rc = lib.efd_modesum_sum_loglike(pa, ws, nb, 2, d, w, out, None)
+        lib.efd_last_error(buf, 256)
+        return rc, buf.value
+
+    assert call(a, b, d=None)[0] == -1 and b"NULL d, w or out" in buf.value
+    assert call(a, b, out=None)[0] == -1
+    for field, bad, both in (("grid_symmetric", 0, True), ("accumulate", 1, True),
+                             ("k0", 1001, True), ("k0", 499, False)):
+        c = _lib.ModesumArgs.from_buffer_copy(b)
+        setattr(c, field, bad)
+        a2 = _lib.ModesumArgs.from_buffer_copy(a)
+        if both:   # (members that disagree fail the batch's agreement check first)
+            setattr(a2, field, bad)
+        rc, msg = call(a2, c)
+        assert rc == -1 and b"fused likelihood needs" in msg, (field, msg)
