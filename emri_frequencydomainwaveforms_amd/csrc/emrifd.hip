@@ -81,6 +81,15 @@ constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
 constexpr double INV_SQRT_3_2PI = 1.44720250911653531871; // sqrt(2 pi / 3)
+// EFD_VSCALE: the records' F'' coefficients also carry |KRH_1|^(1/4), so the fast path's square
+// is v = sqrt|KRH_1| / |y| instead of 1/|y|: rho's leading correction 1 + KRH_1 / y^2 becomes
+// 1 - v^2, one FMA (the K_{1/3} series constants below are rescaled to v)
+#ifndef EFD_VSCALE
+#define EFD_VSCALE 1
+#endif
+constexpr double VS = 0.18633899812498247470;             // sqrt|KRH_1|
+constexpr double FDD_SCALE = EFD_VSCALE ? 0.29827892638794838654 : SQRT_3_2PI;
+constexpr double INV_FDD_SCALE = EFD_VSCALE ? 3.3525667136785156343 : INV_SQRT_3_2PI;
 
 // Fast-path series length: FAST_J terms of each of R and I/w, exact (truncation < 1e-17) for
 // |y| >= FAST_Y (J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48); lanes below FAST_Y take the general
@@ -1007,9 +1016,9 @@ __device__ void build_item(
         const double G1 = dm * ct[1 * 8 + 4] + dn * ct[1 * 8 + 5];
         const double G2 = dm * ct[2 * 8 + 4] + dn * ct[2 * 8 + 5];
         // pre-scaled so the fast path's w = 3 F''^2 / (2 pi |F'|^3) is one square
-        it.fdd[0] = SQRT_3_2PI * (3.0 * G0);
-        it.fdd[1] = SQRT_3_2PI * (2.0 * G1);
-        it.fdd[2] = SQRT_3_2PI * G2;
+        it.fdd[0] = FDD_SCALE * (3.0 * G0);
+        it.fdd[1] = FDD_SCALE * (2.0 * G1);
+        it.fdd[2] = FDD_SCALE * G2;
         // lower bound of |y| = 2 pi |F'|^3 / (3 F''^2) over w in [0, dtj]: min |F'| and max |F''|
         // of the two quadratics from their end points and vertices (F' changing sign -> 0)
         const double dt = it.dtj;
@@ -1775,7 +1784,7 @@ __device__ __forceinline__ RecSign rec_sign(bool fdneg) {
     RecSign r;
     r.fdcls = fdneg ? 0x018 : 0x180;
     r.shift = fdneg ? -192 : 192;
-    r.kth = fdneg ? -KTH0 : KTH0;
+    r.kth = EFD_VSCALE ? (fdneg ? -KTH0 / VS : KTH0 / VS) : (fdneg ? -KTH0 : KTH0);
     return r;
 }
 // lanes where v_cmp_class_f64(x, cls) holds, as a wave mask
@@ -1801,6 +1810,9 @@ __device__ __forceinline__ double ftz_select(bool ok, double v) {
 }
 #ifndef EFD_EARLY_MASK
 #define EFD_EARLY_MASK 1
+#endif
+#if EFD_VSCALE && !(EFD_EARLY_MASK && EFD_SALU_MASKS && EFD_REC_SIGN)
+#error "EFD_VSCALE: the early-mask, SALU-mask, record-sign fast path only"
 #endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
@@ -1849,17 +1861,31 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
             // the |y| >= FAST_Y test only matters for J = 4 (J = 3 lanes pass it by their
             // record's bound), but a nested J test's condition crossed the join as a per-lane
             // boolean (v_cndmask + v_cmp for every record)
-            goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
-            ww = fmin(ww, 1.0);
             // |w| <= 1/153: rho's KRH_3 term (< 2.2e-14) and theta's KTHN_2 term (< 1.3e-12 rad)
             // are below the accuracy of the rest of the evaluation
+#if EFD_VSCALE
+            // ww = v = VS w: rho = 1 - v^2 + (KRH_2 / KRH_1^2) v^4, theta / (TH_0 / VS) =
+            // v (1 + (KTHN_1 / |KRH_1|) v^2)
+            goodm &= __builtin_amdgcn_ballot_w64(ww <= VS / FAST_Y);
+            ww = fmin(ww, 1.0);
+            const double uu = ww * ww;
+            const double r = fma(45.7, uu * uu, 1.0 - uu);
+            thn = ww * fma(-14.733333333333333333, uu, 1.0);
+#else
+            goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
+            ww = fmin(ww, 1.0);
             const double uu = ww * ww;
             const double r = fma(KRH[2], uu * uu, fma(KRH[1], uu, 1.0));
             thn = ww * fma(KTHN[1], uu, 1.0);
+#endif
             am = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm & goodm), ampm * r);
             c0 = 1.0;
         } else {
+#if EFD_VSCALE
+            c0 = fma(-ww, ww, 1.0);   // 1 + KRH_1 w^2 = 1 - v^2
+#else
             c0 = fma(KRH[1], ww * ww, 1.0);
+#endif
             thn = ww;
             am = ampm;
         }
@@ -1946,7 +1972,7 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
         for (int q = 0; q < 4; ++q) c.b[q] = cubic(it->b[q >> 1][q & 1], w);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-        fdd = INV_SQRT_3_2PI * fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+        fdd = INV_FDD_SCALE * fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
     } else {  // t(g) overshot the record's knot interval: evaluate like scipy
 #ifdef EFD_EXP_COUNT
         atomicAdd(&g_exp_count[4], 1ull);
