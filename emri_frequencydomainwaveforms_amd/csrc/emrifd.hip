@@ -3308,6 +3308,19 @@ static int64_t resident_tile_slots() {
     return v;
 }
 
+// Longest-first dispatch (k_tile_order) for one waveform: only when its tiles outnumber the
+// resident slots and it has at least ORDER_MIN_K harmonics. With few harmonics the tiles' record
+// lists are short and even, and the sort's ~9 us on the preparation chain cost more than the
+// order saved: configs 1 and 3 (tens of harmonics, 3,082 tiles) ran 7% faster without it
+// (2,147 / 2,122 vs 2,023 / 1,944 and 8,182 / 8,231 vs 7,777 / 7,410 waveforms/s, two rounds),
+// while config 2 (3,020 harmonics) keeps +0.2% (paired A/B, ratio 1.002, CI 1.001-1.003).
+// prepare and sum see the same arguments, so they agree on whether tperm exists.
+constexpr int32_t ORDER_MIN_K = 1024;
+static bool use_cost_order(const Layout& L, int32_t K) {
+    return EFD_PREBUILT_LISTS && EFD_COST_ORDER && K >= ORDER_MIN_K &&
+           L.ntiles > resident_tile_slots();
+}
+
 // argument checks of efd_modesum / _prepare / _sum (phase as in modesum_impl)
 static int check_modesum_args(const efd_modesum_args* a, const void* workspace, int phase) {
     if (!a || !workspace) return fail(EFD_ERR_ARG, "efd_modesum: NULL argument");
@@ -3445,7 +3458,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
                            seginfo, nseg, segbase, stb0, stb1, L.ntiles, tkeys, tcnt);
         HIP_TRY(hipGetLastError());
 #if EFD_COST_ORDER
-        if (L.ntiles > resident_tile_slots() && !(skip & 32)) {
+        if (use_cost_order(L, K) && !(skip & 32)) {
             hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
                                (int32_t*)(ws + L.tperm));
             HIP_TRY(hipGetLastError());
@@ -3462,7 +3475,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
         int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
         const int32_t* tperm =
-            (EFD_PREBUILT_LISTS && EFD_COST_ORDER && L.ntiles > resident_tile_slots())
+            use_cost_order(L, K)
                 ? (const int32_t*)(ws + L.tperm) : nullptr;
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum<P, C, BPL>), grid, block, 0, st, items, ranges, seglh,          \
@@ -3545,7 +3558,7 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         d.sctab = (const double2*)(ws + L.sctab);
         d.tkeys = (const uint32_t*)(ws + L.tkeys);
         d.tcnt = EFD_PREBUILT_LISTS ? (const int32_t*)(ws + L.tcnt) : nullptr;
-        d.tperm = (EFD_PREBUILT_LISTS && EFD_COST_ORDER && L.ntiles > resident_tile_slots())
+        d.tperm = use_cost_order(L, ai->K)
                       ? (const int32_t*)(ws + L.tperm) : nullptr;
         d.segbase = (const int32_t*)(ws + L.segbase);
         d.stb0 = (const int32_t*)(ws + L.stb0);
