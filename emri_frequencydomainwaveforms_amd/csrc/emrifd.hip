@@ -1866,8 +1866,11 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
 #if EFD_VSCALE
             // ww = v = VS w: rho = 1 - v^2 + (KRH_2 / KRH_1^2) v^4, theta / (TH_0 / VS) =
             // v (1 + (KTHN_1 / |KRH_1|) v^2)
-            goodm &= __builtin_amdgcn_ballot_w64(ww <= VS / FAST_Y);
-            ww = fmin(ww, 1.0);
+            // lanes past the series' range get w = +0 (high word cleared, flushed): finite
+            // angle, masked amplitude below; one v_cndmask instead of fmin's max + min
+            const uint64_t inrange = __builtin_amdgcn_ballot_w64(ww <= VS / FAST_Y);
+            goodm &= inrange;
+            ww = ftz_select(__builtin_amdgcn_inverse_ballot_w64(inrange), ww);
             const double uu = ww * ww;
             const double r = fma(45.7, uu * uu, 1.0 - uu);
             thn = ww * fma(-14.733333333333333333, uu, 1.0);
