@@ -3319,8 +3319,14 @@ static int64_t resident_tile_slots() {
 // while config 2 (3,020 harmonics) keeps +0.2% (paired A/B, ratio 1.002, CI 1.001-1.003).
 // prepare and sum see the same arguments, so they agree on whether tperm exists.
 constexpr int32_t ORDER_MIN_K = 1024;
+// Prebuilt tile lists (k_tile_keys) from EFD_LISTS_MIN_K harmonics up; below, the sum builds
+// them itself (short lists: one window pass per tile)
+#ifndef EFD_LISTS_MIN_K
+#define EFD_LISTS_MIN_K 0
+#endif
+static bool use_prebuilt(int32_t K) { return EFD_PREBUILT_LISTS && K >= EFD_LISTS_MIN_K; }
 static bool use_cost_order(const Layout& L, int32_t K) {
-    return EFD_PREBUILT_LISTS && EFD_COST_ORDER && K >= ORDER_MIN_K &&
+    return use_prebuilt(K) && EFD_COST_ORDER && K >= ORDER_MIN_K &&
            L.ntiles > resident_tile_slots();
 }
 
@@ -3456,7 +3462,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     // pipeline
     {
         const dim3 block(TILE);
-        if (!(skip & 16))
+        if (!(skip & 16) && use_prebuilt(K))
         hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)L.ntiles), block, 0, st, ranges, seglh,
                            seginfo, nseg, segbase, stb0, stb1, L.ntiles, tkeys, tcnt);
         HIP_TRY(hipGetLastError());
@@ -3476,7 +3482,7 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
         const dim3 grid((unsigned)((L.ntiles + gq - 1) / gq * gq)), block(TILE);
         const int acc = a->accumulate ? 1 : 0;
         if (a->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->prof_begin, st));
-        int32_t* tcnt_sum = EFD_PREBUILT_LISTS ? tcnt : nullptr;
+        int32_t* tcnt_sum = use_prebuilt(K) ? tcnt : nullptr;
         const int32_t* tperm =
             use_cost_order(L, K)
                 ? (const int32_t*)(ws + L.tperm) : nullptr;
@@ -3560,7 +3566,7 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         d.coefT = (const double*)(ws + L.coefT);
         d.sctab = (const double2*)(ws + L.sctab);
         d.tkeys = (const uint32_t*)(ws + L.tkeys);
-        d.tcnt = EFD_PREBUILT_LISTS ? (const int32_t*)(ws + L.tcnt) : nullptr;
+        d.tcnt = use_prebuilt(ai->K) ? (const int32_t*)(ws + L.tcnt) : nullptr;
         d.tperm = use_cost_order(L, ai->K)
                       ? (const int32_t*)(ws + L.tperm) : nullptr;
         d.segbase = (const int32_t*)(ws + L.segbase);
