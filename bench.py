@@ -23,15 +23,19 @@ emri_pe.py shards with no data-path exchange: weak scaling); value = all ranks' 
 max over ranks of the timed region.
 
 roofline: the mode-sum kernel (k_modesum_batch, or k_modesum at --batch 1) timed with HIP events
-recorded on its own stream around each launch in the timed region; t = launch time / B per
-waveform; achieved = B * B_alg per launch / launch time, B_alg = 32 C + 32 n_interp N_t + 16 N_f
-(32 B per SPA contribution of the reference's scatter formulation),
-peak 8.0 TB/s (MI355X_MICROARCH.md). traffic: HBM bytes per launch from the committed rocprofv3
-PMC pass (profiles/) when it was taken at the same batch, or null.
+recorded on its own stream around each launch in the timed region. The kernel is bound by the
+FP64 vector ALU (output-stationary: each bin written once, ~0.27 GB of HBM traffic per
+waveform), so bound = "fp64_valu": achieved = FP64 FLOP per launch (rocprofv3 PMC counters of
+the committed profile, per SPA evaluation, times this run's evaluations) / launch time, peak
+78.6 TFLOP/s. traffic: HBM bytes per launch from the same PMC pass. SURVEY.md section 8d's
+scatter-formulation bytes (32 B per SPA contribution) are reported as scatter_equiv_gbs, a
+secondary figure: the kernel never issues that traffic.
 
-cpu_baseline: the oracle's C restatement (oracle/fd_oracle_c.c, OpenMP, kind "port") timed on a
-bounded sample of the same workload (a subset of its harmonics) on this host, extrapolated to
-waveforms/s through the contribution count; rank 0 at N = 1 only.
+cpu_baseline: the host twin efd_modesum_cpu (the same algorithm in C++17 + OpenMP, kind "twin")
+on this host: all cores on full waveforms, and 1 thread on a subset of harmonics extrapolated by
+SPA evaluation count (single_thread). cpu_reference: the oracle's C restatement (per harmonic
+and bin, the notebook's construction; the checker) on a subset, extrapolated by contribution
+count. Rank 0 at N = 1 only.
 """
 
 import argparse
@@ -76,16 +80,103 @@ def build_workload(T=2.0, dt=10.0, eps=1e-5, M=1e6, mu=10.0, e0=0.35, theta=np.p
                 params=dict(M=M, mu=mu, p0=float(p0), e0=e0, T=T, dt=dt, eps=eps))
 
 
-def cpu_baseline(w, seconds=15.0):
-    """Time the C oracle on a growing subset of harmonics until ~`seconds` of CPU work."""
+def fp64_roofline(B, n_eval, kern_ms, caustic):
+    """FP64 VALU roofline of the mode-sum kernel: FLOP per launch from the committed rocprofv3
+    PMC pass (profiles/pmc_traffic.json, written by tools/summarize_profiles.py: FP64 FMA counts
+    2, MUL/ADD/TRANS 1, times 64 lanes x measured lane utilisation), taken per SPA evaluation and
+    scaled to this run's evaluation count, over this run's kernel time, against the 78.6 TFLOP/s
+    vector FP64 peak. traffic: HBM bytes per launch of the same PMC pass (2 FETCH_SIZE +
+    WRITE_SIZE, gfx950 correction)."""
+    import hashlib
+    out = {"bound": "fp64_valu", "achieved": None, "peak": FP64_VALU_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": None, "traffic": None}
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(prof):
+        return out
+    try:
+        pj = json.load(open(prof))
+        f = pj.get("fp64") or {}
+        fpe = f.get("flops_per_evaluation")
+        if fpe is None and f.get("flops_per_launch") and pj.get("evaluations_per_launch"):
+            fpe = f["flops_per_launch"] / pj["evaluations_per_launch"]
+        if fpe is None or pj.get("caustic") != caustic:
+            return out
+        src = os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc", "emrifd.hip")
+        sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+        flops = fpe * n_eval * B
+        tf = flops / (kern_ms * 1e-3) / 1e12
+        out.update(achieved=tf, frac=tf / FP64_VALU_PEAK_TFLOPS,
+                   flops_per_launch=flops, flops_per_evaluation=fpe,
+                   valu_busy=f.get("valu_busy"),
+                   pmc_source=pj.get("source"), pmc_matches_build=pj.get("src_sha16") == sha)
+        if int(pj.get("batch", 1)) == B and pj.get("workload") == "config2":
+            out["traffic"] = pj.get("hbm_bytes_per_launch")
+    except (ValueError, OSError, KeyError, TypeError):
+        pass
+    return out
+
+
+def cpu_baseline(w, seconds=10.0):
+    """The host twin (efd_modesum_cpu: the same algorithm as the HIP path in C++17 + OpenMP,
+    AVX-512) timed on this box's host cores: all cores on the full waveform (1 warm-up + 3 timed,
+    median), and 1 thread on a subset of harmonics sized to ~`seconds`, extrapolated by SPA
+    evaluation count (the twin's cost is per evaluation). SURVEY.md section 8(d)."""
+    from emri_frequencydomainwaveforms_amd import cputwin
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+
+    def run(sel):
+        return cputwin.modesum(w["t"], w["amp"][:, sel], w["phi_phi"], w["phi_r"], w["f_phi"],
+                               w["f_r"], w["m"][sel], w["n"][sel], w["ylm_p"][sel],
+                               w["ylm_m"][sel], w["freq"], w["prefactor"])
+    allh = np.arange(len(w["m"]))
+    prev = cputwin.set_threads(threads)
+    try:
+        run(allh)
+        _, ev_all, _ = cputwin.stats()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            run(allh)
+            ts.append(time.perf_counter() - t0)
+        t_all = float(np.median(ts))
+        cputwin.set_threads(1)
+        order = np.argsort(-np.abs(w["amp"]).max(axis=0))   # strongest harmonics first
+        k = 16
+        while True:
+            sel = np.sort(order[:k])
+            t0 = time.perf_counter()
+            run(sel)
+            dt = time.perf_counter() - t0
+            _, ev_s, _ = cputwin.stats()
+            if dt > 0.5 * seconds or k >= len(order):
+                break
+            k = min(len(order), int(k * max(2.0, 0.8 * seconds / max(dt, 1e-3))))
+    finally:
+        cputwin.set_threads(prev)
+    one = ev_s / dt / ev_all
+    return {"value": 1.0 / t_all, "unit": "waveforms/s", "cores": threads, "kind": "twin",
+            "sample": f"full config-2 waveform (3,020 harmonics, {ev_all} SPA evaluations), "
+                      f"median of 3 after a warm-up, {t_all:.3f} s each on {threads} threads",
+            "single_thread": {"value": one, "unit": "waveforms/s", "cores": 1,
+                              "sample": f"{k} of {len(order)} harmonics ({ev_s} of {ev_all} SPA "
+                                        f"evaluations) in {dt:.1f} s on 1 thread, extrapolated "
+                                        f"by evaluation count"},
+            "implementation": "efd_modesum_cpu (csrc/emrifd_cpu.cpp): the HIP path's algorithm "
+                              "on the host, C++17 + OpenMP, -O3 -march=x86-64-v4"}
+
+
+def cpu_reference(w, seconds=5.0):
+    """The oracle's C restatement (oracle/fd_oracle_c.c: per harmonic, per bin, the reference
+    notebook's construction) on a bounded subset of harmonics, extrapolated by contribution count:
+    the checker, timed for reference (it is not the same algorithm as the twin)."""
     from oracle import fd_oracle, fd_oracle_c
-    lib = fd_oracle_c.load()
-    if lib is None:
+    if fd_oracle_c.load() is None:
         return None
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     C_total = fd_oracle.contributions(w["t"], w["f_phi"], w["f_r"], w["m"], w["n"], w["freq"])
-    order = np.argsort(-np.abs(w["amp"]).max(axis=0))   # strongest harmonics first (typical mix)
+    order = np.argsort(-np.abs(w["amp"]).max(axis=0))
     k = 8
     while True:
         sel = order[:k]
@@ -96,14 +187,12 @@ def cpu_baseline(w, seconds=15.0):
                             w["f_r"], w["m"][sel], w["n"][sel], w["ylm_p"][sel], w["ylm_m"][sel],
                             w["freq"], w["prefactor"], caustic="uniform", nthreads=threads)
         dt = time.perf_counter() - t0
-        if dt > 0.6 * seconds or k >= len(order):
+        if dt > 0.5 * seconds or k >= len(order):
             break
-        k = min(len(order), int(k * max(2.0, 0.7 * seconds / max(dt, 1e-3))))
-    rate = C_s / dt                                    # contributions per second
-    return {"value": rate / C_total, "unit": "waveforms/s", "cores": threads, "kind": "port",
-            "sample": f"{k} of {len(order)} harmonics of config 2 ({C_s} of {C_total} SPA "
-                      f"contributions) in {dt:.1f} s on {threads} threads, extrapolated by "
-                      f"contribution count"}
+        k = min(len(order), int(k * max(2.0, 0.8 * seconds / max(dt, 1e-3))))
+    return {"value": C_s / dt / C_total, "unit": "waveforms/s", "cores": threads, "kind": "port",
+            "sample": f"{k} of {len(order)} harmonics ({C_s} of {C_total} contributions) in "
+                      f"{dt:.1f} s on {threads} threads, extrapolated by contribution count"}
 
 
 def main():
@@ -114,7 +203,7 @@ def main():
     ap.add_argument("--caustic", default="uniform", choices=["uniform", "spa"])
     ap.add_argument("--T", type=float, default=2.0)
     ap.add_argument("--eps", type=float, default=1e-5)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pipeline", default="overlap", choices=["overlap", "serial"],
                     help="overlap: prepare(i+1) on a second stream beside sum(i), fused h+/hx; "
@@ -257,32 +346,21 @@ def main():
         n_interp = 2 * K + 4
         b_alg = 32.0 * C + 32.0 * n_interp * nt + 16.0 * nf
         wf_ms = kern_ms / B   # one launch sums B waveforms
-        achieved = B * b_alg / (kern_ms * 1e-3) / 1e9   # algorithmic bytes per launch / launch
-        traffic = None
-        fp64 = None
-        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(prof):
-            try:
-                pj = json.load(open(prof))
-                if (pj.get("workload") == "config2" and pj.get("caustic") == args.caustic
-                        and int(pj.get("batch", 1)) == B):
-                    traffic = pj.get("hbm_bytes_per_launch")
-                    f = pj.get("fp64")
-                    if f:
-                        tf = f["flops_per_launch"] / (kern_ms * 1e-3) / 1e12
-                        fp64 = {"achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                "frac": tf / FP64_VALU_PEAK_TFLOPS,
-                                "valu_busy": f["valu_busy"],
-                                "source": "FP64 VALU lane ops per launch from the committed "
-                                          "rocprofv3 PMC pass / this run's kernel_ms"}
-            except (ValueError, OSError, KeyError):
-                traffic = None
+        # SURVEY 8(d)'s scatter-formulation bytes: a secondary figure, never the roofline (the
+        # output-stationary kernel never makes those accesses, so it exceeds HBM "peak")
+        scatter_gbs = B * b_alg / (kern_ms * 1e-3) / 1e9
+        roof = fp64_roofline(B, n_eval, kern_ms, args.caustic)
         cpu = None
+        cpu = cpu_ref = None
         if world == 1 and not args.no_cpu_baseline:
             try:
                 cpu = cpu_baseline(w, seconds=args.cpu_seconds)
             except Exception as exc:  # the baseline must not kill the GPU measurement
                 cpu = {"value": None, "error": repr(exc)}
+            try:
+                cpu_ref = cpu_reference(w)
+            except Exception as exc:
+                cpu_ref = {"value": None, "error": repr(exc)}
         value = world * args.steps * B / elapsed
         line = {
             "metric": METRIC,
@@ -306,18 +384,22 @@ def main():
                        "pipeline": args.pipeline + (" (diagnostic: sum only)"
                                                     if args.diag_sum_only else ""),
                        "slots": len(slots), "sum_streams": len(s_sums), "batch": B},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_alg_per_launch": B * b_alg, "waveforms_per_launch": B,
-                         "kernel": "k_modesum_batch" if B > 1 else "k_modesum",
-                         "kernel_ms": kern_ms, "kernel_ms_per_waveform": wf_ms,
-                         "kernel_timing": "HIP events around each k_modesum launch in the timed "
-                                          "region (sum stream), mean",
-                         "contributions_per_s": C / (wf_ms * 1e-3),
-                         "sum_gap_ms": gap_ms,
-                         "sum_gap_ms_min_max": [min(gaps, default=0.0), max(gaps, default=0.0)],
-                         "fp64_valu": fp64},
+            "roofline": dict(roof, **{
+                "kernel": "k_modesum_batch" if B > 1 else "k_modesum",
+                "kernel_ms": kern_ms, "kernel_ms_per_waveform": wf_ms,
+                "waveforms_per_launch": B,
+                "kernel_timing": "HIP events around each k_modesum launch in the timed region "
+                                 "(sum stream), mean",
+                "spa_evaluations_per_s": n_eval / (wf_ms * 1e-3),
+                "contributions_per_s": C / (wf_ms * 1e-3),
+                "scatter_equiv_gbs": scatter_gbs,
+                "scatter_equiv_note": "SURVEY 8(d) B_alg = 32 C + 32 n_interp N_t + 16 N_f per "
+                                      "waveform / kernel time: the reference scatter "
+                                      "formulation's traffic, which this kernel never issues "
+                                      "(not an HBM roofline)",
+                "sum_gap_ms": gap_ms}),
             "cpu_baseline": cpu,
+            "cpu_reference": cpu_ref,
         }
         print(json.dumps(line))
     if world > 1:

@@ -1,24 +1,44 @@
-"""Build libemrifd.so in-tree with hipcc for gfx950 (no JIT cache, so the .so travels)."""
+"""Build libemrifd.so in-tree (no JIT cache, so the .so travels with the repo snapshot):
 
+  csrc/emrifd_cpu.cpp -> g++ -O3 -march=x86-64-v4 -fopenmp (the host twin, efd_*_cpu; AVX-512 is
+                         on both this container's Sapphire Rapids and the GPU box's EPYC 9575F)
+  csrc/emrifd.hip     -> hipcc --offload-arch=gfx950, linked with the twin's object and libgomp
+"""
+
+import glob
 import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "emrifd.hip")
+CSRC = os.path.join(HERE, "csrc")
+SRC = os.path.join(CSRC, "emrifd.hip")
+CPU_SRC = os.path.join(CSRC, "emrifd_cpu.cpp")
 OUT = os.path.join(HERE, "libemrifd.so")
+OBJDIR = os.path.join(HERE, "build")
 ARCH = os.environ.get("EFD_OFFLOAD_ARCH", "gfx950")
+CPU_ARCH = os.environ.get("EFD_CPU_ARCH", "x86-64-v4")
 
 
-def build(force=False, verbose=False):
-    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= os.path.getmtime(SRC):
-        hdr = os.path.join(os.path.dirname(HERE), "include", "emrifd.h")
-        if not os.path.exists(hdr) or os.path.getmtime(OUT) >= os.path.getmtime(hdr):
+def _inputs():
+    hdr = os.path.join(os.path.dirname(HERE), "include", "emrifd.h")
+    return [SRC, CPU_SRC, hdr] + glob.glob(os.path.join(CSRC, "*.inc"))
+
+
+def build(force=False, verbose=False, extra=()):
+    if not force and os.path.exists(OUT):
+        t = os.path.getmtime(OUT)
+        if all(os.path.getmtime(p) <= t for p in _inputs() if os.path.exists(p)):
             return OUT
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", OUT + ".tmp", SRC]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    os.makedirs(OBJDIR, exist_ok=True)
+    obj = os.path.join(OBJDIR, "emrifd_cpu.o")
+    cpu = ["g++", "-O3", f"-march={CPU_ARCH}", "-fopenmp", "-ffp-contract=off", "-fPIC",
+           "-std=c++17", "-c", CPU_SRC, "-o", obj]
+    hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *extra,
+           "-o", OUT + ".tmp", obj, SRC, "-lgomp"]
+    for cmd in (cpu, hip):
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -40,6 +40,14 @@ EXPORTED_SYMBOLS = (
     "efd_polarizations",
     "efd_loglike",
     "efd_inner_product",
+    "efd_modesum_cpu",
+    "efd_modesum_cpu_stats",
+    "efd_spline_build_cpu",
+    "efd_polarizations_cpu",
+    "efd_loglike_cpu",
+    "efd_inner_product_cpu",
+    "efd_cpu_threads",
+    "efd_cpu_last_error",
 )
 
 
@@ -173,6 +181,24 @@ def load(path=None):
     lib.efd_loglike.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
     lib.efd_inner_product.restype = ctypes.c_int
     lib.efd_inner_product.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
+    if hasattr(lib, "efd_modesum_cpu"):   # the host twins (csrc/emrifd_cpu.cpp)
+        lib.efd_modesum_cpu.restype = ctypes.c_int
+        lib.efd_modesum_cpu.argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
+        lib.efd_modesum_cpu_stats.restype = ctypes.c_int
+        lib.efd_modesum_cpu_stats.argtypes = [ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                              ctypes.POINTER(i32)]
+        lib.efd_spline_build_cpu.restype = ctypes.c_int
+        lib.efd_spline_build_cpu.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
+        lib.efd_polarizations_cpu.restype = ctypes.c_int
+        lib.efd_polarizations_cpu.argtypes = [vp, i64, i64, vp, vp, vp]
+        lib.efd_loglike_cpu.restype = ctypes.c_int
+        lib.efd_loglike_cpu.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
+        lib.efd_inner_product_cpu.restype = ctypes.c_int
+        lib.efd_inner_product_cpu.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
+        lib.efd_cpu_threads.restype = ctypes.c_int
+        lib.efd_cpu_threads.argtypes = [ctypes.c_int]
+        lib.efd_cpu_last_error.restype = ctypes.c_int
+        lib.efd_cpu_last_error.argtypes = [ctypes.c_char_p, ctypes.c_int]
     _ = dbl
     if path is None:
         _lib = lib

@@ -102,7 +102,8 @@ constexpr double FAST_Y = FAST_J <= 3 ? 555.0 : FAST_J == 4 ? 153.0 : FAST_J == 
 static_assert(FAST_J >= 3 && FAST_J <= 6, "fast-path series: 3..6 terms");
 // Truncation after J terms is KB[J] w^(2J) < 1e-17 for |y| >= JSER_Y[J]; k_items picks the
 // smallest J whose bound holds on the whole interval (a lower bound of |y| there).
-__constant__ double JSER_Y[7] = {0.0, 6.0e7, 8.7e3, 570.0, 153.0, 75.0, 48.0};
+#define EFD_TABLE __constant__
+#include "spa_tables.inc"
 
 thread_local std::string g_err;
 
@@ -154,6 +155,12 @@ static_assert(offsetof(Item, b) % 16 == 0 && sizeof(Item::b) == 8 * 16, "b: 8 wh
 constexpr int ROUNDS = EFD_STAGE_ROUNDS;         // 16-B pieces per thread per LDS stage
 constexpr int NC = (ROUNDS * TILE) / PIECES;     // records per LDS stage
 
+// The error flags (runs_overflow, bad_mn, bad_tile) are sticky: k_group clears only the counters
+// of a header it has initialised before (magic == HDR_MAGIC), so an error raised by any call on
+// this workspace survives later preparations until efd_modesum_status reports and clears it (a
+// pipeline slot reused by several walkers before its status is read loses none of them). A
+// header without the magic (fresh device memory) is zeroed whole.
+constexpr int64_t HDR_MAGIC = 0x45464448445233LL;   // "EFDHDR3"
 struct Header {
     int64_t contributions;      // C of the last call: (l, m, n) branch x bin pairs (k_items)
     int64_t evaluations;        // SPA evaluations: (m, n) group branch x bin pairs
@@ -161,7 +168,8 @@ struct Header {
     int32_t groups;             // G: distinct (m, n) of the call (k_group)
     int32_t bad_mn;             // set by k_group when |m| > 255 or |n| > 1023
     int32_t bad_tile;           // set by k_modesum when a dispatch-order entry is out of range
-    int64_t pad[4];             // 64 B
+    int64_t magic;              // HDR_MAGIC once k_group has initialised the header
+    int64_t pad[3];             // 64 B
 };
 static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
@@ -386,10 +394,22 @@ __global__ __launch_bounds__(256) void k_group(const int32_t* __restrict__ marr,
     __shared__ int red[32];
     __shared__ int wsum[2 * NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // the call's header starts at zero (this is the preparation's first kernel; every later
-    // writer runs after it in stream order): no separate hipMemsetAsync per waveform
-    static_assert(sizeof(Header) == 8 * sizeof(unsigned long long), "header: 8 words");
-    if (tid < 8) reinterpret_cast<unsigned long long*>(hdr)[tid] = 0ull;
+    // the call's counters start at zero (this is the preparation's first kernel; every later
+    // writer runs after it in stream order): no separate hipMemsetAsync per waveform. The error
+    // flags stay set until efd_modesum_status clears them (sticky; see Header)
+    if (tid == 0) {
+        const bool init = hdr->magic == HDR_MAGIC;
+        hdr->contributions = 0;
+        hdr->evaluations = 0;
+        hdr->groups = 0;
+        if (!init) {
+            hdr->runs_overflow = 0;
+            hdr->bad_mn = 0;
+            hdr->bad_tile = 0;
+            hdr->pad[0] = hdr->pad[1] = hdr->pad[2] = 0;
+            hdr->magic = HDR_MAGIC;
+        }
+    }
     __syncthreads();
     // k_modesum's (sin, cos)(k pi/256) table, computed once per waveform here and copied into
     // each tile's LDS by LDS-DMA (cheaper than 512 sincospi per tile at small harmonic counts)
@@ -1391,20 +1411,6 @@ __device__ __forceinline__ double rsqrt_pos_sum(double x) {
 // Series split: R = sum_j b_j u^j, I = w sum_j c_j u^j, u = w^2, b_j = (-1)^j a_{2j},
 // c_j = (-1)^j a_{2j+1}. With 6 terms the truncation is < 1e-17 for |y| >= 555 (fast path);
 // smaller |y| (hours before plunge, turning points) takes kfactor_slow.
-__constant__ double KB[20] = {
-    1.0, -0.037133487654320986, 0.05764919041266972, -0.2915913992307505, 3.079453030173167,
-    -55.62278536591708, 1533.1694320127956, -59892.51356587907, 3148257.4178668265,
-    -214288036.96368033, 18335766937.890568, -1926471158970.4465, 243826826879716.03,
-    -3.659030701264313e+16, 6.424049357901938e+18, -1.3045132993176097e+21,
-    3.0338710865943386e+23, -8.011464687609593e+25, 2.3839516727271057e+28,
-    -7.940171107576632e+30};
-__constant__ double KC[20] = {
-    -0.06944444444444445, 0.03799305912780064, -0.11609906402551541, 0.8776669695100169,
-    -12.341573332345238, 278.46508077760257, -9207.206599726414, 419524.87511655106,
-    -25198919.871602368, 1929375549.182493, -183418303528.83255, 21196999388647.65,
-    -2926599219297925.0, 4.7576810203630675e+17, -8.995207427058378e+19,
-    1.9570621786581614e+22, -4.854832179436167e+24, 1.3621079545263217e+27,
-    -4.2915604492858035e+29, 1.5087738952527293e+32};
 
 
 
@@ -1413,7 +1419,6 @@ __constant__ double KC[20] = {
 // local variable x = 8 m - (9 + 2k) in [-1, 1) exact (m = mantissa in [1, 2)), then one Horner
 // chain of KTAB_DEG FMAs each for Re and Im. Max error 1.1e-16 against mpmath. Outside the range
 // the interval index is clamped (callers mask or never get there).
-#include "kfactor_table.inc"
 constexpr double KTAB_WMIN = 0x1p-8, KTAB_WMAX = 0x1p10;
 static_assert(KTAB_E_LO == -8 && KTAB_E_HI == 10, "KTAB_WMIN/WMAX follow the table's range");
 __device__ __forceinline__ void kfactor_tab(double ww, double& R, double& I) {
@@ -1469,31 +1474,6 @@ __device__ __forceinline__ void kseries_fast(double ww, double& R, double& I) {
 // Ascending-series coefficients of kfactor_slow, c+-_k = 1 / (k! Gamma(k + 1 +- 1/3)) (the
 // recurrence c_k = c_(k-1) / (k (k +- 1/3)) evaluated once, in double), and the Horner degree
 // for |y| < i + 1 (next term < 1e-19 of the leading one); |y| < 18.4 needs at most 41.
-__constant__ double ASC_P[42] = {
-    1.1198465217221856, 0.8398848912916392, 0.1799753338482084, 0.01799753338482084,
-    0.001038319233739664, 3.89369712652374e-05, 1.024657138558879e-06, 1.9960853348549593e-08,
-    2.9941280022824386e-10, 3.564438097955284e-12, 3.449456223827694e-14, 2.766943495048952e-16,
-    1.869556415573616e-18, 1.0785902397540092e-20, 5.375034417378783e-23, 2.336971485816862e-25,
-    8.942492930421667e-28, 3.0347826686951365e-30, 9.196311117257989e-33, 2.5035329720303054e-35,
-    6.156228619746653e-38, 1.3741581740505923e-40, 2.796794112721694e-43, 5.211417601344772e-46,
-    8.923660276275295e-49, 1.4089989909908362e-51, 2.0579342614277064e-54, 2.788528809522637e-57,
-    3.514952280910888e-60, 4.13199719542816e-63, 4.540656258712264e-66, 4.674663272524637e-69,
-    4.5180379566926256e-72, 4.1073072333569326e-75, 3.5185384637552244e-78, 2.8451793507454644e-81,
-    2.175213570906318e-84, 1.5747202492082417e-87, 1.0810436493420424e-90, 7.047220660639129e-94,
-    4.368111979734997e-97, 2.577564110779896e-100};
-__constant__ double ASC_M[42] = {
-    0.7384881116216483, 1.1077321674324723, 0.3323196502297417, 0.04153995627871771,
-    0.0028322697462762076, 0.00012138298912612317, 3.5700879154742108e-06, 7.65018839030188e-08,
-    1.2473133245057413e-09, 1.5991196468022326e-11, 1.6542617035885167e-13, 1.4098821337402132e-15,
-    1.007058666957295e-17, 6.115740892453209e-20, 3.1963802573797266e-22, 1.4529001169907847e-24,
-    5.796144083739833e-27, 2.045697911908176e-29, 6.433012301598037e-32, 1.8138192579693712e-34,
-    4.611404893142469e-37, 1.0625356896641634e-39, 2.2290958524423007e-42, 4.2757593077537736e-45,
-    7.527745260129883e-48, 1.2207154475886294e-50, 1.8292439274554885e-53, 2.540616565910401e-56,
-    3.279625515374872e-59, 3.945018663241626e-62, 4.432605239597333e-65, 4.662628232395511e-68,
-    4.6012778609166224e-71, 4.2683468097556795e-74, 3.728899367870425e-77, 3.073268709783318e-80,
-    2.393511456217537e-83, 1.7642590586370054e-86, 1.2325983176318156e-89, 8.173728896762703e-93,
-    5.151509808884057e-96, 3.089670017323505e-99};
-__constant__ int ASC_DEG[19] = {10, 12, 15, 17, 19, 21, 22, 24, 26, 27, 29, 30, 32, 34, 35, 37, 38, 40, 41};
 
 // (R + i I) for |y| < FAST_Y: the table (kfactor_tab) down to |y| = 2^-10, below that the
 // ascending series K = pi/(2 sin(pi/3)) (I_{-1/3} - I_{1/3}) divided by Q_spa.
@@ -1590,8 +1570,6 @@ __device__ __forceinline__ double cubic(const double* __restrict__ c, double w) 
 #ifndef EFD_POLAR
 #define EFD_POLAR 1
 #endif
-__constant__ double KRH[4] = {1.0, -0.034722222222222222222, 0.055097415123456790123,
-                              -0.283034838766718107};
 // Runtime series length J as increments on the 2-term form, which every record evaluates (81% of
 // records need J = 2; for J = 1 the second terms fall below the rounding of the first): a
 // switch over J-term Horner chains merged its results through 64-bit register copies (2 VALU
@@ -1600,8 +1578,6 @@ __constant__ double KRH[4] = {1.0, -0.034722222222222222222, 0.05509741512345679
 // inline constant 1.0 and the caller's add of theta to the reduced angle becomes an FMA with
 // TH_0: one VALU operation fewer per evaluation than the TH-form chain.
 constexpr double KTH0 = -0.069444444444444444444;   // TH_0
-__constant__ double KTHN[4] = {1.0, -0.51157407407407407407, 1.5977044753086419754,
-                               -12.267136107513349990};   // TH_j / TH_0
 // EFD_J34: records of series length 3 take the fourth terms too (below 1e-17 on their
 // intervals, by the choice of J), so J = 3 and J = 4 share one branch: the compiler otherwise
 // if-converts the J >= 4 increments and merges the two results with 4 v_cndmask per evaluation.
@@ -3632,6 +3608,12 @@ int efd_modesum_status(const void* workspace, void* stream) {
     Header h{};
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
+    if (h.runs_overflow != 0 || h.bad_mn != 0 || h.bad_tile != 0) {
+        // reported once: clear the sticky flags (the stream is idle, so nothing races this)
+        char* w = (char*)const_cast<void*>(workspace);
+        HIP_TRY(hipMemset(w + offsetof(Header, runs_overflow), 0, sizeof(int32_t)));
+        HIP_TRY(hipMemset(w + offsetof(Header, bad_mn), 0, 2 * sizeof(int32_t)));
+    }
     if (h.runs_overflow != 0)
         return fail(EFD_ERR_ARG, "efd_modesum: a harmonic has more than 8 monotonic runs");
     if (h.bad_mn != 0)

@@ -231,6 +231,8 @@ class Likelihood:
         symmetric (the caller takes the per-walker path)."""
         torch = self.torch
         from .summation import WaveformPipeline, sum_batch_loglike
+        if not self._fused_grid_ok(tm, kwargs):
+            return False
         G = self.FUSED_GROUP
         caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),
                                   "create_waveform", None), "caustic", "uniform")
@@ -244,33 +246,42 @@ class Likelihood:
         P.order_after_current()
         s_sum.wait_stream(cur)
         n = len(params)
-        for g0 in range(0, n, G):
-            used, jobs = [], []
-            for i in range(g0, min(n, g0 + G)):
-                j = P.next_slot()
-                if F["busy"][j] is not None:   # the slot's previous sum has read its workspace
-                    P.stream(j).wait_event(F["busy"][j])
-                try:
+        try:
+            for g0 in range(0, n, G):
+                used, jobs = [], []
+                for i in range(g0, min(n, g0 + G)):
+                    j = P.next_slot()
+                    if F["busy"][j] is not None:   # the slot's previous sum has read its workspace
+                        P.stream(j).wait_event(F["busy"][j])
                     slot = tm.submit(P, None, *params[i], *args, order=False, prepare_only=True,
                                      **kwargs)
-                except ValueError:
-                    if i == 0:
-                        return False   # not a symmetric grid: nothing queued yet
-                    raise
-                used.append(slot)
-                jobs.append(P.job(slot))
-            for slot in used:
-                s_sum.wait_stream(P.stream(slot))
-            sum_batch_loglike(jobs, self._d, self._w_templ, out[g0:g0 + len(used)],
-                              stream=s_sum.cuda_stream)
-            ev = torch.cuda.Event()
-            ev.record(s_sum)
-            for slot in used:
-                F["busy"][slot] = ev
-        s_sum.synchronize()
-        P.wait()   # device-side errors of every slot's workspace
+                    used.append(slot)
+                    jobs.append(P.job(slot))
+                for slot in used:
+                    s_sum.wait_stream(P.stream(slot))
+                sum_batch_loglike(jobs, self._d, self._w_templ, out[g0:g0 + len(used)],
+                                  stream=s_sum.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(s_sum)
+                for slot in used:
+                    F["busy"][slot] = ev
+        finally:
+            # `out` belongs to the current stream: nothing may still write it when it is
+            # returned, or freed after an exception
+            s_sum.synchronize()
+        P.wait()   # device-side errors of every slot's workspace (sticky across slot reuse)
         cur.wait_stream(s_sum)
         return True
+
+    def _fused_grid_ok(self, tm, kwargs):
+        """Whether the template's grid for these kwargs is mirror-symmetric (the fused sum's
+        requirement); set up once per grid, without queueing any device work."""
+        cw = getattr(getattr(getattr(tm, "waveform_generator", None), "waveform_generator", None),
+                     "create_waveform", None)
+        if cw is None or not hasattr(cw, "_grid"):
+            return False
+        _, sym = cw._grid(kwargs.get("T", 1.0), kwargs.get("dt", 10.0), kwargs.get("f_arr"))
+        return bool(sym)
 
     def _pipeline_for(self, tm):
         """The WaveformPipeline (self.num_streams slots) and per-slot buffers of get_ll."""

@@ -111,6 +111,8 @@ def _staged_upload(arrays, dev, stream=None, staging=None):
         staging = _STAGING.setdefault((dev.type, dev.index), {})
     st = staging
     if st.get("buf") is None or st["buf"].numel() < total:
+        if st.get("done") is not None:
+            st["done"].synchronize()        # the old buffer's last copy has read it
         st["buf"] = torch.empty(max(total, 1 << 20), dtype=torch.uint8, pin_memory=True)
         st["done"] = None
     if st.get("done") is not None:
@@ -151,12 +153,20 @@ class ModeSumEngine:
         if nbytes == 0:
             raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
         if self._ws is None or self._ws.numel() < nbytes or self._ws.device != device:
+            old = self._ws if self._ws is not None and self._ws.device == device else None
             self._ws = None
-            if stream is not None:
-                with torch.cuda.stream(stream):
-                    self._ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
-            else:
-                self._ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            import contextlib
+            ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+            with ctx:
+                ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+                # the header's device-side error flags are sticky until efd_modesum_status
+                # reads them: a grown workspace inherits its predecessor's header (stream
+                # order), a first one starts clean (nothing from the memory's previous owner)
+                if old is not None:
+                    ws[:64].copy_(old[:64])
+                else:
+                    ws[:64].zero_()
+            self._ws = ws
         return self._ws
 
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
@@ -428,6 +438,10 @@ class WaveformPipeline:
             lay = (key, offs, max(off, 1))
         _, offs, total = lay
         if sl.get("pin") is None or sl["pin"].numel() < total:
+            if sl.get("pin_done") is not None:
+                # the old buffer's last copy (efd_upload, invisible to torch's host allocator)
+                # must have read it before the block can be handed out again
+                sl["pin_done"].synchronize()
             sl["pin"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8, pin_memory=True)
             sl["pin_np"] = sl["pin"].numpy()
             sl["pin_done"] = None
@@ -587,6 +601,7 @@ class FDInterpolatedModeSum:
         self._k0 = 0
         self._fh = None
         self._f_obj = None
+        self._f_tag = None
 
     @property
     def caustic(self):
@@ -600,7 +615,9 @@ class FDInterpolatedModeSum:
             # device tensor seen last time is taken as is (no device->host copy, so the walker
             # loop of a pipelined Likelihood never synchronises); a host array is compared with
             # the cached copy before any validation
-            if f_arr is self._f_obj and hasattr(f_arr, "detach"):
+            # (unless it was modified in place since: its version counter or storage moved)
+            if (f_arr is self._f_obj and hasattr(f_arr, "detach")
+                    and self._f_tag == (f_arr._version, f_arr.data_ptr())):
                 return self._freq_dev, self._sym
             if hasattr(f_arr, "detach"):
                 fh = f_arr.detach().cpu().numpy().astype(np.float64)
@@ -608,7 +625,7 @@ class FDInterpolatedModeSum:
                 fh = np.asarray(f_arr, dtype=np.float64)
             if (self._freq_key is not None and self._freq_key[0] == "f"
                     and np.array_equal(fh, self._fh)):
-                self._f_obj = f_arr
+                self._remember(f_arr)
                 return self._freq_dev, self._sym
             if fh.ndim != 1 or len(fh) == 0 or np.any(np.diff(fh) <= 0):
                 raise ValueError("f_arr must be a strictly increasing 1-D frequency array")
@@ -625,8 +642,12 @@ class FDInterpolatedModeSum:
             self._freq_key = key
             self._fh = fh
             self.frequency = self._freq_dev if self.use_gpu else fh
-        self._f_obj = f_arr
+        self._remember(f_arr)
         return self._freq_dev, self._sym
+
+    def _remember(self, f_arr):
+        self._f_obj = f_arr
+        self._f_tag = (f_arr._version, f_arr.data_ptr()) if hasattr(f_arr, "detach") else None
 
     def submit_channels(self, pipeline, out, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr,
                         n_arr, M, p, e, dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j,

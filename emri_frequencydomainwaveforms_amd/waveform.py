@@ -210,15 +210,18 @@ class GenerateEMRIWaveform:
         walker loop of Likelihood.get_ll keeps several templates in flight). Returns the slot;
         work that reads out belongs on pipeline.stream(slot)."""
         gen = self.waveform_generator
+        if k0 is not None and gen.output_type == "fd":
+            # checked before anything is queued (the grid is set up from the call's kwargs)
+            cw = gen.create_waveform
+            cw._grid(kwargs.get("T", 1.0), kwargs.get("dt", 10.0), kwargs.get("f_arr"))
+            if k0 != cw.positive_start():
+                raise ValueError("positive_frequency_mask does not match the generator's grid")
         theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
         rot = 1.0 + 0.0j
         if self.frame == "detector":
             rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
-        slot = gen.submit_channels(pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0,
+        return gen.submit_channels(pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0,
                                    Phi_r0, extra_scale=rot, **kwargs)
-        if k0 is not None and k0 != gen.create_waveform.positive_start():
-            raise ValueError("positive_frequency_mask does not match the generator's grid")
-        return slot
 
     def fill_channels(self, out, *params, k0=None, **kwargs):
         """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).

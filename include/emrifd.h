@@ -157,10 +157,12 @@ int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* works
                             const size_t* workspace_bytes, int32_t count, const double* d,
                             const double* w, double* out, void* stream);
 
-/* Synchronises `stream` and reports errors detected on the device by the last efd_modesum on
- * this workspace: a harmonic with more than 8 monotonic frequency runs, or |m| > 255 or
- * |n| > 1023 -> EFD_ERR_ARG; a tile dispatch-order entry out of range in the sum (its bins left
- * unwritten, e.g. a sum run on a workspace another call prepared) -> EFD_ERR_HIP. */
+/* Synchronises `stream` and reports errors detected on the device by the calls on this
+ * workspace since the previous efd_modesum_status (the flags are sticky across preparations, so
+ * a workspace reused by several waveforms before its status is read loses none): a harmonic
+ * with more than 8 monotonic frequency runs, or |m| > 255 or |n| > 1023 -> EFD_ERR_ARG; a tile
+ * dispatch-order entry out of range in the sum (its bins left unwritten, e.g. a sum run on a
+ * workspace another call prepared) -> EFD_ERR_HIP. Reported flags are cleared. */
 int efd_modesum_status(const void* workspace, void* stream);
 
 /* Contributions C (harmonic branch x bin pairs, the reference's per-(l, m, n) formulation) of
@@ -255,6 +257,33 @@ int efd_loglike(const double* h, const double* d, const double* w, int32_t nchan
 #define EFD_INNER_SCRATCH 2048
 int efd_inner_product(const double* a, const double* b, const double* w, int32_t nchan,
                       int64_t nbin, double* out, double* scratch, void* stream);
+
+/*
+ * CPU twins: the same algorithm on HOST pointers, C++17 + OpenMP
+ * (csrc/emrifd_cpu.cpp, linked into libemrifd.so). Signatures are those of the HIP entry points;
+ * `stream`, `workspace` and `scratch` are accepted for parity and ignored (pass NULL / 0). The
+ * reference's CPU path is the numpy branch of the same FEW generator (check_mode_by_mode.py:50-60,
+ * emri_pe.py:68-80); these twins are the CPU baseline bench.py times at 1 thread and all cores.
+ * efd_modesum_cpu: the same grouping, splines, interval records and tile-wise output-stationary
+ * sum with the uniform K_{1/3} fast path as efd_modesum, exact IEEE divisions / square roots;
+ * synchronous. Errors (EFD_ERR_ARG) are reported by return code + efd_cpu_last_error.
+ */
+int efd_modesum_cpu(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
+                    void* stream);
+/* Counters of the calling thread's last efd_modesum_cpu (as efd_modesum_stats). */
+int efd_modesum_cpu_stats(int64_t* contributions, int64_t* evaluations, int32_t* groups);
+int efd_spline_build_cpu(const double* x, int n, const double* y, int ninterp, double* coef,
+                         void* stream);
+int efd_polarizations_cpu(const double* S, int64_t nf, int64_t k0, double* hp, double* hc,
+                          void* stream);
+int efd_loglike_cpu(const double* h, const double* d, const double* w, int32_t nchan,
+                    int64_t nbin, double* out, double* scratch, void* stream);
+int efd_inner_product_cpu(const double* a, const double* b, const double* w, int32_t nchan,
+                          int64_t nbin, double* out, double* scratch, void* stream);
+/* OpenMP threads of the twins (n <= 0: all available); returns the previous setting. */
+int efd_cpu_threads(int n);
+/* Last error message of the calling thread's CPU-twin call. */
+int efd_cpu_last_error(char* buf, int len);
 
 #ifdef __cplusplus
 }

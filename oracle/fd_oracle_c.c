@@ -174,18 +174,39 @@ static int64_t upper_bound(const double* f, int64_t nf, double v) {
     return lo;
 }
 
-/* amp: complex [K][nt] interleaved; ylm_p, ylm_m: complex [K]; out: complex [nf] (written). */
+/* amp: complex [K][nt] interleaved; ylm_p, ylm_m: complex [K]; out: complex [nf] (written).
+ * extrap (optional, real [nf]): per bin, the summed magnitude |term| of the contributions whose
+ * t(g) lies outside the trajectory [t_0, t_{nt-1}], where scipy's splines extrapolate (the
+ * inverse spline of a nearly flat monotonic run can overshoot the run's times by far). Those
+ * terms are part of the construction (CubicSpline extrapolates by default), but their phase
+ * comes from cubics evaluated far outside their interval and is numerically undetermined: two
+ * faithful evaluations of it agree in magnitude only. The parity tests bound such bins by it. */
+int fdo_modesum_ex(const double* t, int nt, const double* amp, const double* phi_phi,
+                   const double* phi_r, const double* f_phi, const double* f_r, const int* marr,
+                   const int* narr, const double* ylm_p, const double* ylm_m, int K,
+                   const double* freq, int64_t nf, double scale_re, double scale_im, int caustic,
+                   int nthreads, double* out, double* extrap);
 int fdo_modesum(const double* t, int nt, const double* amp, const double* phi_phi,
                 const double* phi_r, const double* f_phi, const double* f_r, const int* marr,
                 const int* narr, const double* ylm_p, const double* ylm_m, int K,
                 const double* freq, int64_t nf, double scale_re, double scale_im, int caustic,
                 int nthreads, double* out) {
+    return fdo_modesum_ex(t, nt, amp, phi_phi, phi_r, f_phi, f_r, marr, narr, ylm_p, ylm_m, K,
+                          freq, nf, scale_re, scale_im, caustic, nthreads, out, NULL);
+}
+
+int fdo_modesum_ex(const double* t, int nt, const double* amp, const double* phi_phi,
+                   const double* phi_r, const double* f_phi, const double* f_r, const int* marr,
+                   const int* narr, const double* ylm_p, const double* ylm_m, int K,
+                   const double* freq, int64_t nf, double scale_re, double scale_im, int caustic,
+                   int nthreads, double* out, double* extrap) {
     if (nt < 2 || K < 0 || nf <= 0) return -1;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
     double complex* S = (double complex*)out;
     memset(out, 0, sizeof(double) * 2 * nf);
+    if (extrap) memset(extrap, 0, sizeof(double) * nf);
     int ni = nt - 1;
     double* F = malloc(sizeof(double) * nt);
     double* ph = malloc(sizeof(double) * nt);
@@ -269,6 +290,7 @@ int fdo_modesum(const double* t, int nt, const double* amp, const double* phi_ph
                                cexp(I * (TWO_PI_D * g * tt + Ph));
                     }
                     S[k] -= term * scale;
+                    if (extrap && (tt < t[0] || tt > t[nt - 1])) extrap[k] += cabs(term * scale);
                 }
             }
             i0 = b;

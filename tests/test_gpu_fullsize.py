@@ -4,13 +4,17 @@ size-independent properties of the spectrum.
 
 - Full spectrum vs oracle/fd_oracle_c (per-(l, m, n) harmonic, the reference formulation; ~12 s
   on 16 host threads per evaluation), identical support (set of non-zero bins) and identical
-  contribution count C. Tolerance: max|S_gpu - S_ref| <= max(1e-9 max|S_ref|, 2 D) where
-  D = max|S_ref' - S_ref| is the oracle's own response to 1-ulp perturbations of its inputs
-  (t, f_phi, Phi_phi). At 2 yr the trajectory reaches turning points of F = m f_phi + n f_r
-  (e.g. (m, n) = (5, 13) near 0.01675 Hz), where the reference's inverse spline t(F) is
-  ill-conditioned: 1 ulp in the inputs moves those bins by ~3e-5 of the harmonic's peak and
-  the numpy and C oracles differ by 3e-7 there. D measures that floor instead of guessing it;
-  away from folds the 1e-9 bound of the small-size tests applies.
+  contribution count C. Tolerance, per bin (tests/helpers.split_check): D_k = max |S_ref'(k) -
+  S_ref(k)| is the oracle's own response to two random 4-ulp perturbations of its trajectory
+  inputs (t, Phi_phi, Phi_r, f_phi, f_r), as a running max over +-8 bins. At 2 yr the trajectory reaches turning points of
+  F = m f_phi + n f_r (e.g. (m, n) = (5, 13) near 0.01675 Hz), where the reference's inverse
+  spline t(F) is ill-conditioned: 1 ulp in the inputs moves those bins by ~3e-5 of the
+  harmonic's peak. Bins with D_k > 1e-9 max|S_ref| (the folds) must meet |S - S_ref| <= 2 D_k;
+  every other bin must meet |S - S_ref| <= 1e-9 max|S_ref|; bins holding terms whose t(g)
+  the splines extrapolate outside the trajectory (a nearly flat run's inverse spline
+  overshooting, e.g. (m, n) = (6, -19) near 5.26 mHz) get + 2 E_k, E_k their magnitude: their
+  phase is numerically undetermined (split_check's docstring). The measured errors and the fold
+  count go to $EFD_PARITY_OUT (profiles/r03_parity.json).
 - Linearity in the harmonic set: S(all) == S(A) + S(B) for a split of the harmonics that cuts
   (m, n) groups apart (accumulate = 1), to 1e-12 max|S|.
 - Bitwise determinism of repeated runs.
@@ -28,6 +32,7 @@ pytestmark = pytest.mark.gpu
 import bench  # noqa: E402
 from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine  # noqa: E402
 from oracle import fd_oracle, fd_oracle_c  # noqa: E402
+from tests.helpers import record_parity, split_check, ulp_perturbation  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -50,18 +55,25 @@ def test_config2_full_spectrum_vs_c_oracle(cfg2):
     C, n_eval, groups = eng.stats()
     assert len(w["m"]) == 3020 and groups == len(set(zip(w["m"].tolist(), w["n"].tolist())))
     threads = min(16, len(os.sched_getaffinity(0)))
-    R = fd_oracle_c.modesum(w["t"], w["amp"].T, w["phi_phi"], w["phi_r"], w["f_phi"], w["f_r"],
-                            w["m"], w["n"], w["ylm_p"], w["ylm_m"], w["freq"], w["prefactor"],
-                            caustic="uniform", nthreads=threads)
-    rng = np.random.default_rng(7)
-    ulp = lambda x: x * (1.0 + rng.choice([-1.0, 1.0], len(x)) * 2.0 ** -52)  # noqa: E731
-    Rp = fd_oracle_c.modesum(ulp(w["t"]), w["amp"].T, ulp(w["phi_phi"]), w["phi_r"],
-                             ulp(w["f_phi"]), w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"],
-                             w["freq"], w["prefactor"], caustic="uniform", nthreads=threads)
-    mx = np.abs(R).max()
-    floor = np.abs(Rp - R).max()
-    err = np.abs(S - R).max()
-    assert err <= max(1e-9 * mx, 2.0 * floor), (err / mx, floor / mx)
+    R, E = fd_oracle_c.modesum(w["t"], w["amp"].T, w["phi_phi"], w["phi_r"], w["f_phi"],
+                               w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"], w["freq"],
+                               w["prefactor"], caustic="uniform", nthreads=threads, extrap=True)
+    Rps = []
+    for seed in (7, 8):
+        pert = ulp_perturbation(seed)
+        Rps.append(fd_oracle_c.modesum(pert(w["t"]), w["amp"].T, pert(w["phi_phi"]),
+                                       pert(w["phi_r"]), pert(w["f_phi"]), pert(w["f_r"]),
+                                       w["m"], w["n"], w["ylm_p"],
+                                       w["ylm_m"], w["freq"], w["prefactor"], caustic="uniform",
+                                       nthreads=threads))
+    ok, stats, _ = split_check(S, R, Rps, E=E)
+    record_parity("config2", dict(stats, contributions=C, evaluations=n_eval, groups=groups))
+    if not ok and os.environ.get("EFD_PARITY_OUT"):   # the neighbourhood of the worst bin
+        k = stats["worst_bin"]["k"]
+        sl = slice(max(0, k - 200), k + 200)
+        np.savez(os.path.join(os.environ["EFD_PARITY_OUT"], "config2_worst.npz"), k=k,
+                 S=S[sl], R=R[sl], Rps=np.array([x[sl] for x in Rps]), f=w["freq"][sl])
+    assert ok, stats
     np.testing.assert_array_equal(S != 0, R != 0)
     assert C == fd_oracle.contributions(w["t"], w["f_phi"], w["f_r"], w["m"], w["n"], w["freq"])
     assert n_eval < C / 3     # one SPA evaluation per (m, n) group serves every l

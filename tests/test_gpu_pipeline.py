@@ -89,3 +89,30 @@ def test_pipeline_surfaces_slot_errors(sources):
     pipe.submit(_host(d), freq, True, 1.0, out=torch.view_as_real(S))
     with pytest.raises(_lib.EFDError):
         pipe.wait()
+
+
+def test_slot_errors_survive_slot_reuse(sources):
+    """a device-side error of an early waveform on a slot is not erased when later
+    waveforms reuse that slot before wait() (sticky header flags); wait() reports it once and
+    the slot is clean afterwards. Covers both error kinds a preparation raises: |m| > 255 and a
+    harmonic with more than 8 monotonic frequency runs (an f_r oscillating along the
+    trajectory makes F = m f_phi + n f_r turn at every knot)."""
+    freq = torch.as_tensor(sources[0]["freq"], device="cuda")
+    S = torch.empty(int(freq.numel()), dtype=torch.complex128, device="cuda")
+    bad_m = _host(sources[0])
+    bad_m["m"] = bad_m["m"].copy()
+    bad_m["m"][0] = 300
+    bad_runs = _host(sources[0])
+    nt = len(bad_runs["t"])
+    assert nt > 20
+    bad_runs["f_r"] = bad_runs["f_r"] * (1.0 + 0.3 * (-1.0) ** np.arange(nt))
+    for bad in (bad_m, bad_runs):
+        pipe = WaveformPipeline(2)
+        pipe.submit(bad, freq, True, 1.0, out=torch.view_as_real(S))      # slot 0
+        for d in sources[1:4]:                                             # slots 1, 0, 1
+            pipe.submit(_host(d), freq, True, 1.0, out=torch.view_as_real(S))
+        with pytest.raises(_lib.EFDError):
+            pipe.wait()
+        pipe.submit(_host(sources[1]), freq, True, 1.0, out=torch.view_as_real(S))
+        pipe.submit(_host(sources[2]), freq, True, 1.0, out=torch.view_as_real(S))
+        pipe.wait()                                                        # reported once

@@ -1,0 +1,77 @@
+"""HIP path == host twin (efd_modesum_cpu): the same algorithm on the GPU and on the CPU.
+
+The twin is held to the oracle in tests/test_cpu_twin.py; here the kernels are held to the twin
+at a tighter bound than to the oracle, since the two share every construction step and differ
+only by rounding (reciprocal / rsqrt estimates with Newton steps and FMA contraction on the GPU,
+the records' order within a tile):
+- small sources, both caustic modes, symmetric / asymmetric / downsampled grids, the fused
+  h+/hx: max|S_hip - S_twin| <= 1e-10 max|S_twin|;
+- config 2 at full size: per bin, 1e-10 max|S_twin| wherever the twin's own response to two
+  random 4-ulp perturbations of the trajectory inputs stays below that, 2 x that response on
+  the remaining (fold / extrapolated-term) bins (tests/helpers.split_check), identical support,
+  contribution and evaluation counts.
+"""
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import bench  # noqa: E402
+from emri_frequencydomainwaveforms_amd import cputwin  # noqa: E402
+from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine  # noqa: E402
+from tests.helpers import record_parity, source_inputs, split_check, ulp_perturbation  # noqa: E402
+
+
+def _hip(d, freq_h, caustic="uniform", amp_nt_k=None):
+    amp = amp_nt_k if amp_nt_k is not None else np.ascontiguousarray(d["amp"].T)
+    inp = DeviceInputs.from_host(d["t"], amp, d["phi_phi"], d["phi_r"], d["f_phi"], d["f_r"],
+                                 d["m"], d["n"], d["ylm_p"], d["ylm_m"])
+    freq = torch.as_tensor(freq_h, device="cuda")
+    sym = bool(np.array_equal(freq_h, -freq_h[::-1]))
+    eng = ModeSumEngine(caustic=caustic)
+    S = eng.run(inp, freq, grid_symmetric=sym, scale=d["prefactor"]).cpu().numpy()
+    return S, eng.stats()
+
+
+@pytest.mark.parametrize("caustic", ["uniform", "spa"])
+def test_hip_equals_twin_small(caustic):
+    d = source_inputs(M=3e5, e0=0.35, T=0.02, dt=20.0, eps=1e-2)
+    freq = d["freq"]
+    T = cputwin.modesum(d["t"], d["amp"].T, d["phi_phi"], d["phi_r"], d["f_phi"], d["f_r"],
+                        d["m"], d["n"], d["ylm_p"], d["ylm_m"], freq, d["prefactor"],
+                        caustic=caustic)
+    S, st = _hip(d, freq, caustic)
+    assert np.abs(S - T).max() <= 1e-10 * np.abs(T).max()
+    np.testing.assert_array_equal(S != 0, T != 0)
+    assert st == cputwin.stats()
+    nz = np.abs(T[freq >= 0]) > 0
+    fmax = freq[freq >= 0][nz].max() * 1.01
+    p = np.linspace(0.0, fmax, 77)
+    for grid in (np.hstack((-np.linspace(fmax, 0.0, 40)[:-1], np.linspace(0.0, fmax, 61))),
+                 np.hstack((-p[::-1][:-1], p))):
+        Tg = cputwin.modesum(d["t"], d["amp"].T, d["phi_phi"], d["phi_r"], d["f_phi"], d["f_r"],
+                             d["m"], d["n"], d["ylm_p"], d["ylm_m"], grid, d["prefactor"],
+                             caustic=caustic)
+        Sg, _ = _hip(d, grid, caustic)
+        assert np.abs(Sg - Tg).max() <= 1e-10 * np.abs(Tg).max()
+
+
+def test_hip_equals_twin_config2_full_size():
+    w = bench.build_workload()
+
+    def twin(p=None):
+        p = p or (lambda x: x)
+        return cputwin.modesum(p(w["t"]), w["amp"], p(w["phi_phi"]), p(w["phi_r"]),
+                               p(w["f_phi"]), p(w["f_r"]), w["m"], w["n"], w["ylm_p"],
+                               w["ylm_m"], w["freq"], w["prefactor"])
+    T = twin()
+    tstats = cputwin.stats()
+    S, st = _hip(w, w["freq"], amp_nt_k=w["amp"])
+    assert st == tstats
+    Tps = [twin(ulp_perturbation(s)) for s in (31, 32)]
+    ok, stats, _ = split_check(S, T, Tps, rel=1e-10)
+    record_parity("config2_hip_vs_twin", stats)
+    assert ok, stats
+    np.testing.assert_array_equal(S != 0, T != 0)
