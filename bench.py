@@ -223,10 +223,19 @@ def main():
     ap.add_argument("--diag-sum-only", action="store_true",
                     help="diagnostic, not the metric: each slot is prepared once in the warm-up, "
                          "then every step runs only the mode sum (the sum-stream ceiling)")
+    ap.add_argument("--likelihood", choices=["config4", "config5"], default=None,
+                    help="time emri_pe.py's likelihood instead (BASELINE configs 4 / 5): walker "
+                         "half-steps through Likelihood (fused mode sum + logL), sharded over the "
+                         "ranks by ShardedLikelihood (parameter broadcast + logL all-gather)")
+    ap.add_argument("--api-steps", type=int, default=2,
+                    help="--likelihood: half-steps timed with the host upstream in the loop")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
+
+    if args.likelihood:
+        return bench_likelihood(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -402,6 +411,99 @@ def main():
             "cpu_reference": cpu_ref,
         }
         print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+LIKE_CONFIGS = {
+    # emri_pe.py -Tobs 2 -eps 1e-2 -injectFD 1 -template fd -nwalkers 16 -ntemps 1 (README)
+    "config4": dict(Tobs=2.0, dt=10.0, eps=1e-2, nwalkers=16, ntemps=1),
+    # ... -downsample 100 -Tobs 4 -nwalkers 128 (BASELINE configs[4])
+    "config5": dict(Tobs=4.0, dt=10.0, eps=1e-2, nwalkers=128, ntemps=1, downsample=100),
+}
+
+
+def bench_likelihood(args):
+    """Log-likelihoods/s of emri_pe.py's sampler calls (configs 4 / 5) over the ranks.
+
+    One step = one red-blue half-step: B = ntemps * nwalkers / 2 walkers (8 for config 4, 64 for
+    config 5) from the reference's start distribution (pe.setup), evaluated as Eryn's vectorised
+    call does (Likelihood.__call__: transforms, subset, fused mode sum + logL on the device).
+    With N ranks, ShardedLikelihood broadcasts the B x 6 parameters from rank 0 (RCCL), every rank
+    evaluates its contiguous B / N walkers, and the B logL are all-gathered (RCCL): a fixed batch
+    split over the ranks (strong scaling). `value` times the device path: each walker's host
+    upstream (the Python stand-in trajectory and amplitudes) is memoised after the warm-up;
+    api_loglikes_per_s times --api-steps half-steps with the upstream in the loop."""
+    import torch
+    import torch.distributed as dist
+    from emri_frequencydomainwaveforms_amd import pe
+    from emri_frequencydomainwaveforms_amd.parallel import ShardedLikelihood
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    cfg = LIKE_CONFIGS[args.likelihood]
+    s = pe.setup(**cfg)
+    B = s.half_step
+    batches = s.half_steps()
+    if world > 1:
+        sl = ShardedLikelihood(s.like, broadcast=True, call_kwargs=s.kwargs)
+    else:
+        sl = lambda p: s.like(p, **s.kwargs)  # noqa: E731
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # the API rate: host upstream in the loop
+    sl(batches[0])
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.api_steps):
+        sl(batches[(i + 1) % len(batches)])
+    barrier()
+    api = time.perf_counter() - t0
+    memo = pe.MemoizedUpstream(s.few.waveform_generator)
+    for i in range(max(args.warmup, len(batches))):
+        ll = sl(batches[i % len(batches)])
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ll = sl(batches[i % len(batches)])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed, api], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, api = float(tt[0]), float(tt[1])
+    if rank == 0:
+        line = {
+            "metric": f"FD log-likelihoods/sec (emri_pe {args.likelihood}: "
+                      f"{'downsample=100 ' if cfg.get('downsample') else ''}Tobs={cfg['Tobs']}yr "
+                      f"eps={cfg['eps']} nwalkers={cfg['nwalkers']}) at 1/2/4/8 GPUs",
+            "value": args.steps * B / elapsed, "unit": "logL/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (stand-in trajectory/amplitudes; FEW data absent offline)",
+            "config": {"workload": f"{args.likelihood}: emri_pe.py Likelihood over red-blue "
+                                   f"half-steps of {B} walkers", "walkers_per_step": B,
+                       "N_f": s.info.get("N_f"), "N_f_downsampled": s.info.get("N_f_downsampled"),
+                       "p0": s.info["p0"], "parallelism": f"walker shards x{world} (RCCL "
+                       "broadcast of params + all-gather of logL)" if world > 1 else "1 GPU",
+                       "fused_likelihood": bool(s.like.fused_likelihood)},
+            "api_loglikes_per_s": args.api_steps * B / api,
+            "host_upstream_ms_per_walker": memo.host_s / max(1, len(memo.memo)) * 1e3,
+            "ll_truth_walker_sample": float(np.asarray(ll)[0]),
+            "note": "value: device path with each walker's host upstream memoised after the "
+                    "warm-up (inputs resident); api_loglikes_per_s: the same calls with the "
+                    "Python stand-in upstream in the loop",
+        }
+        print(json.dumps(line))
+    memo.remove()
     if world > 1:
         dist.destroy_process_group()
 

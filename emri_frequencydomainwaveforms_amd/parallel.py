@@ -30,13 +30,16 @@ def shard_range(n, rank, world):
 class ShardedLikelihood:
     """Evaluate a batch of walkers' log-likelihoods across ranks.
 
-    like: anything with `get_ll(params[b, ndim]) -> array[b]` (this package's Likelihood) or a
-    plain callable with the same signature.
+    like: this package's Likelihood (called as Eryn calls it, `like(params, **call_kwargs)`:
+    parameter transforms, subset batching, get_ll; emri_pe.py:399-417 with Eryn's
+    vectorize=True, ensemble.py:1283-1318, and its _FunctionWrapper kwargs, :1539-1583), or any
+    callable params[b, ndim] -> array[b]; an object without __call__ is used through get_ll.
+    call_kwargs: the waveform kwargs of every call (T, dt, eps[, f_arr]).
     """
 
     _STOP = -1
 
-    def __init__(self, like, group=None, src=0, broadcast=True):
+    def __init__(self, like, group=None, src=0, broadcast=True, call_kwargs=None):
         import torch
         import torch.distributed as dist
         if not dist.is_initialized():
@@ -46,6 +49,7 @@ class ShardedLikelihood:
         self.group = group
         self.src = src
         self.broadcast = broadcast
+        self.call_kwargs = dict(call_kwargs or {})
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if dist.get_backend(group) == "nccl":
@@ -55,10 +59,10 @@ class ShardedLikelihood:
         self.evaluated = 0      # walkers this rank evaluated (for accounting / tests)
 
     def _local(self, params):
-        fn = getattr(self.like, "get_ll", self.like)
+        fn = self.like if callable(self.like) else self.like.get_ll
         if len(params) == 0:
             return np.zeros(0, dtype=np.float64)
-        out = np.asarray(fn(params), dtype=np.float64).reshape(-1)
+        out = np.asarray(fn(params, **self.call_kwargs), dtype=np.float64).reshape(-1)
         if len(out) != len(params):
             raise ValueError(f"likelihood returned {len(out)} values for {len(params)} walkers")
         self.evaluated += len(params)

@@ -103,3 +103,32 @@ def setup(Tobs=2.0, dt=10.0, eps=1e-2, M=1e6, mu=10.0, e0=0.35, downsample=None,
     return PESetup(few=few, gen=gen, like=like, transform=tc, truth14=injection,
                    truth6=truth6, start=start, kwargs=kw, f_like=f_like,
                    half_step=max(1, nwalkers * ntemps // 2), info=info)
+
+
+class MemoizedUpstream:
+    """Memoise a generator's host upstream (trajectory, amplitudes, Ylm, mode selection: the
+    stand-ins of trajectory.py / amplitude.py) per parameter set, so repeated likelihood calls on
+    the same walkers time the device path alone ("inputs resident"). Installed on the instance;
+    `remove()` restores it. Arrays in kwargs (f_arr) are keyed by identity."""
+
+    def __init__(self, wg):
+        import time
+        self._time = time.perf_counter
+        self.wg = wg
+        self.orig = wg.prepare
+        self.memo = {}
+        self.host_s = 0.0
+        wg.prepare = self
+
+    def __call__(self, *args, **kwargs):
+        key = repr((args, sorted((k, ("id", id(v)) if hasattr(v, "shape") else v)
+                                 for k, v in kwargs.items())))
+        if key not in self.memo:
+            t0 = self._time()
+            self.memo[key] = self.orig(*args, **kwargs)
+            self.host_s += self._time() - t0
+        return self.memo[key]
+
+    def remove(self):
+        if self.wg.__dict__.get("prepare") is self:
+            del self.wg.prepare        # back to the class's method
