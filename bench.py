@@ -432,7 +432,7 @@ def bench_likelihood(args):
     With N ranks, ShardedLikelihood broadcasts the B x 6 parameters from rank 0 (RCCL), every rank
     evaluates its contiguous B / N walkers, and the B logL are all-gathered (RCCL): a fixed batch
     split over the ranks (strong scaling). `value` times the device path: each walker's host
-    upstream (the Python stand-in trajectory and amplitudes) is memoised after the warm-up;
+    upstream (the C++ stand-in trajectory and amplitudes) is memoised after the warm-up;
     api_loglikes_per_s times --api-steps half-steps with the upstream in the loop."""
     import torch
     import torch.distributed as dist
@@ -500,7 +500,8 @@ def bench_likelihood(args):
             "ll_truth_walker_sample": float(np.asarray(ll)[0]),
             "note": "value: device path with each walker's host upstream memoised after the "
                     "warm-up (inputs resident); api_loglikes_per_s: the same calls with the "
-                    "Python stand-in upstream in the loop",
+                    "host stand-in upstream (C++ trajectory, amplitudes, selection on a thread "
+                    "pool: NOT FEW physics) in the loop",
         }
         print(json.dumps(line))
     memo.remove()

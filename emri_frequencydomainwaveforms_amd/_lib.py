@@ -48,6 +48,9 @@ EXPORTED_SYMBOLS = (
     "efd_inner_product_cpu",
     "efd_cpu_threads",
     "efd_cpu_last_error",
+    "efd_host_trajectory",
+    "efd_host_p_at_t",
+    "efd_host_modes",
 )
 
 
@@ -199,6 +202,14 @@ def load(path=None):
         lib.efd_cpu_threads.argtypes = [ctypes.c_int]
         lib.efd_cpu_last_error.restype = ctypes.c_int
         lib.efd_cpu_last_error.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    if hasattr(lib, "efd_host_trajectory"):   # host upstream stand-ins (csrc/emrifd_host.cpp)
+        lib.efd_host_trajectory.restype = ctypes.c_int
+        lib.efd_host_trajectory.argtypes = [dbl] * 9 + [i32] + [vp] * 7 + [ctypes.POINTER(i32)]
+        lib.efd_host_p_at_t.restype = ctypes.c_int
+        lib.efd_host_p_at_t.argtypes = [dbl] * 10 + [ctypes.POINTER(dbl)]
+        lib.efd_host_modes.restype = ctypes.c_int
+        lib.efd_host_modes.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, dbl, vp,
+                                       ctypes.POINTER(i32), vp, i64]
     _ = dbl
     if path is None:
         _lib = lib

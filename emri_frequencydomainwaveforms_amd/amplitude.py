@@ -15,6 +15,8 @@ branches, keep the modes needed to reach (1 - eps) of the power, fold -m picks o
 the union over time.
 """
 
+import ctypes
+
 import numpy as np
 
 LMAX = 10
@@ -88,6 +90,40 @@ class SyntheticTeukolskyAmplitude:
             else:  # FEW symmetry A_{l,-m,-n} = (-1)^l conj(A_{l,m,n})
                 out[(l, m, n)] = (-1.0) ** l * np.conj(amps[:, self.lmn_indices[(l, -m, -n)]])
         return out
+
+
+    def select(self, p, e, ylms, eps, lib=None):
+        """(keep, teuk): ModeSelector(eps) over this model's modes and the kept modes' complex
+        amplitudes [N_t][K], in one native call (csrc/emrifd_host.cpp: efd_host_modes) when the
+        library is available, else through __call__ + ModeSelector (numpy). ylms: the GetYlms
+        output [Y_lm..., (-1)^l Y_l-m...] over the whole mode list."""
+        if lib is None or not hasattr(lib, "efd_host_modes"):
+            A = self(p, e)
+            keep = ModeSelector(self.m0mask)(A, ylms, None, eps=eps)
+            return keep, np.ascontiguousarray(A[:, keep])
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        e = np.ascontiguousarray(e, dtype=np.float64)
+        K = self.num_teuk_modes
+        yp = np.ascontiguousarray(ylms[:K], dtype=np.complex128)
+        ym = np.ascontiguousarray(ylms[K:], dtype=np.complex128)
+        keep = np.empty(K, dtype=np.int32)
+        nkeep = ctypes.c_int32(0)
+        nt = len(p)
+        cap = 2 * nt * K   # np.empty: untouched pages cost nothing
+        for _ in range(2):
+            teuk = np.empty(cap // 2, dtype=np.complex128)
+            rc = lib.efd_host_modes(p.ctypes.data, e.ctypes.data, nt, self.l_arr.ctypes.data,
+                                    self.m_arr.ctypes.data, self.n_arr.ctypes.data,
+                                    self._phase0.ctypes.data, self._jitter.ctypes.data, K,
+                                    yp.ctypes.data, ym.ctypes.data, float(eps), keep.ctypes.data,
+                                    ctypes.byref(nkeep), teuk.ctypes.data, cap)
+            if rc == 0:
+                k = nkeep.value
+                return keep[:k].astype(np.int64), teuk[:nt * k].reshape(nt, k)
+            if rc != -3:
+                raise RuntimeError(f"efd_host_modes failed ({rc})")
+            cap = 2 * nt * nkeep.value
+        raise RuntimeError("efd_host_modes: amplitude buffer")
 
 
 # FEW-compatible name used by the reference notebooks

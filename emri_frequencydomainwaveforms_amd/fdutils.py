@@ -137,6 +137,12 @@ class get_fd_waveform_fromFD:
         return self.waveform_generator.submit_channels(pipeline, out, *args, k0=self._suffix_k0,
                                                        **kwargs)
 
+    def prefetch(self, params, *args, **kwargs):
+        """The host upstream of a walker batch in parallel (GenerateEMRIWaveform.prefetch),
+        ahead of the per-walker submit/fill calls; a no-op for other generators."""
+        fn = getattr(self.waveform_generator, "prefetch", None)
+        return fn(params, **kwargs) if fn is not None and not args else 0
+
     def fill(self, out, *args, **kwargs):
         """Write [ch1, ch2] into out (complex128 [2][num_bins], device) without copies.
 

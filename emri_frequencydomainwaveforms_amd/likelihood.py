@@ -192,6 +192,8 @@ class Likelihood:
             # stream, the batch costs one host synchronisation
             P = self._pipeline_for(tm)
             P.order_after_current()
+            if hasattr(tm, "prefetch"):
+                tm.prefetch(params, *args, **kwargs)
             for i, params_i in enumerate(params):
                 j = P.next_slot()
                 slot = tm.submit(P, self._pbufs[j], *params_i, *args, order=False, **kwargs)
@@ -233,6 +235,8 @@ class Likelihood:
         from .summation import WaveformPipeline, sum_batch_loglike
         if not self._fused_grid_ok(tm, kwargs):
             return False
+        if hasattr(tm, "prefetch"):
+            tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
         G = self.FUSED_GROUP
         caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),
                                   "create_waveform", None), "caustic", "uniform")

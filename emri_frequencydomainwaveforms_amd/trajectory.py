@@ -12,7 +12,14 @@ separatrix p = 6 + 2e or at T, as FEW's trajectory does.
 The hot path only needs *a* smooth sparse trajectory of FEW's shape (N_t ~ 10^2 knots, ~86 per
 year in the reference notebook :356); RK45 at rtol = atol = 1e-12 gives ~50-100 knots per year.
 `get_p_at_t` mirrors `few.utils.utility.get_p_at_t` as called at check_mode_by_mode.py:200-212.
+
+Two backends with the same equations and integrator: "native" (csrc/emrifd_host.cpp in
+libemrifd.so: scipy RK45's Dormand-Prince tableau, step control, dense output and event root
+restated in C++, ~1 ms per trajectory, releases the GIL) and "python" (scipy.solve_ivp with the
+numpy right-hand side, ~50-100 ms). "auto" takes the native one when the library is built.
 """
+
+import ctypes
 
 import numpy as np
 from scipy.integrate import solve_ivp
@@ -44,19 +51,73 @@ _separatrix_event.terminal = True
 _separatrix_event.direction = -1
 
 
+def _native_lib():
+    try:
+        from . import _lib
+        lib = _lib.load()
+    except Exception:
+        return None
+    return lib if hasattr(lib, "efd_host_trajectory") else None
+
+
 class EMRIInspiral:
     """Sparse inspiral trajectory with the FEW `EMRIInspiral` call surface (stand-in physics)."""
 
-    def __init__(self, func="SchwarzEccFlux", rtol=1e-12, atol=1e-12, max_init_len=1000, **kwargs):
+    def __init__(self, func="SchwarzEccFlux", rtol=1e-12, atol=1e-12, max_init_len=1000,
+                 backend="auto", **kwargs):
         if func not in ("SchwarzEccFlux", "pn5", "PN"):
             raise ValueError(f"unsupported trajectory func {func!r}")
+        if backend not in ("auto", "native", "python"):
+            raise ValueError("backend must be 'auto', 'native' or 'python'")
         self.func = func
         self.rtol = rtol
         self.atol = atol
         self.max_init_len = max_init_len
+        self.lib = None if backend == "python" else _native_lib()
+        if backend == "native" and self.lib is None:
+            raise RuntimeError("the native trajectory needs libemrifd.so (build it first)")
+
+    @property
+    def backend(self):
+        return "native" if self.lib is not None else "python"
+
+    def with_frequencies(self, M, mu, a, p0, e0, x0=1.0, Phi_phi0=0.0, Phi_theta0=0.0,
+                         Phi_r0=0.0, T=1.0, **kwargs):
+        """(t, p, e, Phi_phi, Phi_r, f_phi, f_r): the knots and the orbital frequencies
+        Omega / (2 pi M MTSUN_SI) at them (native backend: one call)."""
+        if self.lib is None:
+            t, p, e, _, pp, _, pr = self(M, mu, a, p0, e0, x0, Phi_phi0, Phi_theta0, Phi_r0, T=T)
+            op, _, orr = get_fundamental_frequencies(0.0, p, e, 0.0)
+            return t, p, e, pp, pr, op / (2 * np.pi * M * MTSUN_SI), orr / (2 * np.pi * M * MTSUN_SI)
+        return self._native(M, mu, a, p0, e0, Phi_phi0, Phi_r0, T, freqs=True)
+
+    def _native(self, M, mu, a, p0, e0, Phi_phi0, Phi_r0, T, freqs=False):
+        if a != 0.0:
+            raise ValueError("SchwarzEccFlux stand-in requires a = 0")
+        if p0 - (6.0 + 2.0 * e0) <= DIST_TO_SEPARATRIX:
+            raise ValueError("initial p0 lies inside the separatrix buffer")
+        L = int(self.max_init_len)
+        bufs = np.empty((7, L))
+        n = ctypes.c_int32(0)
+        p = lambda i: bufs[i].ctypes.data  # noqa: E731
+        rc = self.lib.efd_host_trajectory(float(M), float(mu), float(p0), float(e0),
+                                          float(Phi_phi0), float(Phi_r0), float(T), self.rtol,
+                                          self.atol, L, p(0), p(1), p(2), p(3), p(4),
+                                          p(5) if freqs else None, p(6) if freqs else None,
+                                          ctypes.byref(n))
+        if rc == -3:
+            raise ValueError("trajectory longer than max_init_len")
+        if rc != 0:
+            raise RuntimeError(f"trajectory integration failed ({rc})")
+        k = n.value
+        out = [bufs[i, :k].copy() for i in range(7 if freqs else 5)]
+        return tuple(out)
 
     def __call__(self, M, mu, a, p0, e0, x0=1.0, Phi_phi0=0.0, Phi_theta0=0.0, Phi_r0=0.0,
                  T=1.0, dt=10.0, **kwargs):
+        if self.lib is not None:
+            t, p, e, pp, pr = self._native(M, mu, a, p0, e0, Phi_phi0, Phi_r0, T)
+            return t, p, e, np.ones_like(t), pp, np.full_like(t, Phi_theta0), pr
         if a != 0.0:
             raise ValueError("SchwarzEccFlux stand-in requires a = 0")
         if p0 - (6.0 + 2.0 * e0) <= DIST_TO_SEPARATRIX:
@@ -104,6 +165,15 @@ def get_p_at_t(traj_module, t_out, traj_args, index_of_p=3, index_of_a=2, index_
 
     lo = 6.0 + 2.0 * e0 + DIST_TO_SEPARATRIX + 1e-3 if bounds is None or bounds[0] is None else bounds[0]
     hi = 40.0 if bounds is None or bounds[1] is None else bounds[1]
+    lib = getattr(traj_module, "lib", None)
+    if lib is not None and not traj_kwargs and a == 0.0:
+        out = ctypes.c_double(0.0)
+        rc = lib.efd_host_p_at_t(float(M), float(mu), float(e0), float(t_out), traj_module.rtol,
+                                 traj_module.atol, float(xtol), float(rtol), float(lo), float(hi),
+                                 ctypes.byref(out))
+        if rc != 0:
+            raise ValueError("could not bracket p0 for the requested t_out")
+        return out.value
     if f(lo) > 0:
         raise ValueError("t_out is shorter than the plunge time from the separatrix buffer")
     while f(hi) < 0:

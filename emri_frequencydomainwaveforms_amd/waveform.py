@@ -22,6 +22,9 @@ the complex spectrum S = h+ - i hx is the constant factor exp(-2 i psi) -- folde
 kernel's complex scale, so it costs nothing.
 """
 
+import os
+import threading
+
 import numpy as np
 
 from .amplitude import ModeSelector, RomanAmplitude
@@ -69,12 +72,57 @@ class FastSchwarzschildEccentricFlux:
             sum_kwargs.pop("caustic", None)
             self.create_waveform = TDInterpolatedModeSum(use_gpu=use_gpu, **sum_kwargs)
         self.last_modes = None
+        self._ylm_cache = {}
+        self._prefetched = {}
+        self._lock = threading.Lock()
 
     # -- host-side upstream ------------------------------------------------------------------
+    def _ylms(self, theta, phi):
+        """GetYlms over the whole mode list, cached per viewing angle (the drivers' walkers
+        share their sky and spin angles, emri_pe.py:161-167)."""
+        key = (float(theta), float(phi))
+        with self._lock:
+            y = self._ylm_cache.get(key)
+        if y is None:
+            amp = self.amplitude_generator
+            y = self.ylm_gen(amp.l_arr, amp.m_arr, theta, phi)
+            with self._lock:
+                if len(self._ylm_cache) > 64:
+                    self._ylm_cache.clear()
+                self._ylm_cache[key] = y
+        return y
+
     def prepare(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, T=1.0,
                 eps=1e-5, mode_selection=None, include_minus_m=True):
-        """Trajectory, amplitudes, Ylm and mode selection (host; stand-in physics)."""
+        """Trajectory, amplitudes, Ylm and mode selection (host; stand-in physics).
+
+        With libemrifd.so built, the trajectory, the amplitude model and the selection run in
+        C++ (csrc/emrifd_host.cpp, emrifd_modes.cpp; the same equations and integrator as the
+        numpy/scipy path below, which serves explicit mode_selection lists)."""
+        key = None
+        if mode_selection is None:
+            key = (float(M), float(mu), float(p0), float(e0), float(theta), float(phi),
+                   float(dist), float(Phi_phi0), float(Phi_r0), float(T), float(eps),
+                   bool(include_minus_m))
+            if self._prefetched:
+                with self._lock:
+                    hit = self._prefetched.pop(key, None)
+                if hit is not None:
+                    return hit
         amp = self.amplitude_generator
+        lib = getattr(self.inspiral_generator, "lib", None)
+        if lib is not None and mode_selection is None and hasattr(lib, "efd_host_modes"):
+            t, p, e, Phi_phi, Phi_r, f_phi, f_r = self.inspiral_generator.with_frequencies(
+                M, mu, 0.0, p0, e0, 1.0, Phi_phi0=Phi_phi0, Phi_r0=Phi_r0, T=T)
+            ylms_all = self._ylms(theta, phi)
+            keep, teuk = amp.select(p, e, ylms_all, eps, lib=lib)
+            K = amp.num_teuk_modes
+            ylms = np.concatenate([ylms_all[:K][keep], ylms_all[K:][keep]])
+            if not include_minus_m:
+                ylms[len(keep):] = 0.0
+            self.last_modes = (amp.l_arr[keep], amp.m_arr[keep], amp.n_arr[keep])
+            return dict(t=t, p=p, e=e, Phi_phi=Phi_phi, Phi_r=Phi_r, teuk=teuk, ylms=ylms,
+                        m=amp.m_arr[keep], n=amp.n_arr[keep], f_phi=f_phi, f_r=f_r)
         t, p, e, x, Phi_phi, Phi_theta, Phi_r = self.inspiral_generator(
             M, mu, 0.0, p0, e0, 1.0, Phi_phi0=Phi_phi0, Phi_r0=Phi_r0, T=T)
         if mode_selection is not None:
@@ -106,6 +154,23 @@ class FastSchwarzschildEccentricFlux:
                     m=amp.m_arr[keep], n=amp.n_arr[keep],
                     f_phi=om_phi / (2.0 * np.pi * M * MTSUN_SI),
                     f_r=om_r / (2.0 * np.pi * M * MTSUN_SI))
+
+    def prefetch(self, calls):
+        """Run the host upstream of several sources at once: `calls` are prepare() argument
+        tuples (M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps). The native parts
+        release the GIL, so a thread pool works a walker batch in parallel; the results are held
+        for the prepare() calls that follow (each taken once)."""
+        calls = [tuple(c) for c in calls]
+        for c in calls:                       # Ylm per viewing angle before the threads start
+            self._ylms(c[4], c[5])
+        res = list(_pool().map(lambda c: self.prepare(*c), calls))
+        with self._lock:
+            if len(self._prefetched) > 4096:   # results nobody took (e.g. after an exception)
+                self._prefetched.clear()
+            for c, r in zip(calls, res):
+                key = tuple(float(v) for v in c[:11]) + (True,)
+                self._prefetched[key] = r
+        return len(res)
 
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
@@ -172,6 +237,19 @@ class FastSchwarzschildEccentricFlux:
 
 
 _WAVEFORMS = {"FastSchwarzschildEccentricFlux": FastSchwarzschildEccentricFlux}
+_POOL = None
+
+
+def _pool():
+    """Threads for the host upstream of walker batches (its native parts release the GIL);
+    sized to this process's CPU share, at most 16."""
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        n = len(os.sched_getaffinity(0))
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16)
+        _POOL = ThreadPoolExecutor(max_workers=max(1, n), thread_name_prefix="efd-upstream")
+    return _POOL
 
 
 class GenerateEMRIWaveform:
@@ -222,6 +300,21 @@ class GenerateEMRIWaveform:
             rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
         return gen.submit_channels(pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0,
                                    Phi_r0, extra_scale=rot, **kwargs)
+
+    def prefetch(self, params, T=1.0, dt=10.0, eps=1e-5, mode_selection=None,
+                 include_minus_m=True, **kwargs):
+        """The host upstream of a batch of 14-parameter sets at once (thread pool; see
+        FastSchwarzschildEccentricFlux.prefetch); later calls with the same parameters and
+        kwargs take the results. Only for the FD generator without an explicit mode list."""
+        gen = self.waveform_generator
+        if gen.output_type != "fd" or mode_selection is not None or not include_minus_m:
+            return 0
+        calls = []
+        for prm in np.asarray(params, dtype=np.float64):
+            M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
+            theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
+            calls.append((M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps))
+        return gen.prefetch(calls)
 
     def fill_channels(self, out, *params, k0=None, **kwargs):
         """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).

@@ -285,6 +285,35 @@ int efd_cpu_threads(int n);
 /* Last error message of the calling thread's CPU-twin call. */
 int efd_cpu_last_error(char* buf, int len);
 
+/*
+ * Host upstream of the hot path (csrc/emrifd_host.cpp): STAND-IN PHYSICS, NOT FEW (FEW's flux
+ * and amplitude data are absent offline). The C++ form of the package's Python stand-ins, with
+ * the same equations and integrator (scipy RK45's Dormand-Prince 5(4), step control, dense
+ * output and terminal separatrix event). Host pointers, synchronous, thread-safe.
+ *
+ * efd_host_trajectory <- EMRIInspiral(func="SchwarzEccFlux")(M, mu, 0, p0, e0, 1, T=T)
+ *   (check_mode_by_mode.py:34-35): Peters-Mathews fluxes, exact Schwarzschild frequencies; knots
+ *   t [s], p, e, Phi_phi, Phi_r and (optional, NULL to skip) f_phi, f_r = Omega / (2 pi M
+ *   MTSUN_SI) [Hz], at most max_len (EFD_ERR_WORKSPACE beyond); *nt = knot count.
+ * efd_host_p_at_t <- few.utils.utility.get_p_at_t (check_mode_by_mode.py:200-212): p0 whose
+ *   inspiral plunges after t_out years (Brent; bracket [lo, hi], <= 0 for the defaults).
+ * efd_host_modes <- RomanAmplitude + ModeSelector(eps) (notebook :125-127): the synthetic
+ *   amplitude model over the given mode list (l, m, n, seeded phase0 and jitter), selection of
+ *   the modes holding (1 - eps) of |A Y|^2 at every knot (+m and -m partner branches, union over
+ *   knots) into keep[*nkeep]; with teuk != NULL also their complex amplitudes [nt][*nkeep]
+ *   (EFD_ERR_WORKSPACE when 2 nt nkeep > teuk_cap doubles).
+ */
+int efd_host_trajectory(double M, double mu, double p0, double e0, double Phi_phi0, double Phi_r0,
+                        double T, double rtol, double atol, int32_t max_len, double* t, double* p,
+                        double* e, double* phi_phi, double* phi_r, double* f_phi, double* f_r,
+                        int32_t* nt);
+int efd_host_p_at_t(double M, double mu, double e0, double t_out, double rtol, double atol,
+                    double xtol, double rtol_root, double lo, double hi, double* p0);
+int efd_host_modes(const double* p, const double* e, int32_t nt, const int32_t* l,
+                   const int32_t* m, const int32_t* n, const double* phase0, const double* jitter,
+                   int32_t nmodes, const double* ylm_p, const double* ylm_m, double eps,
+                   int32_t* keep, int32_t* nkeep, double* teuk, int64_t teuk_cap);
+
 #ifdef __cplusplus
 }
 #endif
