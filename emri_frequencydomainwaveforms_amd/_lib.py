@@ -28,6 +28,8 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_workspace_bytes",
     "efd_modesum",
     "efd_modesum_prepare",
+    "efd_modesum_prepare_batch",
+    "efd_modesum_status_batch",
     "efd_modesum_sum",
     "efd_modesum_sum_batch",
     "efd_modesum_sum_loglike",
@@ -153,6 +155,10 @@ def load(path=None):
         if hasattr(lib, name):   # absent only in older experiment builds
             getattr(lib, name).restype = ctypes.c_int
             getattr(lib, name).argtypes = [ctypes.POINTER(ModesumArgs), vp, sz, vp]
+    if hasattr(lib, "efd_modesum_prepare_batch"):
+        lib.efd_modesum_prepare_batch.restype = ctypes.c_int
+        lib.efd_modesum_prepare_batch.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
+                                                  ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp]
     if hasattr(lib, "efd_modesum_sum_batch"):
         lib.efd_modesum_sum_batch.restype = ctypes.c_int
         lib.efd_modesum_sum_batch.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
@@ -164,6 +170,9 @@ def load(path=None):
                                                 vp, vp, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
     lib.efd_modesum_status.argtypes = [vp, vp]
+    if hasattr(lib, "efd_modesum_status_batch"):
+        lib.efd_modesum_status_batch.restype = ctypes.c_int
+        lib.efd_modesum_status_batch.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(i32), vp]
     lib.efd_modesum_contributions.restype = ctypes.c_int
     lib.efd_modesum_contributions.argtypes = [vp, ctypes.POINTER(i64), vp]
     if hasattr(lib, "efd_modesum_stats"):   # absent only in pre-grouping experiment builds

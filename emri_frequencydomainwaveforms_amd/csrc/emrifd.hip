@@ -45,6 +45,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -182,9 +183,11 @@ struct Layout {
     int64_t ntiles, nlanes;
 };
 
-inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
+// (also evaluated on the device by the batched preparation kernels: a few dozen scalar integer
+// operations per workgroup, so the kernel arguments carry one workspace pointer per waveform)
+__host__ __device__ inline Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     Layout L{};
     const int64_t ni = nt - 1;
     L.nlanes = paired ? (nf + 1) / 2 : nf;
@@ -228,6 +231,34 @@ Layout make_layout(int32_t nt, int32_t K, int64_t nf, int paired) {
     L.total = off;
     return L;
 }
+
+// Preparation of up to EFD_BATCH_MAX waveforms per launch (efd_modesum_prepare_batch; a single
+// efd_modesum_prepare is a batch of one): blockIdx.z picks the waveform, the grids are sized for
+// the batch's largest (nt, K), and each workgroup derives its waveform's workspace layout from
+// (nt, K, nf, paired). Every waveform of a batch shares nf and the grid's symmetry.
+struct PrepDesc {
+    const double *t, *phi_phi, *phi_r, *f_phi, *f_r, *amp, *ylm_p, *ylm_m, *freq;
+    const int32_t *m, *n;
+    char* ws;
+    double sc_re, sc_im;
+    int32_t nt, K;
+    int32_t lists;   // 1: prebuilt tile lists (k_tile_keys), 3: and cost-ordered dispatch
+    int32_t pad;
+};
+struct PrepBatch {
+    PrepDesc d[EFD_BATCH_MAX];
+    int64_t nf, nl, nl1;
+    int32_t paired, n;
+};
+static_assert(sizeof(PrepBatch) <= 3072, "kernel arguments stay well inside 4 KB");
+
+// the waveform of this workgroup: its descriptor and workspace layout
+#define PREP_WALKER(B)                                                   \
+    const PrepDesc& D = (B).d[blockIdx.z];                                \
+    const Layout L = make_layout(D.nt, D.K, (B).nf, (B).paired);          \
+    char* const W = D.ws
+template <class T>
+__device__ __forceinline__ T* ws_at(char* ws, size_t off) { return reinterpret_cast<T*>(ws + off); }
 
 // rows of scratch / knot data fetched per block ahead of the serial spline recurrences
 #ifndef EFD_SPLINE_PF
@@ -381,7 +412,7 @@ __device__ __forceinline__ void group_minmax(int& v_lo, int& v_hi, int* red, int
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) { red[wave * 4 + slot] = v_lo; red[16 + wave * 4 + slot] = v_hi; }
 }
-__global__ __launch_bounds__(256) void k_group(const int32_t* __restrict__ marr,
+__device__ __forceinline__ void group_body(const int32_t* __restrict__ marr,
                                                const int32_t* __restrict__ narr, int K,
                                                int32_t* __restrict__ gm, int32_t* __restrict__ gn,
                                                int32_t* __restrict__ gstart,
@@ -554,12 +585,25 @@ __global__ __launch_bounds__(256) void k_group(const int32_t* __restrict__ marr,
         hdr->groups = G;
     }
 }
+__global__ __launch_bounds__(256) void k_group(const int32_t* __restrict__ marr,
+                                               const int32_t* __restrict__ narr, int K,
+                                               int32_t* gm, int32_t* gn, int32_t* gstart,
+                                               int32_t* gmem, Header* hdr, double2* sctab_g,
+                                               unsigned long long* gkeys) {
+    group_body(marr, narr, K, gm, gn, gstart, gmem, hdr, sctab_g, gkeys);
+}
+__global__ __launch_bounds__(256) void k_group_b(const PrepBatch B) {
+    PREP_WALKER(B);
+    group_body(D.m, D.n, D.K, ws_at<int32_t>(W, L.gm), ws_at<int32_t>(W, L.gn),
+               ws_at<int32_t>(W, L.gstart), ws_at<int32_t>(W, L.gmem), ws_at<Header>(W, L.header),
+               ws_at<double2>(W, L.sctab), ws_at<unsigned long long>(W, L.gkeys));
+}
 
 // K0b: group amplitudes at the knots, one thread per (knot i, group g):
 //   Bp = sum_l y0_l A_l(t_i),  Bm = sum_l y1_l A_l(t_i),  y0 = -scale Y+,  y1 = conj(-scale Y-)
 // (y1 = 0 for m = 0: no partner), summed in ascending h. gamp is [nt][4K]: (Bp re, Bp im,
 // Bm re, Bm im) of group g at 4g. S = -h_nb(-f) * scale: the minus sign and scale live here.
-__global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ amp,
+__device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
                                                    const double* __restrict__ ylm_p,
                                                    const double* __restrict__ ylm_m, double sc_re,
                                                    double sc_im, const int32_t* __restrict__ gm,
@@ -588,6 +632,22 @@ __global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ am
     }
     double* o = gamp + (size_t)i * 4 * K + 4 * g;
     o[0] = bpr; o[1] = bpi; o[2] = bmr; o[3] = bmi;
+}
+__global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ amp,
+                                                   const double* __restrict__ ylm_p,
+                                                   const double* __restrict__ ylm_m, double sc_re,
+                                                   double sc_im, const int32_t* __restrict__ gm,
+                                                   const int32_t* __restrict__ gstart,
+                                                   const int32_t* __restrict__ gmem, int nt, int K,
+                                                   const Header* __restrict__ hdr,
+                                                   double* __restrict__ gamp) {
+    group_amp_body(amp, ylm_p, ylm_m, sc_re, sc_im, gm, gstart, gmem, nt, K, hdr, gamp);
+}
+__global__ __launch_bounds__(256) void k_group_amp_b(const PrepBatch B) {
+    PREP_WALKER(B);
+    group_amp_body(D.amp, D.ylm_p, D.ylm_m, D.sc_re, D.sc_im, ws_at<int32_t>(W, L.gm),
+                   ws_at<int32_t>(W, L.gstart), ws_at<int32_t>(W, L.gmem), D.nt, D.K,
+                   ws_at<Header>(W, L.header), ws_at<double>(W, L.gamp));
 }
 
 // ----------------------------------------------------------------------------------------
@@ -860,7 +920,7 @@ __device__ void inverse_splines(const double* __restrict__ t, const double* __re
 // chains on few workgroups, so running them side by side costs max() instead of sum().
 // Block 0: trajectory splines; blocks [1, 1 + nb_amp): amplitude splines (64 interpolants per
 // block); the rest: inverse splines (64 harmonics per block).
-__global__ __launch_bounds__(64) void k_prep(
+__device__ __forceinline__ void prep_body(
     const double* __restrict__ t, const double* __restrict__ phi_phi,
     const double* __restrict__ phi_r, const double* __restrict__ f_phi,
     const double* __restrict__ f_r, const double* __restrict__ gamp,
@@ -887,6 +947,30 @@ __global__ __launch_bounds__(64) void k_prep(
         inverse_splines(t, f_phi, f_r, gm, gn, nt, K, hdr->groups, runs, items, invcp, invdp,
                         &hdr->runs_overflow, b - 1 - nb_amp);
     }
+}
+__global__ __launch_bounds__(64) void k_prep(
+    const double* __restrict__ t, const double* __restrict__ phi_phi,
+    const double* __restrict__ phi_r, const double* __restrict__ f_phi,
+    const double* __restrict__ f_r, const double* __restrict__ gamp,
+    const int32_t* __restrict__ gm,
+    const int32_t* __restrict__ gn, int nt, int K,
+    int nb_amp, double* __restrict__ coefT, double* __restrict__ kslope,
+    double* __restrict__ tscratch, double* coefA, int32_t* __restrict__ runs,
+    Item* __restrict__ items, double* __restrict__ invcp, double* __restrict__ invdp,
+    Header* __restrict__ hdr) {
+    prep_body(t, phi_phi, phi_r, f_phi, f_r, gamp, gm, gn, nt, K, nb_amp, coefT, kslope, tscratch,
+              coefA, runs, items, invcp, invdp, hdr);
+}
+// the grid is sized for the batch's largest K: blocks past this waveform's roles leave at once
+__global__ __launch_bounds__(64) void k_prep_b(const PrepBatch B) {
+    PREP_WALKER(B);
+    const int nb_amp = (4 * D.K + 63) / 64, nb_inv = (D.K + 63) / 64;
+    if ((int)blockIdx.x >= 1 + nb_amp + nb_inv) return;
+    prep_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ws_at<double>(W, L.gamp),
+              ws_at<int32_t>(W, L.gm), ws_at<int32_t>(W, L.gn), D.nt, D.K, nb_amp,
+              ws_at<double>(W, L.coefT), ws_at<double>(W, L.kslope), ws_at<double>(W, L.tscratch),
+              ws_at<double>(W, L.coefA), ws_at<int32_t>(W, L.runs), ws_at<Item>(W, L.items),
+              ws_at<double>(W, L.invcp), ws_at<double>(W, L.invdp), ws_at<Header>(W, L.header));
 }
 
 __global__ __launch_bounds__(64) void k_spline_shared(const double* __restrict__ x, int n,
@@ -951,7 +1035,7 @@ __device__ void build_item(
 // K4: one thread per (group g, knot interval j). Counts both the SPA evaluations the kernel
 // makes (per group) and the reference formulation's contributions C (per (l, m, n) harmonic:
 // the group's evaluations times its member count).
-__global__ void k_items(const double* __restrict__ t, const double* __restrict__ f_phi,
+__device__ __forceinline__ void items_body(const double* __restrict__ t, const double* __restrict__ f_phi,
                         const double* __restrict__ f_r, const int32_t* __restrict__ gm,
                         const int32_t* __restrict__ gn, const int32_t* __restrict__ gstart,
                         int nt, int K, const double* __restrict__ coefA,
@@ -987,6 +1071,14 @@ __global__ void k_items(const double* __restrict__ t, const double* __restrict__
         if (c) atomicAdd((unsigned long long*)&hdr->contributions, c);
         if (e) atomicAdd((unsigned long long*)&hdr->evaluations, e);
     }
+}
+__global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
+    PREP_WALKER(B);
+    items_body(D.t, D.f_phi, D.f_r, ws_at<int32_t>(W, L.gm), ws_at<int32_t>(W, L.gn),
+               ws_at<int32_t>(W, L.gstart), D.nt, D.K, ws_at<double>(W, L.coefA),
+               ws_at<double>(W, L.coefT), ws_at<int32_t>(W, L.runs), D.freq, B.nf, B.paired, B.nl,
+               B.nl1, ws_at<Item>(W, L.items), ws_at<int4>(W, L.ranges),
+               ws_at<Header>(W, L.header));
 }
 
 // One interval record of group h; `evals` = its (branch x bin) evaluation count.
@@ -1111,7 +1203,7 @@ __device__ void build_item(
 // is deterministic.
 // seglh = (lo, hi) lane range; seginfo = (first record, count, dir, s).
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict__ runs,
+__device__ __forceinline__ void segment_slots_body(const int32_t* __restrict__ runs,
                                                        const int4* __restrict__ ranges, int nt,
                                                        int K, int lim0, int lim1,
                                                        const Header* __restrict__ hdr,
@@ -1181,6 +1273,17 @@ __global__ __launch_bounds__(256) void k_segment_slots(const int32_t* __restrict
         blocktiles[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
     }
 }
+// slot blocks of one waveform: (2 MAXRUNS K + 255) / 256; the grid has the batch's largest count
+__device__ __forceinline__ int slot_blocks(int K) { return (2 * MAXRUNS * K + 255) / 256; }
+__global__ __launch_bounds__(256) void k_segment_slots(const PrepBatch B) {
+    PREP_WALKER(B);
+    if ((int)blockIdx.x >= slot_blocks(D.K)) return;
+    segment_slots_body(ws_at<int32_t>(W, L.runs), ws_at<int4>(W, L.ranges), D.nt, D.K,
+                       (int)(B.paired ? B.nl : B.nf), (int)(B.paired ? B.nl1 : B.nf),
+                       ws_at<Header>(W, L.header), ws_at<int2>(W, L.slotlh),
+                       ws_at<int4>(W, L.slotinfo), ws_at<int32_t>(W, L.slotcnt),
+                       ws_at<int32_t>(W, L.slottiles));
+}
 
 // one workgroup per slot block: its output offset is the sum of the earlier blocks' counts
 // Segment-tile boundaries: segment s covers tiles [t0, t1] (t0 = lo / TILE_LANES); its
@@ -1191,7 +1294,7 @@ constexpr int32_t SEG_NO_STB = INT32_MIN;
 #ifndef EFD_STB
 #define EFD_STB 1   // 0: every segment takes the bisection (reference for the bitwise check)
 #endif
-__global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict__ slot_lh,
+__device__ __forceinline__ void segment_compact_body(const int2* __restrict__ slot_lh,
                                                          const int4* __restrict__ slot_info,
                                                          const int32_t* __restrict__ blockcnt,
                                                          const int32_t* __restrict__ blocktiles,
@@ -1199,7 +1302,7 @@ __global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict_
                                                          int2* __restrict__ seglh,
                                                          int4* __restrict__ seginfo,
                                                          int32_t* __restrict__ segbase,
-                                                         int32_t* __restrict__ nseg) {
+                                                         int32_t* __restrict__ nseg, int nblk) {
     __shared__ int wc[4];
     __shared__ int64_t wt[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1242,7 +1345,17 @@ __global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict_
         segbase[pos] = (EFD_STB && toff + ntl <= stbcap) ? (int32_t)(toff - lh.x / TILE_LANES)
                                                          : SEG_NO_STB;
     }
-    if (blk == (int)gridDim.x - 1 && tid == 0) *nseg = base + wc[0] + wc[1] + wc[2] + wc[3];
+    if (blk == nblk - 1 && tid == 0) *nseg = base + wc[0] + wc[1] + wc[2] + wc[3];
+}
+__global__ __launch_bounds__(256) void k_segment_compact(const PrepBatch B) {
+    PREP_WALKER(B);
+    const int nblk = slot_blocks(D.K);
+    if ((int)blockIdx.x >= nblk) return;
+    segment_compact_body(ws_at<int2>(W, L.slotlh), ws_at<int4>(W, L.slotinfo),
+                         ws_at<int32_t>(W, L.slotcnt), ws_at<int32_t>(W, L.slottiles),
+                         2 * MAXRUNS * D.K, L.stbcap, ws_at<int2>(W, L.seglh),
+                         ws_at<int4>(W, L.seginfo), ws_at<int32_t>(W, L.segbase),
+                         ws_at<int32_t>(W, L.nseg), nblk);
 }
 
 // One workgroup per segment (grid-stride): for every record p of the segment in lane order
@@ -1251,7 +1364,7 @@ __global__ __launch_bounds__(256) void k_segment_compact(const int2* __restrict_
 // klo >= (t+1)*TL). Lane ranges are monotone in p, so each tile gets exactly one of each: the
 // same answers as k_modesum's bisection, from two loads instead of ~2 log2(n) dependent ones.
 __device__ __forceinline__ int div_floor_nn(int64_t a) { return (int)(a / TILE_LANES); }   // a >= 0
-__global__ __launch_bounds__(256) void k_seg_tiles(const int4* __restrict__ ranges,
+__device__ __forceinline__ void seg_tiles_body(const int4* __restrict__ ranges,
                                                    const int2* __restrict__ seglh,
                                                    const int4* __restrict__ seginfo,
                                                    const int32_t* __restrict__ segbase,
@@ -1283,6 +1396,12 @@ __global__ __launch_bounds__(256) void k_seg_tiles(const int4* __restrict__ rang
             for (int t = max(a, t0); t <= min(b, t1); ++t) stb1[sbase + t] = p;
         }
     }
+}
+__global__ __launch_bounds__(256) void k_seg_tiles(const PrepBatch B) {
+    PREP_WALKER(B);
+    seg_tiles_body(ws_at<int4>(W, L.ranges), ws_at<int2>(W, L.seglh), ws_at<int4>(W, L.seginfo),
+                   ws_at<int32_t>(W, L.segbase), ws_at<int32_t>(W, L.nseg),
+                   ws_at<int32_t>(W, L.stb0), ws_at<int32_t>(W, L.stb1));
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2711,6 +2830,25 @@ struct LlBatch {
     int64_t ntiles;
     int32_t n;
 };
+// efd_modesum_status_batch: each workspace's error flags (bit 0 runs_overflow, 1 bad_mn,
+// 2 bad_tile) into out[i], and the reported flags cleared (sticky until reported; see Header)
+struct StatusBatch {
+    Header* h[EFD_BATCH_MAX];
+    int32_t n;
+};
+__global__ __launch_bounds__(64) void k_status_gather(const StatusBatch sb, int32_t* out) {
+    const int i = threadIdx.x;
+    if (i >= sb.n) return;
+    Header* h = sb.h[i];
+    const int32_t f = (h->runs_overflow ? 1 : 0) | (h->bad_mn ? 2 : 0) | (h->bad_tile ? 4 : 0);
+    out[i] = f;
+    if (f) {
+        h->runs_overflow = 0;
+        h->bad_mn = 0;
+        h->bad_tile = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
     __shared__ double red[256];
     const double* p = lb.part[blockIdx.x];
@@ -2738,7 +2876,7 @@ __global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
 // KEYCAP keys get tcnt = -1 and build in the sum.
 constexpr int TK_HITS = TILE;
 constexpr int TK_ROWS = 8;   // windows of the segment table per barrier
-__global__ __launch_bounds__(TILE) void k_tile_keys(
+__device__ __forceinline__ void tile_keys_body(
     const int4* __restrict__ ranges, const int2* __restrict__ seglh,
     const int4* __restrict__ seginfo, const int32_t* __restrict__ nsegp,
     const int32_t* __restrict__ segbase, const int32_t* __restrict__ stb0,
@@ -2893,6 +3031,14 @@ __global__ __launch_bounds__(TILE) void k_tile_keys(
     }
     if (tid == 0) tcnt[tile] = total;
 }
+__global__ __launch_bounds__(TILE) void k_tile_keys(const PrepBatch B) {
+    PREP_WALKER(B);
+    if (D.lists == 0) return;
+    tile_keys_body(ws_at<int4>(W, L.ranges), ws_at<int2>(W, L.seglh), ws_at<int4>(W, L.seginfo),
+                   ws_at<int32_t>(W, L.nseg), ws_at<int32_t>(W, L.segbase),
+                   ws_at<int32_t>(W, L.stb0), ws_at<int32_t>(W, L.stb1), L.ntiles,
+                   ws_at<uint32_t>(W, L.tkeys), ws_at<int32_t>(W, L.tcnt));
+}
 #undef EFD_MODESUM_PARAMS
 #undef EFD_MODESUM_ARGS
 
@@ -2927,8 +3073,8 @@ __device__ __forceinline__ int wave_bucket_add(int* hist, int bucket, bool valid
     }
     return res;
 }
-__global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__ tcnt,
-                                                     int64_t ntiles, int32_t* __restrict__ tperm) {
+__device__ __forceinline__ void tile_order_body(const int32_t* __restrict__ tcnt,
+                                                int64_t ntiles, int32_t* __restrict__ tperm) {
     __shared__ int hist[ORDER_BUCKETS];
     const int tid = threadIdx.x;
     if (tid < ORDER_BUCKETS) hist[tid] = 0;
@@ -2969,6 +3115,11 @@ __global__ __launch_bounds__(1024) void k_tile_order(const int32_t* __restrict__
         const int pos = wave_bucket_add(hist, bkt, i < ntiles);
         if (i < ntiles) tperm[pos] = (int32_t)i;
     }
+}
+__global__ __launch_bounds__(1024) void k_tile_order(const PrepBatch B) {
+    PREP_WALKER(B);
+    if (D.lists != 3) return;
+    tile_order_body(ws_at<int32_t>(W, L.tcnt), L.ntiles, ws_at<int32_t>(W, L.tperm));
 }
 
 // ----------------------------------------------------------------------------------------
@@ -3327,7 +3478,123 @@ static int check_modesum_args(const efd_modesum_args* a, const void* workspace, 
     return EFD_OK;
 }
 
-// phase: 1 = prepare (K0-K5), 2 = sum (K8), 3 = both
+// Preparation (K0-K6) of `count` waveforms in one chain of launches; blockIdx.z = waveform.
+// efd_modesum_prepare and efd_modesum's first phase are a batch of one.
+static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
+                              void* const* workspace, const size_t* workspace_bytes,
+                              int32_t count, void* stream) {
+    const std::string F(fn);
+    if (!a || !workspace || !workspace_bytes) return fail(EFD_ERR_ARG, F + ": NULL argument");
+    if (count < 1 || count > EFD_BATCH_MAX)
+        return fail(EFD_ERR_ARG, F + ": count out of range [1, EFD_BATCH_MAX]");
+    PrepBatch B{};
+    B.n = count;
+    int ntmax = 0, Kmax = 0, nimax = 0;
+    int64_t items_max = 0, ntiles = 0;
+    bool any_lists = false, any_order = false;
+    for (int i = 0; i < count; ++i) {
+        const efd_modesum_args* ai = a[i];
+        const int rc = check_modesum_args(ai, workspace[i], 1);
+        if (rc != EFD_OK) return rc;
+        if (ai->nf != a[0]->nf || (ai->grid_symmetric != 0) != (a[0]->grid_symmetric != 0))
+            return fail(EFD_ERR_ARG, F + ": nf and grid_symmetric must agree across the batch");
+        const int paired = ai->grid_symmetric ? 1 : 0;
+        const Layout L = make_layout(ai->nt, ai->K, ai->nf, paired);
+        if (workspace_bytes[i] < L.total)
+            return fail(EFD_ERR_WORKSPACE, F + ": workspace too small (see "
+                                               "efd_modesum_workspace_bytes)");
+        for (int j = 0; j < i; ++j)
+            if (workspace[j] == workspace[i])
+                return fail(EFD_ERR_ARG, F + ": one workspace per waveform");
+        PrepDesc& d = B.d[i];
+        d.t = ai->t; d.phi_phi = ai->phi_phi; d.phi_r = ai->phi_r; d.f_phi = ai->f_phi;
+        d.f_r = ai->f_r; d.amp = ai->amp; d.ylm_p = ai->ylm_p; d.ylm_m = ai->ylm_m;
+        d.freq = ai->freq; d.m = ai->m; d.n = ai->n;
+        d.ws = (char*)workspace[i];
+        d.sc_re = ai->scale_re; d.sc_im = ai->scale_im;
+        d.nt = ai->nt; d.K = ai->K;
+        d.lists = use_prebuilt(ai->K) ? (use_cost_order(L, ai->K) ? 3 : 1) : 0;
+        any_lists |= d.lists != 0;
+        any_order |= d.lists == 3;
+        ntmax = std::max(ntmax, ai->nt);
+        Kmax = std::max(Kmax, ai->K);
+        nimax = std::max(nimax, ai->nt - 1);
+        items_max = std::max(items_max, (int64_t)(ai->nt - 1) * ai->K);
+        if (i == 0) {
+            B.paired = paired;
+            B.nf = ai->nf;
+            B.nl = L.nlanes;
+            B.nl1 = paired ? ((ai->nf % 2) ? L.nlanes - 1 : L.nlanes) : ai->nf;
+            ntiles = L.ntiles;
+        }
+    }
+    (void)nimax;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned nz = (unsigned)count;
+#ifdef EFD_EXP_SKIP   // diagnostic: after the warm-up, skip preparation kernels (bit mask: 1 groups,
+    // 2 k_prep, 4 k_items, 8 segment table, 16 k_tile_keys, 32 k_tile_order); valid only when
+    // every call repeats the same inputs on workspaces that already hold their results
+    static int exp_calls = 0;
+    const int skip = ++exp_calls > 16 ? EFD_EXP_SKIP : 0;
+#else
+    constexpr int skip = 0;
+#endif
+    // K0: (m, n) groups and their amplitudes at the knots
+    if (!(skip & 1)) {
+        hipLaunchKernelGGL(k_group_b, dim3(1, 1, nz), dim3(256), 0, st, B);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax + 255) / 256, ntmax, nz), dim3(256), 0, st,
+                           B);
+        HIP_TRY(hipGetLastError());
+    }
+    // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
+    // grids sized for G = K, blocks past the device-side G return at once)
+    if (!(skip & 2)) {
+        const int nb = 1 + (4 * Kmax + 63) / 64 + (Kmax + 63) / 64;
+        hipLaunchKernelGGL(k_prep_b, dim3(nb, 1, nz), dim3(64), sizeof(double) * 7 * ntmax, st,
+                           B);
+        HIP_TRY(hipGetLastError());
+#ifdef EFD_EXP_PREP_ROLE
+        return EFD_OK;   // timing experiment: the later stages would read partial data
+#endif
+    }
+    // K4: interval records
+    if (!(skip & 4)) {
+        const int64_t blocks = (items_max + 255) / 256;
+        hipLaunchKernelGGL(k_items, dim3((unsigned)blocks, 1, nz), dim3(256), 0, st, B);
+        HIP_TRY(hipGetLastError());
+    }
+    // K5: segment table
+    if (!(skip & 8)) {
+        const int nslot = Kmax * MAXRUNS * 2;
+        const int nblk = (nslot + 255) / 256;
+        hipLaunchKernelGGL(k_segment_slots, dim3(nblk, 1, nz), dim3(256), 0, st, B);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_segment_compact, dim3(nblk, 1, nz), dim3(256), 0, st, B);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_seg_tiles, dim3((unsigned)std::min(nslot, 1024), 1, nz), dim3(256),
+                           0, st, B);
+        HIP_TRY(hipGetLastError());
+    }
+#if EFD_PREBUILT_LISTS
+    // K6: the tiles' record lists (k_tile_keys): moves the latency-bound build out of the mode
+    // sum into the preparation phase, which overlaps the previous waveform's sum in a two-stream
+    // pipeline
+    if (!(skip & 16) && any_lists) {
+        hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)ntiles, 1, nz), dim3(TILE), 0, st, B);
+        HIP_TRY(hipGetLastError());
+    }
+#if EFD_COST_ORDER
+    if (!(skip & 32) && any_order) {
+        hipLaunchKernelGGL(k_tile_order, dim3(1, 1, nz), dim3(1024), 0, st, B);
+        HIP_TRY(hipGetLastError());
+    }
+#endif
+#endif
+    return EFD_OK;
+}
+
+// phase: 1 = prepare (K0-K6), 2 = sum (K8), 3 = both
 static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
                         void* stream, int phase) {
     {
@@ -3342,116 +3609,30 @@ static int modesum_impl(const efd_modesum_args* a, void* workspace, size_t works
     hipStream_t st = (hipStream_t)stream;
     char* ws = (char*)workspace;
     Header* hdr = (Header*)(ws + L.header);
-    double* coefA = (double*)(ws + L.coefA);
-    double* coefT = (double*)(ws + L.coefT);
-    double* kslope = (double*)(ws + L.kslope);
-    double* invcp = (double*)(ws + L.invcp);
-    double* invdp = (double*)(ws + L.invdp);
-    int32_t* runs = (int32_t*)(ws + L.runs);
-    Item* items = (Item*)(ws + L.items);
-    int4* ranges = (int4*)(ws + L.ranges);
-    int2* seglh = (int2*)(ws + L.seglh);
-    int4* seginfo = (int4*)(ws + L.seginfo);
-    int32_t* nseg = (int32_t*)(ws + L.nseg);
-    int32_t* gm = (int32_t*)(ws + L.gm);
-    int32_t* gn = (int32_t*)(ws + L.gn);
-    int32_t* gstart = (int32_t*)(ws + L.gstart);
-    int32_t* gmem = (int32_t*)(ws + L.gmem);
-    double* gamp = (double*)(ws + L.gamp);
-    double2* sctab_g = (double2*)(ws + L.sctab);
-    uint32_t* tkeys = (uint32_t*)(ws + L.tkeys);
+    const Item* items = (const Item*)(ws + L.items);
+    const int4* ranges = (const int4*)(ws + L.ranges);
+    const int2* seglh = (const int2*)(ws + L.seglh);
+    const int4* seginfo = (const int4*)(ws + L.seginfo);
+    const int32_t* nseg = (const int32_t*)(ws + L.nseg);
+    const int32_t* gm = (const int32_t*)(ws + L.gm);
+    const int32_t* gn = (const int32_t*)(ws + L.gn);
+    const double* coefA = (const double*)(ws + L.coefA);
+    const double* coefT = (const double*)(ws + L.coefT);
+    const double2* sctab_g = (const double2*)(ws + L.sctab);
+    const uint32_t* tkeys = (const uint32_t*)(ws + L.tkeys);
     int32_t* tcnt = (int32_t*)(ws + L.tcnt);
-    int32_t* segbase = (int32_t*)(ws + L.segbase);
-    int32_t* stb0 = (int32_t*)(ws + L.stb0);
-    int32_t* stb1 = (int32_t*)(ws + L.stb1);
-
+    const int32_t* segbase = (const int32_t*)(ws + L.segbase);
+    const int32_t* stb0 = (const int32_t*)(ws + L.stb0);
+    const int32_t* stb1 = (const int32_t*)(ws + L.stb1);
     const int nt = a->nt, K = a->K;
     const int64_t nf = a->nf;
     const int64_t nl = L.nlanes;
-    const int64_t nl1 = paired ? ((nf % 2) ? nl - 1 : nl) : nf;
 
     if (phase & 1) {
-#ifdef EFD_EXP_SKIP   // diagnostic: after the warm-up, skip preparation kernels (bit mask: 1 groups,
-    // 2 k_prep, 4 k_items, 8 segment table, 16 k_tile_keys, 32 k_tile_order); valid only when
-    // every call repeats the same inputs on workspaces that already hold their results
-    static int exp_calls = 0;
-    const int skip = ++exp_calls > 16 ? EFD_EXP_SKIP : 0;
-#else
-    constexpr int skip = 0;
-#endif
-    if (!(skip & 1)) {
-
-    // K0: (m, n) groups
-    hipLaunchKernelGGL(k_group, dim3(1), dim3(256), 0, st, a->m, a->n, K, gm, gn, gstart, gmem,
-                       hdr, sctab_g, (unsigned long long*)(ws + L.gkeys));
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_group_amp, dim3((K + 255) / 256, nt), dim3(256), 0, st, a->amp, a->ylm_p,
-                       a->ylm_m, a->scale_re, a->scale_im, gm, gstart, gmem, nt, K, hdr, gamp);
-    HIP_TRY(hipGetLastError());
+        const int rc = prepare_batch_impl("efd_modesum_prepare", &a, &workspace, &workspace_bytes,
+                                          1, stream);
+        if (rc != EFD_OK) return rc;
     }
-    // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
-    // grids sized for G = K, blocks past the device-side G return at once)
-    if (!(skip & 2)) {
-        const int nb_amp = (4 * K + 63) / 64;
-        const int nb_inv = (K + 63) / 64;
-        hipLaunchKernelGGL(k_prep, dim3(1 + nb_amp + nb_inv), dim3(64), sizeof(double) * 7 * nt, st,
-                           a->t, a->phi_phi, a->phi_r, a->f_phi, a->f_r, gamp, gm, gn, nt, K,
-                           nb_amp, coefT, kslope, (double*)(ws + L.tscratch), coefA, runs, items,
-                           invcp, invdp, hdr);
-        HIP_TRY(hipGetLastError());
-#ifdef EFD_EXP_PREP_ROLE
-        return EFD_OK;   // timing experiment: the later stages would read partial data
-#endif
-    }
-    // K4: interval records
-    if (!(skip & 4)) {
-        const int64_t total = (int64_t)(nt - 1) * K;
-        const int threads = 256;
-        const int64_t blocks = (total + threads - 1) / threads;
-        hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(threads), 0, st, a->t, a->f_phi,
-                           a->f_r, gm, gn, gstart, nt, K, coefA, coefT, runs, a->freq, nf, paired,
-                           nl, nl1, items, ranges, hdr);
-        HIP_TRY(hipGetLastError());
-    }
-    // K5: segment table
-    if (!(skip & 8)) {
-        const int nslot = K * MAXRUNS * 2;
-        int2* slot_lh = (int2*)(ws + L.slotlh);
-        int4* slot_info = (int4*)(ws + L.slotinfo);
-        const int nblk = (nslot + 255) / 256;
-        int32_t* blockcnt = (int32_t*)(ws + L.slotcnt);
-        int32_t* blocktiles = (int32_t*)(ws + L.slottiles);
-        hipLaunchKernelGGL(k_segment_slots, dim3(nblk), dim3(256), 0, st, runs, ranges, nt, K,
-                           (int)(paired ? nl : nf), (int)(paired ? nl1 : nf), hdr, slot_lh,
-                           slot_info, blockcnt, blocktiles);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_segment_compact, dim3(nblk), dim3(256), 0, st, slot_lh, slot_info,
-                           blockcnt, blocktiles, nslot, L.stbcap, seglh, seginfo, segbase, nseg);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_seg_tiles, dim3((unsigned)std::min(nslot, 1024)), dim3(256), 0, st,
-                           ranges, seglh, seginfo, segbase, nseg, stb0, stb1);
-    }
-    HIP_TRY(hipGetLastError());
-#if EFD_PREBUILT_LISTS
-    // K6: the tiles' record lists (k_tile_keys): moves the latency-bound build out of the mode
-    // sum into the preparation phase, which overlaps the previous waveform's sum in a two-stream
-    // pipeline
-    {
-        const dim3 block(TILE);
-        if (!(skip & 16) && use_prebuilt(K))
-        hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)L.ntiles), block, 0, st, ranges, seglh,
-                           seginfo, nseg, segbase, stb0, stb1, L.ntiles, tkeys, tcnt);
-        HIP_TRY(hipGetLastError());
-#if EFD_COST_ORDER
-        if (use_cost_order(L, K) && !(skip & 32)) {
-            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, tcnt, L.ntiles,
-                               (int32_t*)(ws + L.tperm));
-            HIP_TRY(hipGetLastError());
-        }
-#endif
-    }
-#endif
-    }  // phase 1
     // K8: mode sum
     if (phase & 2) {
         const int64_t gq = 8 * XCD_GROUP;
@@ -3488,6 +3669,12 @@ int efd_modesum(const efd_modesum_args* a, void* workspace, size_t workspace_byt
 int efd_modesum_prepare(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
                         void* stream) {
     return modesum_impl(a, workspace, workspace_bytes, stream, 1);
+}
+
+int efd_modesum_prepare_batch(const efd_modesum_args* const* a, void* const* workspace,
+                              const size_t* workspace_bytes, int32_t count, void* stream) {
+    return prepare_batch_impl("efd_modesum_prepare_batch", a, workspace, workspace_bytes, count,
+                              stream);
 }
 
 int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace_bytes,
@@ -3622,6 +3809,44 @@ int efd_modesum_status(const void* workspace, void* stream) {
         return fail(EFD_ERR_HIP, "efd_modesum: a tile dispatch-order entry was out of range "
                                  "(prepare/sum workspace mismatch?); bins were left unwritten");
     return EFD_OK;
+}
+
+int efd_modesum_status_batch(void* const* workspace, int32_t count, int32_t* flags,
+                             void* stream) {
+    if (!workspace || count < 1 || count > EFD_BATCH_MAX)
+        return fail(EFD_ERR_ARG, "efd_modesum_status_batch: NULL workspaces or count out of "
+                                 "range [1, EFD_BATCH_MAX]");
+    StatusBatch sb{};
+    sb.n = count;
+    for (int i = 0; i < count; ++i) {
+        if (!workspace[i]) return fail(EFD_ERR_ARG, "efd_modesum_status_batch: NULL workspace");
+        sb.h[i] = (Header*)workspace[i];
+    }
+    // one gather kernel writing into mapped host memory, one synchronisation: the flags of a
+    // walker batch cost what one efd_modesum_status costs
+    static std::mutex mu;
+    static int32_t* host = nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!host) HIP_TRY(hipHostMalloc((void**)&host, sizeof(int32_t) * EFD_BATCH_MAX,
+                                     hipHostMallocMapped));
+    int32_t* dev = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&dev, host, 0));
+    hipLaunchKernelGGL(k_status_gather, dim3(1), dim3(64), 0, (hipStream_t)stream, sb, dev);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    int first = -1;
+    for (int i = 0; i < count; ++i) {
+        const int32_t f = ((volatile int32_t*)host)[i];
+        if (flags) flags[i] = f;
+        if (f && first < 0) first = i;
+    }
+    if (first < 0) return EFD_OK;
+    const int32_t f = host[first];
+    const std::string w = "efd_modesum (waveform " + std::to_string(first) + " of the batch): ";
+    if (f & 1) return fail(EFD_ERR_ARG, w + "a harmonic has more than 8 monotonic runs");
+    if (f & 2) return fail(EFD_ERR_ARG, w + "|m| > 255 or |n| > 1023");
+    return fail(EFD_ERR_HIP, w + "a tile dispatch-order entry was out of range (prepare/sum "
+                                 "workspace mismatch?); bins were left unwritten");
 }
 
 int efd_modesum_contributions(const void* workspace, int64_t* contributions, void* stream) {

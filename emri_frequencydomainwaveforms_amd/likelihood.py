@@ -217,63 +217,58 @@ class Likelihood:
             return out
         return out.cpu().numpy()
 
-    # walkers per fused launch, and the fused path's WaveformPipeline slots (at least two
-    # groups): small groups keep the next walkers' preparation beside the current sum (one
-    # group of 8 waited for all 8 preparations: config 4 3,222 vs 3,977 logL/s unfused); 3 and
-    # 6 slots measured best (configs 4 / 5: 4,936 / 7,015 vs 4,122 / 3,545 unfused, same box)
-    FUSED_GROUP = 3
-    FUSED_SLOTS = 4
+    # walkers per fused group: one efd_modesum_prepare_batch and one efd_modesum_sum_loglike
+    # each; FUSED_DEPTH groups rotate so group i+1's preparation runs beside group i's sum
+    FUSED_GROUP = 8
+    FUSED_DEPTH = 2
 
     def _get_ll_fused(self, tm, params, args, kwargs, out):
-        """The pipelined path with the likelihood fused into the mode sum: each walker's upload
-        and preparation on a WaveformPipeline slot, then per group of FUSED_GROUP walkers one
-        efd_modesum_sum_loglike on a sum stream writing their log-likelihoods into out (the
-        templates never reach HBM). Slots are reused only after the sum that read them (an event
-        per group). Returns False, before queueing anything, when the template's grid is not
-        symmetric (the caller takes the per-walker path)."""
+        """The pipelined path with the likelihood fused into the mode sum: per group of
+        FUSED_GROUP walkers, the template chain collects each walker's host inputs
+        (BatchPreparer), one upload and one efd_modesum_prepare_batch prepare the group on its
+        stream, and one efd_modesum_sum_loglike on a sum stream writes the group's
+        log-likelihoods into out (the templates never reach HBM). A group's workspaces are reused
+        only after the sum that read them (an event per group). Returns False, before queueing
+        anything, when the template's grid is not symmetric (the caller takes the per-walker
+        path)."""
         torch = self.torch
-        from .summation import WaveformPipeline, sum_batch_loglike
+        from .summation import BatchPreparer, sum_batch_loglike
         if not self._fused_grid_ok(tm, kwargs):
             return False
         if hasattr(tm, "prefetch"):
             tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
-        G = self.FUSED_GROUP
+        n = len(params)
+        ngroups = -(-n // self.FUSED_GROUP)
+        G = -(-n // ngroups)                       # balanced groups of at most FUSED_GROUP
         caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),
                                   "create_waveform", None), "caustic", "uniform")
         F = self._fused
-        ns = max(2 * G, self.FUSED_SLOTS)
-        if F is None or F["pipe"].caustic != caustic or F["pipe"].num_slots != ns:
-            F = self._fused = dict(pipe=WaveformPipeline(ns, caustic=caustic, device=self.device),
-                                   stream=torch.cuda.Stream(self.device), busy=[None] * ns)
-        P, s_sum = F["pipe"], F["stream"]
+        if F is None or F["prep"].caustic != caustic or F["prep"].group < G:
+            F = self._fused = dict(prep=BatchPreparer(max(G, self.FUSED_GROUP), self.FUSED_DEPTH,
+                                                      caustic=caustic, device=self.device),
+                                   stream=torch.cuda.Stream(self.device))
+        B, s_sum = F["prep"], F["stream"]
         cur = torch.cuda.current_stream(self.device)
-        P.order_after_current()
+        B.order_after_current()
         s_sum.wait_stream(cur)
-        n = len(params)
         try:
             for g0 in range(0, n, G):
-                used, jobs = [], []
                 for i in range(g0, min(n, g0 + G)):
-                    j = P.next_slot()
-                    if F["busy"][j] is not None:   # the slot's previous sum has read its workspace
-                        P.stream(j).wait_event(F["busy"][j])
-                    slot = tm.submit(P, None, *params[i], *args, order=False, prepare_only=True,
-                                     **kwargs)
-                    used.append(slot)
-                    jobs.append(P.job(slot))
-                for slot in used:
-                    s_sum.wait_stream(P.stream(slot))
-                sum_batch_loglike(jobs, self._d, self._w_templ, out[g0:g0 + len(used)],
+                    tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
+                              **kwargs)
+                gi, jobs = B.flush()
+                s_sum.wait_stream(B.stream(gi))
+                sum_batch_loglike(jobs, self._d, self._w_templ, out[g0:g0 + len(jobs)],
                                   stream=s_sum.cuda_stream)
                 ev = torch.cuda.Event()
                 ev.record(s_sum)
-                for slot in used:
-                    F["busy"][slot] = ev
+                B.release(gi, ev)
         finally:
+            B._pending = []
             # `out` belongs to the current stream: nothing may still write it when it is
             # returned, or freed after an exception
             s_sum.synchronize()
-        P.wait()   # device-side errors of every slot's workspace (sticky across slot reuse)
+        B.wait()   # device-side errors of every group's workspaces (sticky across reuse)
         cur.wait_stream(s_sum)
         return True
 

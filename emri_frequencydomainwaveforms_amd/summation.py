@@ -264,8 +264,17 @@ def sum_batch(jobs, stream=None, prof_events=(None, None)):
         raise ValueError(f"sum_batch takes 1..{_lib.EFD_BATCH_MAX} waveforms")
     args, wss = [], []
     for i, (eng, kw) in enumerate(jobs):
-        kw = {k: v for k, v in kw.items() if k != "_args"}
-        a, ws = eng._args(prof_events=prof_events if i == 0 else (None, None), **kw)
+        kw = dict(kw)
+        a0 = kw.pop("_args", None)
+        if a0 is not None and "inp" not in kw:
+            # a BatchPreparer job: its prepare struct, with this call's outputs
+            a, ws = _lib.ModesumArgs.from_buffer_copy(a0), eng._ws
+            ptr = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
+            a.out, a.hp, a.hc = ptr(kw.get("out")), ptr(kw.get("hp")), ptr(kw.get("hc"))
+            a.accumulate = 1 if kw.get("accumulate") else 0
+            a.prof_begin, a.prof_end = prof_events if i == 0 else (None, None)
+        else:
+            a, ws = eng._args(prof_events=prof_events if i == 0 else (None, None), **kw)
         args.append(a)
         wss.append(ws)
     n = len(jobs)
@@ -486,6 +495,164 @@ class WaveformPipeline:
         self.join()
 
 
+_F64 = np.dtype(np.float64)
+_I32 = np.dtype(np.int32)
+
+
+class BatchPreparer:
+    """Walker batches prepared in one chain of launches (efd_modesum_prepare_batch).
+
+    It stands in for a WaveformPipeline in the template chain's `submit(..., prepare_only=True)`
+    (fdutils / waveform / FDInterpolatedModeSum.submit_channels): `submit` only collects the
+    walker's host inputs. `flush()` then packs the collected walkers into one pinned buffer, makes
+    one host->device copy and one efd_modesum_prepare_batch call on the next group's stream, and
+    returns (group, jobs) for sum_batch_loglike / sum_batch. `depth` groups, each with `group`
+    workspaces, rotate: a group is reused after the event its sum recorded (`release`), so
+    group i+1's preparation runs beside group i's sum. Per walker the host pays the packing
+    copies and one argument struct instead of ~10 launches (efd_modesum_prepare).
+    """
+
+    def __init__(self, group=8, depth=2, caustic="uniform", device=None):
+        torch = require_gpu()
+        if not 1 <= group <= _lib.EFD_BATCH_MAX or depth < 1:
+            raise ValueError(f"group must be in 1..{_lib.EFD_BATCH_MAX}, depth >= 1")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.caustic = caustic
+        self.group = group
+        self.groups = [dict(engines=[ModeSumEngine(caustic=caustic) for _ in range(group)],
+                            stream=torch.cuda.Stream(self.device), pin=None, pin_np=None,
+                            pin_done=None, dbuf=None, busy=None, used=False)
+                       for _ in range(depth)]
+        self.lib = self.groups[0]["engines"][0].lib
+        self._next = 0
+        self._pending = []
+        self.last_jobs = []
+
+    # -- the WaveformPipeline surface the template chain uses ---------------------------------
+    def next_slot(self):
+        return len(self._pending)
+
+    def submit(self, host, freq, grid_symmetric, scale=1.0 + 0.0j, out=None, hp=None, hc=None,
+               k0=0, accumulate=False, order=True, prepare_only=False):
+        if not prepare_only or out is not None or hp is not None or hc is not None:
+            raise ValueError("BatchPreparer collects prepare_only submissions")
+        if len(self._pending) >= self.group:
+            raise ValueError(f"at most {self.group} walkers per flush")
+        self._pending.append((host, freq, bool(grid_symmetric), complex(scale), int(k0),
+                              bool(accumulate)))
+        return len(self._pending) - 1
+
+    def order_after_current(self):
+        torch = _torch()
+        cur = torch.cuda.current_stream(self.device)
+        for g in self.groups:
+            g["stream"].wait_stream(cur)
+
+    def stream(self, gi):
+        return self.groups[gi]["stream"]
+
+    # -- one batch -----------------------------------------------------------------------------
+    def flush(self):
+        """Upload and prepare the collected walkers; returns (group index, jobs)."""
+        import ctypes
+        torch = _torch()
+        pend, self._pending = self._pending, []
+        if not pend:
+            raise ValueError("flush: nothing submitted")
+        gi = self._next
+        self._next = (gi + 1) % len(self.groups)
+        G = self.groups[gi]
+        st = G["stream"]
+        if G["busy"] is not None:
+            st.wait_event(G["busy"])        # the group's last sum has read its workspaces
+        per = []
+        off = 0
+        for host, *_ in pend:
+            amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
+            nt, K = amps.shape
+            arrays = [np.ascontiguousarray(host["t"], dtype=_F64),
+                      np.ascontiguousarray(host["phi_phi"], dtype=_F64),
+                      np.ascontiguousarray(host["phi_r"], dtype=_F64),
+                      np.ascontiguousarray(host["f_phi"], dtype=_F64),
+                      np.ascontiguousarray(host["f_r"], dtype=_F64), amps,
+                      np.ascontiguousarray(host["m"], dtype=_I32),
+                      np.ascontiguousarray(host["n"], dtype=_I32),
+                      np.ascontiguousarray(host["ylm_p"], dtype=np.complex128),
+                      np.ascontiguousarray(host["ylm_m"], dtype=np.complex128)]
+            if len(arrays[0]) != nt or any(len(a) != nt for a in arrays[1:5]):
+                raise ValueError("trajectory arrays and amplitudes must share N_t")
+            if any(a.size != K for a in arrays[6:]):
+                raise ValueError("m, n, ylm_p, ylm_m must have K entries")
+            offs = []
+            for a in arrays:
+                offs.append(off)
+                off = (off + a.nbytes + 255) // 256 * 256
+            per.append((nt, K, arrays, offs))
+        total = max(off, 1)
+        if G["pin"] is None or G["pin"].numel() < total:
+            if G["pin_done"] is not None:
+                G["pin_done"].synchronize()
+            G["pin"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8, pin_memory=True)
+            G["pin_np"] = G["pin"].numpy()
+            G["pin_done"] = None
+        if G["pin_done"] is not None:
+            G["pin_done"].synchronize()     # the group's previous copy out of the pinned buffer
+        hb = G["pin_np"]
+        for _, _, arrays, offs in per:
+            for a, o in zip(arrays, offs):
+                hb[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        if G["dbuf"] is None or G["dbuf"].numel() < total:
+            with torch.cuda.stream(st):
+                G["dbuf"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8,
+                                        device=self.device)
+        base = G["dbuf"].data_ptr()
+        _lib.check(self.lib.efd_upload(base, G["pin"].data_ptr(), total, st.cuda_stream),
+                   "efd_upload", self.lib)
+        if G["pin_done"] is None:
+            G["pin_done"] = torch.cuda.Event()
+        G["pin_done"].record(st)
+        jobs, args, wss = [], [], []
+        for (nt, K, _, o), (_, freq, sym, scale, k0, acc), eng in zip(per, pend, G["engines"]):
+            nf = int(freq.numel())
+            ws = eng._workspace(nt, K, nf, freq.device, stream=st)
+            a = _lib.ModesumArgs(
+                t=base + o[0], phi_phi=base + o[1], phi_r=base + o[2], f_phi=base + o[3],
+                f_r=base + o[4], nt=nt, amp=base + o[5], m=base + o[6], n=base + o[7],
+                ylm_p=base + o[8], ylm_m=base + o[9], K=K, freq=freq.data_ptr(), nf=nf,
+                grid_symmetric=1 if sym else 0, scale_re=scale.real, scale_im=scale.imag,
+                caustic=CAUSTIC_MODES[self.caustic], accumulate=1 if acc else 0, k0=k0)
+            eng._last_args = a
+            args.append(a)
+            wss.append(ws)
+            jobs.append((eng, dict(freq=freq, k0=k0, grid_symmetric=sym, _args=a)))
+        n = len(pend)
+        pa = (ctypes.POINTER(_lib.ModesumArgs) * n)(*[ctypes.pointer(a) for a in args])
+        pw = (ctypes.c_void_p * n)(*[ws.data_ptr() for ws in wss])
+        pb = (ctypes.c_size_t * n)(*[ws.numel() for ws in wss])
+        _lib.check(self.lib.efd_modesum_prepare_batch(pa, pw, pb, n, st.cuda_stream),
+                   "efd_modesum_prepare_batch", self.lib)
+        G["used"] = True
+        self.last_jobs = jobs
+        return gi, jobs
+
+    def release(self, gi, event):
+        """The group's workspaces and inputs are free again once `event` (recorded after the sum
+        that reads them) has completed."""
+        self.groups[gi]["busy"] = event
+
+    def wait(self):
+        """Synchronise every group and raise if any workspace reported a device-side error."""
+        import ctypes
+        for G in self.groups:
+            wss = [eng._ws.data_ptr() for eng in G["engines"] if eng._ws is not None]
+            if not G["used"] or not wss:
+                continue
+            pw = (ctypes.c_void_p * len(wss))(*wss)
+            if self.lib.efd_modesum_status_batch(pw, len(wss), None,
+                                                 G["stream"].cuda_stream) != _lib.EFD_OK:
+                raise _lib.EFDError(_lib.last_error(self.lib))
+
+
 def td_length(T, dt, odd_len=True):
     """Samples of FEW's padded TD output: the length of the FD grid for the same (T, dt)."""
     N = int(T * YRSID_SI / dt) + 1
@@ -693,11 +860,15 @@ class FDInterpolatedModeSum:
         return slot
 
     def spectrum(self, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr, n_arr, M, p, e,
-                 dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j):
-        """S(f) = h+ - i hx on the grid (torch complex128 on the GPU)."""
-        om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
-        f_phi = om_phi / (2.0 * np.pi * M * MTSUN_SI)
-        f_r = om_r / (2.0 * np.pi * M * MTSUN_SI)
+                 dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j, f_phi=None, f_r=None):
+        """S(f) = h+ - i hx on the grid (torch complex128 on the GPU). f_phi, f_r: the orbital
+        frequencies at the knots when the upstream already has them (the native trajectory),
+        else FEW's get_fundamental_frequencies(p, e) (the same values submit_channels uses, so
+        an injection and a walker on the same parameters give bitwise the same template)."""
+        if f_phi is None or f_r is None:
+            om_phi, _, om_r = get_fundamental_frequencies(0.0, p, e, 0.0)
+            f_phi = om_phi / (2.0 * np.pi * M * MTSUN_SI)
+            f_r = om_r / (2.0 * np.pi * M * MTSUN_SI)
         inp = DeviceInputs.from_host(t, teuk_modes, Phi_phi, Phi_r, f_phi, f_r, m_arr, n_arr,
                                      ylm_p, ylm_m)
         freq, sym = self._grid(T, dt, f_arr)

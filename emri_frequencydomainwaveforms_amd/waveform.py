@@ -187,7 +187,8 @@ class FastSchwarzschildEccentricFlux:
         scale = complex(extra_scale) * (mu * MRSUN_SI / (dist * Gpc))
         return self.create_waveform.spectrum(d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:],
                                              d["Phi_phi"], d["Phi_r"], d["m"], d["n"], M, d["p"],
-                                             d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale)
+                                             d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale,
+                                             f_phi=d["f_phi"], f_r=d["f_r"])
 
     def submit_channels(self, pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0,
                         Phi_r0=0.0, dt=10.0, T=1.0, eps=1e-5, mode_selection=None,

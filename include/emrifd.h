@@ -141,6 +141,19 @@ int efd_modesum_sum_batch(const efd_modesum_args* const* a, void* const* workspa
                           const size_t* workspace_bytes, int32_t count, void* stream);
 
 /*
+ * efd_modesum_prepare for `count` waveforms (1 <= count <= EFD_BATCH_MAX) in one chain of
+ * launches: each preparation kernel runs once for the batch, its grid's z index picking the
+ * waveform (one waveform's launches cost ~10 us of host time and as many dispatches; a
+ * likelihood's walker batch pays them once). a[i], workspace[i] are what efd_modesum_prepare
+ * would take for waveform i; every a[i] must agree on nf and grid_symmetric and each waveform
+ * needs its own workspace. Each workspace ends up bitwise as after its own efd_modesum_prepare
+ * (which is this call with count = 1). Not part of the reference's interface: an extension for
+ * its batched callers (Likelihood over a walker batch, likelihood.py:246-274).
+ */
+int efd_modesum_prepare_batch(const efd_modesum_args* const* a, void* const* workspace,
+                              const size_t* workspace_bytes, int32_t count, void* stream);
+
+/*
  * efd_modesum_sum_batch with the Gaussian log-likelihood of each waveform fused into the mode
  * sum's epilogue (Likelihood.get_ll over a batch of walkers, likelihood.py:246-274):
  *   out[i] = -1/2 * 4 * sum_c sum_j | d[c][j] - h_c,i[j] * w[c][j] |^2,  c in {+, x},
@@ -164,6 +177,16 @@ int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* works
  * dispatch-order entry out of range in the sum (its bins left unwritten, e.g. a sum run on a
  * workspace another call prepared) -> EFD_ERR_HIP. Reported flags are cleared. */
 int efd_modesum_status(const void* workspace, void* stream);
+
+/*
+ * efd_modesum_status for `count` workspaces (1 <= count <= EFD_BATCH_MAX) used on `stream`: one
+ * gather launch and one synchronisation for a walker batch. flags (optional, int32[count])
+ * receives each workspace's error bits (1: more than 8 monotonic runs, 2: |m| > 255 or
+ * |n| > 1023, 4: tile dispatch-order entry out of range); the return value and efd_last_error
+ * report the first failing waveform. Reported flags are cleared, as by efd_modesum_status.
+ */
+int efd_modesum_status_batch(void* const* workspace, int32_t count, int32_t* flags,
+                             void* stream);
 
 /* Contributions C (harmonic branch x bin pairs, the reference's per-(l, m, n) formulation) of
  * the last efd_modesum on this workspace (for the roofline); synchronises `stream`. */

@@ -154,13 +154,13 @@ def test_fused_likelihood_many_walkers(setup):
     like.fused_likelihood = False
     np.testing.assert_allclose(llf, like.get_ll(walkers, **kw), rtol=1e-12, atol=0.0)
     # argument errors: wrong data shape (host-side ValueError), unprepared mix of grids (C ABI)
-    P = like._fused["pipe"]
-    jobs = [P.job(s) for s in range(2)]
+    jobs = like._fused["prep"].last_jobs[:2]
     out = torch.empty(2, dtype=torch.float64, device="cuda")
     with pytest.raises(ValueError):
         sum_batch_loglike(jobs, like._d[:, 1:].contiguous(), like._w_templ, out)
-    kw0 = {k: v for k, v in jobs[0][1].items() if k != "_args"}   # rebuild the struct
-    bad = [(jobs[0][0], dict(kw0, accumulate=True)), jobs[1]]
+    bad_args = _lib.ModesumArgs.from_buffer_copy(jobs[0][1]["_args"])
+    bad_args.accumulate = 1
+    bad = [(jobs[0][0], dict(jobs[0][1], _args=bad_args)), jobs[1]]
     with pytest.raises(_lib.EFDError):
         sum_batch_loglike(bad, like._d, like._w_templ, out)
 
@@ -172,13 +172,11 @@ def test_spectrum_matches_oracle_through_api(setup):
                     eps=1e-2).cpu().numpy()
     d = wg.prepare(M, MU, params[3], E0, np.pi / 3, -np.pi / 2, 1.0, 0.2, 0.4, T, 1e-2)
     K = len(d["m"])
-    from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI, MTSUN_SI
-    from emri_frequencydomainwaveforms_amd.frequencies import get_fundamental_frequencies
-    op, _, orr = get_fundamental_frequencies(0.0, d["p"], d["e"], 0.0)
+    from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI
     freq = wg.create_waveform.frequency.cpu().numpy()
-    R = fd_oracle.fd_modesum(d["t"], d["teuk"].T, d["Phi_phi"], d["Phi_r"],
-                             op / (2 * np.pi * M * MTSUN_SI), orr / (2 * np.pi * M * MTSUN_SI),
-                             d["m"], d["n"], d["ylms"][:K], d["ylms"][K:], freq,
+    # the upstream's own orbital frequencies at the knots (native trajectory or FEW's formula)
+    R = fd_oracle.fd_modesum(d["t"], d["teuk"].T, d["Phi_phi"], d["Phi_r"], d["f_phi"],
+                             d["f_r"], d["m"], d["n"], d["ylms"][:K], d["ylms"][K:], freq,
                              MU * MRSUN_SI / Gpc)
     assert np.abs(S - R).max() <= 1e-9 * np.abs(R).max()
 

@@ -1,0 +1,159 @@
+"""efd_modesum_prepare_batch: a walker batch prepared in one chain of launches.
+
+Each waveform of a batch (different N_t, K and (m, n) sets, on one shared grid) must give
+bitwise the spectrum, polarisations, contribution / evaluation counts and fused log-likelihood of
+its own efd_modesum_prepare (the one-waveform path, itself pinned to the oracle in
+test_gpu_modesum.py / test_gpu_configs.py). efd_modesum_status_batch must name the failing
+waveform of a batch and clear its flag. The batched Likelihood path (BatchPreparer) is held to
+the per-walker unfused path in test_gpu_api.py and test_gpu_pe_configs.py.
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from emri_frequencydomainwaveforms_amd import _lib  # noqa: E402
+from emri_frequencydomainwaveforms_amd.summation import (BatchPreparer, DeviceInputs,  # noqa: E402
+                                                         ModeSumEngine, sum_batch,
+                                                         sum_batch_loglike)
+from tests.helpers import source_inputs  # noqa: E402
+
+KEYS = ("t", "phi_phi", "phi_r", "f_phi", "f_r", "m", "n", "ylm_p", "ylm_m")
+
+
+def _host(d):
+    h = {k: d[k] for k in KEYS}
+    h["amp"] = np.ascontiguousarray(d["amp"].T)     # [nt][K]
+    return h
+
+
+@pytest.fixture(scope="module")
+def sources():
+    out = []
+    for M, e0, eps in ((3e5, 0.35, 1e-2), (5e5, 0.2, 1e-3), (2e5, 0.5, 1e-2), (4e5, 0.1, 1e-5),
+                       (3e5, 0.6, 1e-2), (6e5, 0.3, 1e-4)):
+        out.append(source_inputs(M=M, e0=e0, T=0.02, dt=20.0, eps=eps))
+    return out
+
+
+def _single(d, freq, caustic):
+    h = _host(d)
+    inp = DeviceInputs.from_host(h["t"], h["amp"], h["phi_phi"], h["phi_r"], h["f_phi"],
+                                 h["f_r"], h["m"], h["n"], h["ylm_p"], h["ylm_m"])
+    eng = ModeSumEngine(caustic=caustic)
+    S = eng.run(inp, freq, grid_symmetric=True, scale=d["prefactor"])
+    return S, eng.stats()
+
+
+@pytest.mark.parametrize("caustic", ["uniform", "spa"])
+def test_prepare_batch_bitwise_equals_single(sources, caustic):
+    assert len({(len(d["t"]), len(d["m"])) for d in sources}) == len(sources)  # ragged batch
+    freq = torch.as_tensor(sources[0]["freq"], device="cuda")
+    nf = int(freq.numel())
+    B = BatchPreparer(group=len(sources), depth=2, caustic=caustic)
+    for rep in range(2):   # the second flush reuses the other group's workspaces, then this one
+        for d in sources:
+            B.submit(_host(d), freq, True, d["prefactor"], prepare_only=True)
+        gi, jobs = B.flush()
+        outs = [torch.empty(nf, dtype=torch.complex128, device="cuda") for _ in sources]
+        with torch.cuda.stream(B.stream(gi)):
+            sum_batch([(eng, dict(kw, out=torch.view_as_real(o)))
+                       for (eng, kw), o in zip(jobs, outs)], stream=B.stream(gi).cuda_stream)
+        B.wait()
+        for (eng, _), o, d in zip(jobs, outs, sources):
+            S, st = _single(d, freq, caustic)
+            assert torch.equal(o, S)
+            assert eng.stats(B.stream(gi).cuda_stream) == st
+            assert st[0] > 0
+
+
+def test_prepare_batch_loglike_bitwise(sources):
+    freq_h = sources[0]["freq"]
+    freq = torch.as_tensor(freq_h, device="cuda")
+    nf = int(freq.numel())
+    k0 = int(np.searchsorted(freq_h, 0.0))
+    nb = nf - k0
+    rng = np.random.default_rng(3)
+    d = torch.as_tensor(rng.standard_normal((2, nb)) + 1j * rng.standard_normal((2, nb)),
+                        device="cuda") * 1e-22
+    w = torch.as_tensor(rng.uniform(0.5, 2.0, (2, nb)) * 1e40, device="cuda")
+    # reference: each walker prepared alone (efd_modesum_prepare), then one fused batch
+    engs = [ModeSumEngine() for _ in sources]
+    jobs1 = []
+    for eng, src in zip(engs, sources):
+        h = _host(src)
+        inp = DeviceInputs.from_host(h["t"], h["amp"], h["phi_phi"], h["phi_r"], h["f_phi"],
+                                     h["f_r"], h["m"], h["n"], h["ylm_p"], h["ylm_m"])
+        eng.launch(inp, freq, None, True, src["prefactor"], phase="prepare", k0=k0,
+                   hp=None, hc=None)
+        jobs1.append((eng, dict(inp=inp, freq=freq, out=None, grid_symmetric=True,
+                                scale=src["prefactor"], k0=k0)))
+    ref = torch.empty(len(sources), dtype=torch.float64, device="cuda")
+    sum_batch_loglike(jobs1, d, w, ref)
+    B = BatchPreparer(group=len(sources))
+    for src in sources:
+        B.submit(_host(src), freq, True, src["prefactor"], k0=k0, prepare_only=True)
+    gi, jobs = B.flush()
+    got = torch.empty(len(sources), dtype=torch.float64, device="cuda")
+    torch.cuda.current_stream().wait_stream(B.stream(gi))
+    sum_batch_loglike(jobs, d, w, got)
+    torch.cuda.synchronize()
+    B.wait()
+    assert torch.equal(got, ref)
+    assert torch.all(torch.isfinite(got)) and torch.all(got < 0)
+
+
+def test_prepare_batch_argument_checks(sources):
+    freq = torch.as_tensor(sources[0]["freq"], device="cuda")
+    B = BatchPreparer(group=2)
+    with pytest.raises(ValueError):
+        B.submit(_host(sources[0]), freq, True, 1.0)          # not prepare_only
+    B.submit(_host(sources[0]), freq, True, 1.0, prepare_only=True)
+    B.submit(_host(sources[1]), freq, True, 1.0, prepare_only=True)
+    with pytest.raises(ValueError):
+        B.submit(_host(sources[2]), freq, True, 1.0, prepare_only=True)   # group full
+    B.flush()
+    B.wait()
+    lib = _lib.load()
+    # the C ABI: a shared workspace and a grid mismatch are refused before any launch
+    eng = B.groups[0]["engines"][0]
+    a = B.last_jobs[0][1]["_args"]
+    pa = (ctypes.POINTER(_lib.ModesumArgs) * 2)(ctypes.pointer(a), ctypes.pointer(a))
+    pw = (ctypes.c_void_p * 2)(eng._ws.data_ptr(), eng._ws.data_ptr())
+    pb = (ctypes.c_size_t * 2)(eng._ws.numel(), eng._ws.numel())
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.efd_modesum_prepare_batch(pa, pw, pb, 2, st) == _lib.EFD_ERR_ARG
+    a2 = _lib.ModesumArgs.from_buffer_copy(a)
+    a2.grid_symmetric = 0
+    eng2 = B.groups[0]["engines"][1]
+    pa = (ctypes.POINTER(_lib.ModesumArgs) * 2)(ctypes.pointer(a), ctypes.pointer(a2))
+    pw = (ctypes.c_void_p * 2)(eng._ws.data_ptr(), eng2._ws.data_ptr())
+    pb = (ctypes.c_size_t * 2)(eng._ws.numel(), eng2._ws.numel())
+    assert lib.efd_modesum_prepare_batch(pa, pw, pb, 2, st) == _lib.EFD_ERR_ARG
+    assert lib.efd_modesum_prepare_batch(pa, pw, pb, 0, st) == _lib.EFD_ERR_ARG
+    assert lib.efd_modesum_prepare_batch(pa, pw, pb, _lib.EFD_BATCH_MAX + 1, st) == _lib.EFD_ERR_ARG
+
+
+def test_status_batch_names_failing_waveform(sources):
+    freq = torch.as_tensor(sources[0]["freq"], device="cuda")
+    B = BatchPreparer(group=3, depth=1)
+    for i in range(3):
+        h = _host(sources[i])
+        if i == 2:
+            h["m"] = h["m"].copy()
+            h["m"][0] = 300                                  # |m| > 255: bad_mn on waveform 2
+        B.submit(h, freq, True, 1.0, prepare_only=True)
+    B.flush()
+    with pytest.raises(_lib.EFDError, match="waveform 2 of the batch"):
+        B.wait()
+    B.wait()   # reported once: the flag is cleared
+    lib = _lib.load()
+    wss = [eng._ws.data_ptr() for eng in B.groups[0]["engines"]]
+    flags = (ctypes.c_int32 * 3)()
+    rc = lib.efd_modesum_status_batch((ctypes.c_void_p * 3)(*wss), 3, flags,
+                                      B.stream(0).cuda_stream)
+    assert rc == _lib.EFD_OK and list(flags) == [0, 0, 0]

@@ -211,8 +211,8 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
     like.fused_likelihood = fused
     if group:
         like.FUSED_GROUP = group
-    if os.environ.get("FUSED_SLOTS"):
-        like.FUSED_SLOTS = int(os.environ["FUSED_SLOTS"])
+    if os.environ.get("FUSED_DEPTH"):
+        like.FUSED_DEPTH = int(os.environ["FUSED_DEPTH"])
     B = len(walkers)
     ll = like.get_ll(walkers, **kw)        # warm-up (also the correctness anchor: ll[0] == 0)
     _sync()

@@ -45,7 +45,7 @@ def main():
     wall = (time.perf_counter() - t0) / args.reps
     # host time up to the batch's synchronisation: time the loop with the final wait stubbed
     fused = getattr(like, "_fused", None)
-    P = fused["pipe"] if fused else like._pipe
+    P = fused["prep"] if fused else like._pipe
     real_wait = P.wait
     P.wait = lambda: None
     real_sync = torch.cuda.Stream.synchronize
