@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_prepare",
     "efd_modesum_prepare_batch",
     "efd_modesum_status_batch",
+    "efd_stage_batch",
     "efd_modesum_sum",
     "efd_modesum_sum_batch",
     "efd_modesum_sum_loglike",
@@ -170,6 +171,10 @@ def load(path=None):
                                                 vp, vp, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
     lib.efd_modesum_status.argtypes = [vp, vp]
+    if hasattr(lib, "efd_stage_batch"):
+        lib.efd_stage_batch.restype = ctypes.c_int
+        lib.efd_stage_batch.argtypes = [vp, sz, ctypes.c_uint64, i32, vp, vp, vp,
+                                        ctypes.POINTER(ModesumArgs), vp, ctypes.POINTER(sz)]
     if hasattr(lib, "efd_modesum_status_batch"):
         lib.efd_modesum_status_batch.restype = ctypes.c_int
         lib.efd_modesum_status_batch.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(i32), vp]

@@ -42,6 +42,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <algorithm>
 #include <atomic>
@@ -2813,8 +2814,21 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
                      int accumulate_out, const double* __restrict__ lld,
                      const double* __restrict__ llw) {
     const int n = batch.n;
-    const int w = (int)(blockIdx.x % (unsigned)n);
-    const int64_t pos = blockIdx.x / (unsigned)n;
+    int w;
+    int64_t pos;
+    if (lld == nullptr) {
+        w = (int)(blockIdx.x % (unsigned)n);
+        pos = blockIdx.x / (unsigned)n;
+    } else {
+        // fused likelihood: the n waveforms of one dispatch place run back to back on one XCD
+        // (workgroups are dealt round-robin over the 8 XCDs, x = g mod 8), so the tile's data
+        // and weights (48 B per bin, the same for every walker) come from HBM once and from
+        // that XCD's L2 for the other n - 1 walkers; place p*8 + x keeps each waveform's
+        // place-to-XCD assignment that of a single launch
+        const unsigned g = blockIdx.x, r = g >> 3;
+        w = (int)(r % (unsigned)n);
+        pos = (int64_t)(r / (unsigned)n) * 8 + (g & 7u);
+    }
     const BatchDesc& d = batch.d[w];
     modesum_tile<PAIRED, CAUSTIC, BPL>(
         d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt, d.K,
@@ -3447,11 +3461,24 @@ static int64_t resident_tile_slots() {
 // prepare and sum see the same arguments, so they agree on whether tperm exists.
 constexpr int32_t ORDER_MIN_K = 1024;
 // Prebuilt tile lists (k_tile_keys) from EFD_LISTS_MIN_K harmonics up; below, the sum builds
-// them itself (short lists: one window pass per tile)
+// them itself (short lists: one window pass per tile). With tens of harmonics (eps = 1e-2) the
+// in-sum build is cheaper than k_tile_keys' pass over every tile: configs 1 / 3 (one waveform,
+// tools/configs.py) 2,668 -> 2,987 and 8,004 -> 8,603 waveforms/s, config 4's walker groups
+// (bench.py --likelihood, 3 interleaved pairs) 11,253 -> 13,416 logL/s, config 5 neutral
+// (40,729 vs 39,648, 2 pairs); config 2 (3,020 harmonics) keeps the prebuilt lists.
 #ifndef EFD_LISTS_MIN_K
-#define EFD_LISTS_MIN_K 0
+#define EFD_LISTS_MIN_K 1024
 #endif
-static bool use_prebuilt(int32_t K) { return EFD_PREBUILT_LISTS && K >= EFD_LISTS_MIN_K; }
+// (the environment variable EFD_LISTS_MIN_K, read once per process, overrides the build's value:
+// a tuning knob; prepare and sum read the same value, so they agree on whether lists exist)
+static int32_t lists_min_k() {
+    static const int32_t v = [] {
+        const char* e = std::getenv("EFD_LISTS_MIN_K");
+        return e ? (int32_t)std::atoi(e) : (int32_t)EFD_LISTS_MIN_K;
+    }();
+    return v;
+}
+static bool use_prebuilt(int32_t K) { return EFD_PREBUILT_LISTS && K >= lists_min_k(); }
 static bool use_cost_order(const Layout& L, int32_t K) {
     return use_prebuilt(K) && EFD_COST_ORDER && K >= ORDER_MIN_K &&
            L.ntiles > resident_tile_slots();

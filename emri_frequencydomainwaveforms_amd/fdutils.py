@@ -137,6 +137,15 @@ class get_fd_waveform_fromFD:
         return self.waveform_generator.submit_channels(pipeline, out, *args, k0=self._suffix_k0,
                                                        **kwargs)
 
+    def submit_batch(self, preparer, params, *args, **kwargs):
+        """Every row of params (walkers x 14) into a BatchPreparer (the fused likelihood's walker
+        group): the generator's submit_batch when it has one, else per-walker submits."""
+        fn = getattr(self.waveform_generator, "submit_batch", None)
+        if fn is not None and not args:
+            return fn(preparer, params, k0=self._suffix_k0, **kwargs)
+        for prm in params:
+            self.submit(preparer, None, *prm, *args, order=False, prepare_only=True, **kwargs)
+
     def prefetch(self, params, *args, **kwargs):
         """The host upstream of a walker batch in parallel (GenerateEMRIWaveform.prefetch),
         ahead of the per-walker submit/fill calls; a no-op for other generators."""

@@ -232,7 +232,7 @@ class Likelihood:
         anything, when the template's grid is not symmetric (the caller takes the per-walker
         path)."""
         torch = self.torch
-        from .summation import BatchPreparer, sum_batch_loglike
+        from .summation import BatchPreparer
         if not self._fused_grid_ok(tm, kwargs):
             return False
         if hasattr(tm, "prefetch"):
@@ -252,14 +252,18 @@ class Likelihood:
         B.order_after_current()
         s_sum.wait_stream(cur)
         try:
+            batch = getattr(tm, "submit_batch", None)
             for g0 in range(0, n, G):
-                for i in range(g0, min(n, g0 + G)):
-                    tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
-                              **kwargs)
+                if batch is not None:
+                    batch(B, params[g0:g0 + G], *args, **kwargs)
+                else:
+                    for i in range(g0, min(n, g0 + G)):
+                        tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
+                                  **kwargs)
                 gi, jobs = B.flush()
                 s_sum.wait_stream(B.stream(gi))
-                sum_batch_loglike(jobs, self._d, self._w_templ, out[g0:g0 + len(jobs)],
-                                  stream=s_sum.cuda_stream)
+                B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)],
+                              s_sum.cuda_stream)
                 ev = torch.cuda.Event()
                 ev.record(s_sum)
                 B.release(gi, ev)

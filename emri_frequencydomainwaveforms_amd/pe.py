@@ -119,16 +119,21 @@ class MemoizedUpstream:
         self.memo = {}
         self.host_s = 0.0
         wg.prepare = self
+        if hasattr(wg, "prefetch"):
+            wg.prefetch = lambda calls: 0   # the memo holds the upstream: nothing to prefetch
 
     def __call__(self, *args, **kwargs):
-        key = repr((args, sorted((k, ("id", id(v)) if hasattr(v, "shape") else v)
-                                 for k, v in kwargs.items())))
-        if key not in self.memo:
+        key = (tuple(float(a) if isinstance(a, (float, int, np.floating)) else a for a in args),
+               tuple(sorted((k, ("id", id(v)) if hasattr(v, "shape") else v)
+                            for k, v in kwargs.items())))
+        hit = self.memo.get(key)
+        if hit is None:
             t0 = self._time()
-            self.memo[key] = self.orig(*args, **kwargs)
+            hit = self.memo[key] = self.orig(*args, **kwargs)
             self.host_s += self._time() - t0
-        return self.memo[key]
+        return hit
 
     def remove(self):
-        if self.wg.__dict__.get("prepare") is self:
-            del self.wg.prepare        # back to the class's method
+        for name in ("prepare", "prefetch"):
+            if name in self.wg.__dict__:
+                delattr(self.wg, name)   # back to the class's methods

@@ -288,6 +288,14 @@ def sum_batch(jobs, stream=None, prof_events=(None, None)):
     return wss
 
 
+def _check_ll_io(torch, d, w, out, nb, n):
+    if (d.dtype != torch.complex128 or tuple(d.shape) != (2, nb) or not d.is_contiguous()
+            or w.dtype != torch.float64 or tuple(w.shape) != (2, nb) or not w.is_contiguous()
+            or out.dtype != torch.float64 or out.numel() < n or not out.is_contiguous()):
+        raise ValueError(f"sum_batch_loglike: d complex128 [2][{nb}], w float64 [2][{nb}] and "
+                         f"out float64 [>= {n}], contiguous")
+
+
 def sum_batch_loglike(jobs, d, w, out, stream=None):
     """Mode sums of several prepared waveforms with the likelihood fused into the sum
     (efd_modesum_sum_loglike): out[i] = -1/2 * 4 * sum |d - h_i w|^2 over both channels, h_i
@@ -305,11 +313,7 @@ def sum_batch_loglike(jobs, d, w, out, stream=None):
         raise ValueError(f"sum_batch_loglike takes 1..{_lib.EFD_BATCH_MAX} waveforms")
     freq = jobs[0][1]["freq"]
     nb = int(freq.numel()) - int(jobs[0][1].get("k0", 0))
-    if (d.dtype != torch.complex128 or tuple(d.shape) != (2, nb) or not d.is_contiguous()
-            or w.dtype != torch.float64 or tuple(w.shape) != (2, nb) or not w.is_contiguous()
-            or out.dtype != torch.float64 or out.numel() < len(jobs) or not out.is_contiguous()):
-        raise ValueError(f"sum_batch_loglike: d complex128 [2][{nb}], w float64 [2][{nb}] and "
-                         f"out float64 [>= {len(jobs)}], contiguous")
+    _check_ll_io(torch, d, w, out, nb, len(jobs))
     args, wss = [], []
     for eng, kw in jobs:
         kw = dict(kw)
@@ -553,7 +557,9 @@ class BatchPreparer:
 
     # -- one batch -----------------------------------------------------------------------------
     def flush(self):
-        """Upload and prepare the collected walkers; returns (group index, jobs)."""
+        """Upload and prepare the collected walkers; returns (group index, jobs). A job's
+        argument struct lives in the group's reused array: use the jobs before the group's next
+        flush (sum_batch / sum_batch_loglike copy what they need)."""
         import ctypes
         torch = _torch()
         pend, self._pending = self._pending, []
@@ -565,75 +571,108 @@ class BatchPreparer:
         st = G["stream"]
         if G["busy"] is not None:
             st.wait_event(G["busy"])        # the group's last sum has read its workspaces
-        per = []
-        off = 0
-        for host, *_ in pend:
-            amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
-            nt, K = amps.shape
-            arrays = [np.ascontiguousarray(host["t"], dtype=_F64),
-                      np.ascontiguousarray(host["phi_phi"], dtype=_F64),
-                      np.ascontiguousarray(host["phi_r"], dtype=_F64),
-                      np.ascontiguousarray(host["f_phi"], dtype=_F64),
-                      np.ascontiguousarray(host["f_r"], dtype=_F64), amps,
-                      np.ascontiguousarray(host["m"], dtype=_I32),
-                      np.ascontiguousarray(host["n"], dtype=_I32),
-                      np.ascontiguousarray(host["ylm_p"], dtype=np.complex128),
-                      np.ascontiguousarray(host["ylm_m"], dtype=np.complex128)]
-            if len(arrays[0]) != nt or any(len(a) != nt for a in arrays[1:5]):
-                raise ValueError("trajectory arrays and amplitudes must share N_t")
-            if any(a.size != K for a in arrays[6:]):
-                raise ValueError("m, n, ylm_p, ylm_m must have K entries")
-            offs = []
-            for a in arrays:
-                offs.append(off)
-                off = (off + a.nbytes + 255) // 256 * 256
-            per.append((nt, K, arrays, offs))
-        total = max(off, 1)
-        if G["pin"] is None or G["pin"].numel() < total:
-            if G["pin_done"] is not None:
-                G["pin_done"].synchronize()
-            G["pin"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8, pin_memory=True)
-            G["pin_np"] = G["pin"].numpy()
-            G["pin_done"] = None
         if G["pin_done"] is not None:
             G["pin_done"].synchronize()     # the group's previous copy out of the pinned buffer
-        hb = G["pin_np"]
-        for _, _, arrays, offs in per:
-            for a, o in zip(arrays, offs):
-                hb[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
-        if G["dbuf"] is None or G["dbuf"].numel() < total:
+        n = len(pend)
+        if "args" not in G:
+            A = G["args"] = (_lib.ModesumArgs * self.group)()
+            size = ctypes.sizeof(_lib.ModesumArgs)
+            base = ctypes.addressof(A)
+            G["pa"] = ctypes.cast((ctypes.c_void_p * self.group)(
+                *[base + i * size for i in range(self.group)]),
+                ctypes.POINTER(ctypes.POINTER(_lib.ModesumArgs)))
+            G["pw"] = (ctypes.c_void_p * self.group)()
+            G["pb"] = (ctypes.c_size_t * self.group)()
+        freq = pend[0][1]
+        nf = int(freq.numel())
+        for _, f, sym, _, k0, acc in pend:
+            if f is not freq and (int(f.numel()) != nf or f.data_ptr() != freq.data_ptr()):
+                raise ValueError("flush: the walkers of a group share one frequency grid")
+        _, _, sym, _, k0, acc = pend[0]
+        tmpl = _lib.ModesumArgs(freq=freq.data_ptr(), nf=nf, grid_symmetric=1 if sym else 0,
+                                caustic=CAUSTIC_MODES[self.caustic],
+                                accumulate=1 if acc else 0, k0=k0)
+        if any(p[2] != sym or p[4] != k0 or p[5] != acc for p in pend):
+            raise ValueError("flush: grid symmetry, k0 and accumulate must agree in a group")
+        src = np.empty((n, 10), dtype=np.uint64)
+        shape = np.empty((n, 2), dtype=np.int32)
+        scale = np.empty((n, 2), dtype=np.float64)
+        keep = []    # arrays converted here stay alive until the staging copy below
+        for i, (host, _, _, sc, _, _) in enumerate(pend):
+            fast = host.get("_src")
+            if fast is not None:
+                src[i] = fast
+                shape[i] = host["_shape"]
+            else:
+                amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
+                nt, K = amps.shape
+                arrays = [np.ascontiguousarray(host[k], dtype=_F64)
+                          for k in ("t", "phi_phi", "phi_r", "f_phi", "f_r")]
+                arrays += [amps, np.ascontiguousarray(host["m"], dtype=_I32),
+                           np.ascontiguousarray(host["n"], dtype=_I32),
+                           np.ascontiguousarray(host["ylm_p"], dtype=np.complex128),
+                           np.ascontiguousarray(host["ylm_m"], dtype=np.complex128)]
+                if any(a.size != nt for a in arrays[:5]):
+                    raise ValueError("trajectory arrays and amplitudes must share N_t")
+                if any(a.size != K for a in arrays[6:]):
+                    raise ValueError("m, n, ylm_p, ylm_m must have K entries")
+                keep.append(arrays)
+                src[i] = [a.ctypes.data for a in arrays]
+                shape[i] = (nt, K)
+            scale[i] = (sc.real, sc.imag)
+        total = ctypes.c_size_t(0)
+        for attempt in range(2):
+            pin = G["pin"]
+            dbuf = G["dbuf"]
+            rc = self.lib.efd_stage_batch(
+                pin.data_ptr() if pin is not None else None, pin.numel() if pin is not None else 0,
+                dbuf.data_ptr() if dbuf is not None else 0, n, src.ctypes.data,
+                shape.ctypes.data, scale.ctypes.data, ctypes.byref(tmpl), G["args"],
+                ctypes.byref(total))
+            if rc == _lib.EFD_OK and dbuf is not None and dbuf.numel() >= total.value:
+                break
+            if rc not in (_lib.EFD_OK, _lib.EFD_ERR_WORKSPACE) or attempt == 1:
+                raise _lib.EFDError(f"efd_stage_batch failed ({rc})")
+            cap = max(2 * total.value, 1 << 20)
+            G["pin"] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
             with torch.cuda.stream(st):
-                G["dbuf"] = torch.empty(max(2 * total, 1 << 20), dtype=torch.uint8,
-                                        device=self.device)
-        base = G["dbuf"].data_ptr()
-        _lib.check(self.lib.efd_upload(base, G["pin"].data_ptr(), total, st.cuda_stream),
-                   "efd_upload", self.lib)
+                G["dbuf"] = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        del keep
+        _lib.check(self.lib.efd_upload(G["dbuf"].data_ptr(), G["pin"].data_ptr(), total.value,
+                                       st.cuda_stream), "efd_upload", self.lib)
         if G["pin_done"] is None:
             G["pin_done"] = torch.cuda.Event()
         G["pin_done"].record(st)
-        jobs, args, wss = [], [], []
-        for (nt, K, _, o), (_, freq, sym, scale, k0, acc), eng in zip(per, pend, G["engines"]):
-            nf = int(freq.numel())
-            ws = eng._workspace(nt, K, nf, freq.device, stream=st)
-            a = _lib.ModesumArgs(
-                t=base + o[0], phi_phi=base + o[1], phi_r=base + o[2], f_phi=base + o[3],
-                f_r=base + o[4], nt=nt, amp=base + o[5], m=base + o[6], n=base + o[7],
-                ylm_p=base + o[8], ylm_m=base + o[9], K=K, freq=freq.data_ptr(), nf=nf,
-                grid_symmetric=1 if sym else 0, scale_re=scale.real, scale_im=scale.imag,
-                caustic=CAUSTIC_MODES[self.caustic], accumulate=1 if acc else 0, k0=k0)
-            eng._last_args = a
-            args.append(a)
-            wss.append(ws)
-            jobs.append((eng, dict(freq=freq, k0=k0, grid_symmetric=sym, _args=a)))
-        n = len(pend)
-        pa = (ctypes.POINTER(_lib.ModesumArgs) * n)(*[ctypes.pointer(a) for a in args])
-        pw = (ctypes.c_void_p * n)(*[ws.data_ptr() for ws in wss])
-        pb = (ctypes.c_size_t * n)(*[ws.numel() for ws in wss])
-        _lib.check(self.lib.efd_modesum_prepare_batch(pa, pw, pb, n, st.cuda_stream),
-                   "efd_modesum_prepare_batch", self.lib)
+        A, pw, pb = G["args"], G["pw"], G["pb"]
+        jobs = []
+        for i in range(n):
+            eng = G["engines"][i]
+            ws = eng._workspace(int(shape[i, 0]), int(shape[i, 1]), nf, freq.device, stream=st)
+            pw[i] = ws.data_ptr()
+            pb[i] = ws.numel()
+            eng._last_args = A[i]
+            jobs.append((eng, dict(freq=freq, k0=k0, grid_symmetric=sym, _args=A[i])))
+        _lib.check(self.lib.efd_modesum_prepare_batch(G["pa"], ctypes.cast(pw, ctypes.POINTER(
+            ctypes.c_void_p)), pb, n, st.cuda_stream), "efd_modesum_prepare_batch", self.lib)
         G["used"] = True
+        G["n"] = n
         self.last_jobs = jobs
         return gi, jobs
+
+    def sum_loglike(self, gi, d, w, out, stream):
+        """efd_modesum_sum_loglike over group gi's last flush (its argument and workspace
+        arrays as they are, no per-walker rebuilding); d, w, out as sum_batch_loglike."""
+        import ctypes
+        torch = _torch()
+        G = self.groups[gi]
+        n = G["n"]
+        A = G["args"]
+        nb = int(A[0].nf) - int(A[0].k0)
+        _check_ll_io(torch, d, w, out, nb, n)
+        _lib.check(self.lib.efd_modesum_sum_loglike(
+            G["pa"], ctypes.cast(G["pw"], ctypes.POINTER(ctypes.c_void_p)), G["pb"], n,
+            torch.view_as_real(d).data_ptr(), w.data_ptr(), out.data_ptr(), stream),
+            "efd_modesum_sum_loglike", self.lib)
 
     def release(self, gi, event):
         """The group's workspaces and inputs are free again once `event` (recorded after the sum

@@ -120,9 +120,20 @@ class FastSchwarzschildEccentricFlux:
             ylms = np.concatenate([ylms_all[:K][keep], ylms_all[K:][keep]])
             if not include_minus_m:
                 ylms[len(keep):] = 0.0
-            self.last_modes = (amp.l_arr[keep], amp.m_arr[keep], amp.n_arr[keep])
-            return dict(t=t, p=p, e=e, Phi_phi=Phi_phi, Phi_r=Phi_r, teuk=teuk, ylms=ylms,
-                        m=amp.m_arr[keep], n=amp.n_arr[keep], f_phi=f_phi, f_r=f_r)
+            mk, nk = amp.m_arr[keep], amp.n_arr[keep]
+            self.last_modes = (amp.l_arr[keep], mk, nk)
+            d = dict(t=t, p=p, e=e, Phi_phi=Phi_phi, Phi_r=Phi_r, teuk=teuk, ylms=ylms,
+                     m=mk, n=nk, f_phi=f_phi, f_r=f_r)
+            # host addresses of the mode sum's ten inputs, for the batched likelihood's native
+            # staging (summation.BatchPreparer.flush; computed here, in the prefetch threads)
+            arrs = (t, Phi_phi, Phi_r, f_phi, f_r, teuk, mk, nk, ylms)
+            dts = (np.float64,) * 5 + (np.complex128, np.int32, np.int32, np.complex128)
+            if all(a.flags.c_contiguous and a.dtype == dt for a, dt in zip(arrs, dts)):
+                k = len(keep)
+                ptr = [a.ctypes.data for a in arrs]
+                d["_src"] = ptr + [ptr[-1] + 16 * k]
+                d["_shape"] = (len(t), k)
+            return d
         t, p, e, x, Phi_phi, Phi_theta, Phi_r = self.inspiral_generator(
             M, mu, 0.0, p0, e0, 1.0, Phi_phi0=Phi_phi0, Phi_r0=Phi_r0, T=T)
         if mode_selection is not None:
@@ -267,6 +278,23 @@ class GenerateEMRIWaveform:
         self.waveform_generator = waveform_class(*args, **kwargs)
         self.frame = frame
         self.return_list = return_list
+        self._angle_cache = {}
+
+    def _angles(self, qS, phiS, qK, phiK):
+        """(theta, phi, rot) of a sky position and spin orientation: the source-frame viewing
+        angles and the detector-frame rotation exp(-2 i psi) (1 in the source frame), cached
+        per angle set (the drivers' walkers share them, emri_pe.py:161-167)."""
+        key = (float(qS), float(phiS), float(qK), float(phiK))
+        v = self._angle_cache.get(key)
+        if v is None:
+            theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
+            rot = 1.0 + 0.0j
+            if self.frame == "detector":
+                rot = complex(np.exp(-2j * polarization_angle(qS, phiS, qK, phiK)))
+            if len(self._angle_cache) > 4096:
+                self._angle_cache.clear()
+            v = self._angle_cache[key] = (theta, phi, rot)
+        return v
 
     @property
     def use_gpu(self):
@@ -275,10 +303,7 @@ class GenerateEMRIWaveform:
     def _spectrum(self, M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0,
                   Phi_r0, **kwargs):
         # a, x0, Phi_theta0 are ignored for Schwarzschild (emri_pe.py:598, 602)
-        theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
-        rot = 1.0 + 0.0j
-        if self.frame == "detector":
-            rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
+        theta, phi, rot = self._angles(qS, phiS, qK, phiK)
         gen = self.waveform_generator
         return gen.spectrum(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, extra_scale=rot,
                             **kwargs)
@@ -295,12 +320,40 @@ class GenerateEMRIWaveform:
             cw._grid(kwargs.get("T", 1.0), kwargs.get("dt", 10.0), kwargs.get("f_arr"))
             if k0 != cw.positive_start():
                 raise ValueError("positive_frequency_mask does not match the generator's grid")
-        theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
-        rot = 1.0 + 0.0j
-        if self.frame == "detector":
-            rot = np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
+        theta, phi, rot = self._angles(qS, phiS, qK, phiK)
         return gen.submit_channels(pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0,
                                    Phi_r0, extra_scale=rot, **kwargs)
+
+    def submit_batch(self, preparer, params, k0=None, T=1.0, dt=10.0, eps=1e-5, f_arr=None,
+                     mode_selection=None, include_minus_m=True, **kwargs):
+        """submit_channels(prepare_only=True) for every row of params (B x 14) into a
+        BatchPreparer: the grid is checked once, the angles come from the per-angle cache and
+        the host upstream from prepare() (prefetched results when there are any), so a walker
+        costs its dictionary lookups and the preparer's bookkeeping. Same templates, bitwise,
+        as B calls of submit_channels."""
+        gen = self.waveform_generator
+        if gen.output_type != "fd":
+            raise ValueError("submit_batch is the FD path")
+        cw = gen.create_waveform
+        freq, sym = cw._grid(T, dt, f_arr)
+        if k0 is not None and k0 != cw.positive_start():
+            raise ValueError("positive_frequency_mask does not match the generator's grid")
+        if not sym:
+            raise ValueError("submit_batch needs a symmetric grid (the fused likelihood's)")
+        kc = cw._k0
+        for prm in np.asarray(params, dtype=np.float64).reshape(-1, 14).tolist():
+            M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
+            theta, phi, rot = self._angles(qS, phiS, qK, phiK)
+            d = gen.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
+                            mode_selection, include_minus_m)
+            K = len(d["m"])
+            y = d["ylms"]
+            preparer.submit(dict(t=d["t"], amp=d["teuk"], phi_phi=d["Phi_phi"],
+                                 phi_r=d["Phi_r"], f_phi=d["f_phi"], f_r=d["f_r"], m=d["m"],
+                                 n=d["n"], ylm_p=y[:K], ylm_m=y[K:], _src=d.get("_src"),
+                                 _shape=d.get("_shape"), _keep=d),
+                            freq, True, rot * (mu * MRSUN_SI / (dist * Gpc)), k0=kc,
+                            prepare_only=True)
 
     def prefetch(self, params, T=1.0, dt=10.0, eps=1e-5, mode_selection=None,
                  include_minus_m=True, **kwargs):
@@ -313,7 +366,7 @@ class GenerateEMRIWaveform:
         calls = []
         for prm in np.asarray(params, dtype=np.float64):
             M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
-            theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
+            theta, phi, _ = self._angles(qS, phiS, qK, phiK)
             calls.append((M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps))
         return gen.prefetch(calls)
 

@@ -337,6 +337,19 @@ int efd_host_modes(const double* p, const double* e, int32_t nt, const int32_t* 
                    int32_t nmodes, const double* ylm_p, const double* ylm_m, double eps,
                    int32_t* keep, int32_t* nkeep, double* teuk, int64_t teuk_cap);
 
+/*
+ * Host staging of a walker batch for efd_modesum_prepare_batch (not part of the reference's
+ * interface; the batched Likelihood's packing step, likelihood.py:246-274 callers): the ten
+ * input arrays of walker i (src[10 i + f]: t, phi_phi, phi_r, f_phi, f_r, amp [nt][K] complex,
+ * m, n, ylm_p, ylm_m; nt = shape[2 i], K = shape[2 i + 1]) are copied 256-B aligned into the
+ * host buffer pin, and args[i] becomes *tmpl with walker i's nt, K, scale (scale[2 i] + i
+ * scale[2 i + 1]) and device pointers dev_base + offset (valid after pin is copied to
+ * dev_base). *total = bytes needed; EFD_ERR_WORKSPACE (nothing copied) when pin_bytes is less.
+ */
+int efd_stage_batch(void* pin, size_t pin_bytes, uint64_t dev_base, int32_t count,
+                    const uint64_t* src, const int32_t* shape, const double* scale,
+                    const efd_modesum_args* tmpl, efd_modesum_args* args, size_t* total);
+
 #ifdef __cplusplus
 }
 #endif

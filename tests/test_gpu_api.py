@@ -46,15 +46,25 @@ def test_generator_contract(setup):
     assert torch.equal(Sp, S[pos])
     hpp, hcp = gen_list(*params, mask_positive=True, **kw)
     assert torch.equal(hpp, hp[pos]) and torch.equal(hcp, hc[pos])
-    # the spectrum equals the oracle's for the same host inputs
+    # the spectrum equals the oracle's for the same host inputs: source-frame viewing angle
+    # theta = arccos(-R.S) of the sky position (qS, phiS) = (0.5, 0.3) and spin direction
+    # (qK, phiK) = (0.8, 1.1), detector-frame rotation exp(-2 i psi) and 1 / dist in the scale
+    from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI
     wg = gen.waveform_generator
-    theta = np.arccos(-(np.sin(0.5) * np.cos(0.3) * np.sin(0.8) * np.cos(1.1)
-                        + np.sin(0.5) * np.sin(0.3) * np.sin(0.8) * np.sin(1.1)
-                        + np.cos(0.5) * np.cos(0.8)))
-    d = wg.prepare(M, MU, params[3], E0, theta, -np.pi / 2, 1.0, params[11], params[13], T,
-                   1e-2)
+    theta_ref = np.arccos(-(np.sin(0.5) * np.cos(0.3) * np.sin(0.8) * np.cos(1.1)
+                            + np.sin(0.5) * np.sin(0.3) * np.sin(0.8) * np.sin(1.1)
+                            + np.cos(0.5) * np.cos(0.8)))
+    theta, phi, rot = gen._angles(0.5, 0.3, 0.8, 1.1)
+    assert abs(theta - theta_ref) <= 1e-14 and phi == -np.pi / 2 and abs(abs(rot) - 1) < 1e-15
+    d = wg.prepare(M, MU, params[3], E0, theta, phi, 1.0, params[11], params[13], T, 1e-2)
     K = len(d["m"])
     assert K > 20
+    R = fd_oracle.fd_modesum(d["t"], d["teuk"].T, d["Phi_phi"], d["Phi_r"], d["f_phi"],
+                             d["f_r"], d["m"], d["n"], d["ylms"][:K], d["ylms"][K:],
+                             freq.cpu().numpy(), rot * MU * MRSUN_SI / (1.0 * Gpc))
+    Sh = S.cpu().numpy()
+    assert np.abs(Sh - R).max() <= 1e-9 * np.abs(R).max()
+    np.testing.assert_array_equal(Sh != 0, R != 0)
 
 
 def test_f_arr_downsampled(setup):

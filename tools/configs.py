@@ -54,26 +54,12 @@ def _sync():
     torch.cuda.synchronize()
 
 
-class PrepareCache:
-    """Memoise the generator's host upstream (prepare) per parameter set, so a second pass over
-    the same walkers times the device work alone. Installed on the instance only."""
-
-    def __init__(self, wg):
-        self.wg = wg
-        self.orig = wg.prepare
-        self.memo = {}
-        self.host_s = 0.0
-        wg.prepare = self
-
-    def __call__(self, *args, **kwargs):
-        # arrays (f_arr) by identity: the drivers pass the same objects on every call
-        key = repr((args, sorted((k, ("id", id(v)) if hasattr(v, "shape") else v)
-                                 for k, v in kwargs.items())))
-        if key not in self.memo:
-            t0 = time.perf_counter()
-            self.memo[key] = self.orig(*args, **kwargs)
-            self.host_s += time.perf_counter() - t0
-        return self.memo[key]
+def PrepareCache(wg):
+    """Memoise the generator's host upstream per parameter set, so a second pass over the same
+    walkers times the device work alone (emri_frequencydomainwaveforms_amd.pe.MemoizedUpstream,
+    installed on the instance only)."""
+    from emri_frequencydomainwaveforms_amd.pe import MemoizedUpstream
+    return MemoizedUpstream(wg)
 
 
 def config1(reps):
@@ -159,50 +145,15 @@ def config3(reps, slots=4):
 
 
 def _likelihood_setup(T, eps, downsample, nwalkers, seed=2601996):
-    from emri_frequencydomainwaveforms_amd import fdutils
-    from emri_frequencydomainwaveforms_amd.likelihood import Likelihood
-    from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
-    from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform
-    M, mu, e0, dt = 1e6, 10.0, 0.35, 10.0
-    few = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", sum_kwargs=SUM_KW,
-                               use_gpu=True, return_list=True)
-    p0 = float(get_p_at_t(EMRIInspiral(), 0.99 * T, [M, mu, 0.0, e0, 1.0]))
-    truth = _params(M, mu, p0, e0)
-    kw = dict(T=T, dt=dt, eps=eps)
-    sig = few(*truth, mask_positive=True, **kw)
-    frequency = few.waveform_generator.create_waveform.frequency
-    frequency = frequency.cpu().numpy() if hasattr(frequency, "detach") else np.asarray(frequency)
-    pos = frequency >= 0.0
-    if downsample:
-        # emri_pe.py:333-349: uniform grid to 1.01 x the highest non-zero bin of the injection
-        fixed = frequency[pos]
-        nz = (np.abs(sig[0].cpu().numpy()) > 0)
-        num = int(nz.sum() / downsample)
-        p_freq = np.linspace(0.0, fixed[nz].max() * 1.01, num=num)
-        newfreq = np.hstack((-p_freq[::-1][:-1], p_freq))
-        kw["f_arr"] = newfreq
-        pos = newfreq >= 0.0
-        f_like = newfreq[pos]
-    else:
-        f_like = frequency[pos]
-    gen = fdutils.get_fd_waveform_fromFD(few, pos, dt)
-    like = Likelihood(gen, 2, f_arr=f_like, use_gpu=True)
-    data = gen(*truth, **kw)
-    like.inject_signal(data_stream=data, noise_fn=[fdutils.get_sensitivity] * 2,
-                       noise_kwargs=[{}, {}])
-    rng = np.random.default_rng(seed)
-    B = nwalkers // 2   # red-blue half-step, ntemps = 1
-    walkers = np.tile(np.asarray(truth, dtype=np.float64), (B, 1))
-    sig6 = np.array([1e-6, 1e-6, 1e-5, 1e-6, 1e-3, 1e-3])   # ln M, ln mu, p0, e0, Phi_phi0, Phi_r0
-    z = rng.normal(size=(B, 6)) * sig6
-    walkers[:, 0] *= np.exp(z[:, 0])
-    walkers[:, 1] *= np.exp(z[:, 1])
-    walkers[:, 3] += z[:, 2]
-    walkers[:, 4] += z[:, 3]
-    walkers[:, 11] += z[:, 4]
-    walkers[:, 13] += z[:, 5]
-    walkers[0] = truth            # one walker on the truth: logL = 0 exactly
-    return few, like, walkers, kw, len(f_like)
+    """emri_pe.py's setup (emri_frequencydomainwaveforms_amd.pe: its angles, distance, phases,
+    p0 for 0.99 Tobs, downsampled grid, Likelihood, walker start); the batch is the first
+    red-blue half-step of the start, mapped to FEW's 14 parameters by the TransformContainer,
+    with walker 0 on the injection (logL = 0 exactly)."""
+    from emri_frequencydomainwaveforms_amd import pe
+    st = pe.setup(Tobs=T, eps=eps, downsample=downsample, nwalkers=nwalkers, seed=seed)
+    walkers = st.transform.both_transforms(st.half_steps()[0])
+    walkers[0] = st.truth14
+    return st.few, st.like, walkers, st.kwargs, len(st.f_like)
 
 
 def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, group=None):
