@@ -3462,10 +3462,11 @@ static int64_t resident_tile_slots() {
 constexpr int32_t ORDER_MIN_K = 1024;
 // Prebuilt tile lists (k_tile_keys) from EFD_LISTS_MIN_K harmonics up; below, the sum builds
 // them itself (short lists: one window pass per tile). With tens of harmonics (eps = 1e-2) the
-// in-sum build is cheaper than k_tile_keys' pass over every tile: configs 1 / 3 (one waveform,
-// tools/configs.py) 2,668 -> 2,987 and 8,004 -> 8,603 waveforms/s, config 4's walker groups
-// (bench.py --likelihood, 3 interleaved pairs) 11,253 -> 13,416 logL/s, config 5 neutral
-// (40,729 vs 39,648, 2 pairs); config 2 (3,020 harmonics) keeps the prebuilt lists.
+// in-sum build is cheaper than k_tile_keys' pass over every tile in the batched likelihood:
+// config 4's walker groups (bench.py --likelihood, 3 interleaved pairs) 11,253 -> 13,416 logL/s;
+// configs 1 / 3 (tools/configs.py, 2 interleaved pairs) 2,938 vs 2,897 and 8,166 vs 7,996
+// waveforms/s (neutral), config 5 40,729 vs 39,648 (neutral); config 2 (3,020 harmonics) keeps
+// the prebuilt lists.
 #ifndef EFD_LISTS_MIN_K
 #define EFD_LISTS_MIN_K 1024
 #endif

@@ -16,7 +16,7 @@ size-independent properties of the spectrum.
   phase is numerically undetermined (split_check's docstring). The measured errors and the fold
   count go to $EFD_PARITY_OUT (profiles/r03_parity.json).
 - Linearity in the harmonic set: S(all) == S(A) + S(B) for a split of the harmonics that cuts
-  (m, n) groups apart (accumulate = 1), to 1e-12 max|S|.
+  (m, n) groups apart (accumulate = 1), to 1e-12 max|S| (+ 2 E_k at extrapolated-term bins).
 - Bitwise determinism of repeated runs.
 """
 
@@ -40,6 +40,18 @@ def cfg2():
     return bench.build_workload()
 
 
+@pytest.fixture(scope="module")
+def oracle2(cfg2):
+    """The C oracle's config-2 spectrum R and extrapolated-term magnitudes E (one evaluation,
+    shared by the tests of this module)."""
+    w = cfg2
+    threads = min(16, len(os.sched_getaffinity(0)))
+    R, E = fd_oracle_c.modesum(w["t"], w["amp"].T, w["phi_phi"], w["phi_r"], w["f_phi"],
+                               w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"], w["freq"],
+                               w["prefactor"], caustic="uniform", nthreads=threads, extrap=True)
+    return R, E, threads
+
+
 def _inputs(w, sel=None):
     sel = np.arange(len(w["m"])) if sel is None else sel
     return DeviceInputs.from_host(w["t"], w["amp"][:, sel], w["phi_phi"], w["phi_r"], w["f_phi"],
@@ -47,17 +59,14 @@ def _inputs(w, sel=None):
                                   w["ylm_m"][sel])
 
 
-def test_config2_full_spectrum_vs_c_oracle(cfg2):
+def test_config2_full_spectrum_vs_c_oracle(cfg2, oracle2):
     w = cfg2
     freq = torch.as_tensor(w["freq"], device="cuda")
     eng = ModeSumEngine(caustic="uniform")
     S = eng.run(_inputs(w), freq, grid_symmetric=True, scale=w["prefactor"]).cpu().numpy()
     C, n_eval, groups = eng.stats()
     assert len(w["m"]) == 3020 and groups == len(set(zip(w["m"].tolist(), w["n"].tolist())))
-    threads = min(16, len(os.sched_getaffinity(0)))
-    R, E = fd_oracle_c.modesum(w["t"], w["amp"].T, w["phi_phi"], w["phi_r"], w["f_phi"],
-                               w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"], w["freq"],
-                               w["prefactor"], caustic="uniform", nthreads=threads, extrap=True)
+    R, E, threads = oracle2
     Rps = []
     for seed in (7, 8):
         pert = ulp_perturbation(seed)
@@ -79,7 +88,13 @@ def test_config2_full_spectrum_vs_c_oracle(cfg2):
     assert n_eval < C / 3     # one SPA evaluation per (m, n) group serves every l
 
 
-def test_config2_linearity_and_determinism(cfg2):
+def test_config2_linearity_and_determinism(cfg2, oracle2):
+    """Splitting the harmonics re-rounds the l-summed group amplitudes; that is invisible (3e-15
+    of max|S| measured) except at the bins holding terms whose t(g) the splines extrapolate far
+    outside the trajectory (the oracle's E > 0, within +-8 bins), where cubics evaluated at
+    |t| ~ 1e7 s amplify it: there the bound is 1e-12 max|S| + 2 E, as in split_check (the
+    measured error there is ~1e-9 E)."""
+    from scipy.ndimage import maximum_filter1d
     w = cfg2
     freq = torch.as_tensor(w["freq"], device="cuda")
     eng = ModeSumEngine(caustic="uniform")
@@ -91,8 +106,16 @@ def test_config2_linearity_and_determinism(cfg2):
     P = eng.run(_inputs(w, a), freq, grid_symmetric=True, scale=w["prefactor"])
     eng.run(_inputs(w, b), freq, out=P, grid_symmetric=True, scale=w["prefactor"],
             accumulate=True)
-    err = (P - S).abs().max().item() / S.abs().max().item()
-    assert err <= 1e-12, err
+    Sh, Ph = S.cpu().numpy(), P.cpu().numpy()
+    err = np.abs(Ph - Sh)
+    scale = np.abs(Sh).max()
+    Ed = maximum_filter1d(oracle2[1], 17)
+    off = Ed == 0
+    assert err[off].max() <= 1e-12 * scale, err[off].max() / scale
+    assert np.all(err <= 1e-12 * scale + 2.0 * Ed), (err - 2.0 * Ed).max() / scale
+    record_parity("config2_linearity", {"max_rel_off_extrap": float(err[off].max() / scale),
+                                        "max_rel": float(err.max() / scale),
+                                        "extrap_bins": int((~off).sum())})
 
 
 def test_config2_batched_sum_bitwise(cfg2):
