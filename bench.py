@@ -13,7 +13,8 @@ One step = a batch of B (--batch, default 4) full FD waveforms on the device, ea
 workspace and outputs: spline build -> inverse splines -> interval records -> tile lists -> mode
 sum -> h+/hx over f >= 0 (the Likelihood path, emri_pe.py:241, for a batch of walkers). With
 --pipeline overlap (default) batch i+1's preparation (grouping, splines, records: latency-bound
-kernels on few CUs; efd_modesum_prepare per waveform) runs on a second stream beside batch i's
+kernels on few CUs; one efd_modesum_prepare_batch for the B waveforms) runs on a second stream
+beside batch i's
 mode sums, which run as one launch (efd_modesum_sum_batch: the B waveforms' tiles in one
 longest-first dispatch) and write h+/hx themselves (fused polarisations). value counts
 waveforms (B per step); --batch 1 runs one efd_modesum_sum per waveform.
@@ -217,6 +218,10 @@ def main():
     ap.add_argument("--batch", type=int, default=4,
                     help="overlap pipeline: waveforms per step, their mode sums in one launch "
                          "(efd_modesum_sum_batch; 1 = one efd_modesum_sum per waveform)")
+    ap.add_argument("--prep", default="batch", choices=["single", "batch"],
+                    help="overlap pipeline: one efd_modesum_prepare_batch over the step's B "
+                         "waveforms (9 launches per step), or each waveform's "
+                         "efd_modesum_prepare (round 2; 0.993x, 4 paired rounds)")
     ap.add_argument("--sum-priority", type=int, default=0,
                     help="overlap pipeline: torch stream priority of the sum stream (negative = "
                          "higher; the preparation stream keeps the default)")
@@ -246,7 +251,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from emri_frequencydomainwaveforms_amd import _lib
-    from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine, sum_batch
+    from emri_frequencydomainwaveforms_amd.summation import (DeviceInputs, ModeSumEngine,
+                                                             prepare_batch, sum_batch)
 
     w = build_workload(T=args.T, eps=args.eps)
     inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
@@ -288,9 +294,14 @@ def main():
             if not (args.diag_sum_only and i >= len(slots)):
                 if sl["sum_done"] is not None:    # the slot's previous sums have read it
                     s_prep.wait_event(sl["sum_done"])
-                for x in sl["wf"]:
-                    x["eng"].launch(inp, freq, None, True, w["prefactor"],
-                                    stream=s_prep.cuda_stream, phase="prepare")
+                if args.prep == "batch":
+                    prepare_batch([(x["eng"], dict(inp=inp, freq=freq, out=None,
+                                                   grid_symmetric=True, scale=w["prefactor"]))
+                                   for x in sl["wf"]], stream=s_prep.cuda_stream)
+                else:
+                    for x in sl["wf"]:
+                        x["eng"].launch(inp, freq, None, True, w["prefactor"],
+                                        stream=s_prep.cuda_stream, phase="prepare")
                 sl["prep_done"].record(s_prep)
                 ss.wait_event(sl["prep_done"])
             if B == 1:
@@ -392,7 +403,8 @@ def main():
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
                        "pipeline": args.pipeline + (" (diagnostic: sum only)"
                                                     if args.diag_sum_only else ""),
-                       "slots": len(slots), "sum_streams": len(s_sums), "batch": B},
+                       "slots": len(slots), "sum_streams": len(s_sums), "batch": B,
+                       "prep": args.prep},
             "roofline": dict(roof, **{
                 "kernel": "k_modesum_batch" if B > 1 else "k_modesum",
                 "kernel_ms": kern_ms, "kernel_ms_per_waveform": wf_ms,

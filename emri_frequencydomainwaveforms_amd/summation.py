@@ -288,6 +288,34 @@ def sum_batch(jobs, stream=None, prof_events=(None, None)):
     return wss
 
 
+def prepare_batch(jobs, stream=None):
+    """The preparations of several waveforms in one chain of launches
+    (efd_modesum_prepare_batch). jobs: (engine, launch_kwargs) pairs as sum_batch takes them;
+    each workspace ends bitwise as after the engine's own launch(..., phase="prepare"), so the
+    jobs go on to sum_batch / sum_batch_loglike / launch(phase="sum") unchanged."""
+    import ctypes
+    torch = _torch()
+    jobs = list(jobs)
+    if not 1 <= len(jobs) <= _lib.EFD_BATCH_MAX:
+        raise ValueError(f"prepare_batch takes 1..{_lib.EFD_BATCH_MAX} waveforms")
+    args, wss = [], []
+    for eng, kw in jobs:
+        a, ws = eng._args(**{k: v for k, v in kw.items() if k != "_args"})
+        eng._last_args = a
+        args.append(a)
+        wss.append(ws)
+    n = len(jobs)
+    pa = (ctypes.POINTER(_lib.ModesumArgs) * n)(*[ctypes.pointer(a) for a in args])
+    pw = (ctypes.c_void_p * n)(*[ws.data_ptr() for ws in wss])
+    pb = (ctypes.c_size_t * n)(*[ws.numel() for ws in wss])
+    lib = jobs[0][0].lib
+    freq = jobs[0][1]["freq"]
+    st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
+    _lib.check(lib.efd_modesum_prepare_batch(pa, pw, pb, n, st), "efd_modesum_prepare_batch",
+               lib)
+    return wss
+
+
 def _check_ll_io(torch, d, w, out, nb, n):
     if (d.dtype != torch.complex128 or tuple(d.shape) != (2, nb) or not d.is_contiguous()
             or w.dtype != torch.float64 or tuple(w.shape) != (2, nb) or not w.is_contiguous()

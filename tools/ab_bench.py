@@ -1,6 +1,6 @@
 """Interleaved end-to-end A/B of library variants through bench.py (GPU box).
 
-    python tools/ab_bench.py ROUNDS NAME [NAME ...]
+    python tools/ab_bench.py ROUNDS NAME[@ARG,...] [NAME[@ARG,...] ...]
 
 Each round runs `bench.py --no-cpu-baseline` once per variant, in a rotated order, each in its
 own child process with EFD_LIB pointing at the variant (names as in tools/exp_variants.py:
@@ -23,9 +23,13 @@ from exp_variants import lib_path  # noqa: E402
 
 
 def run_one(name, extra):
-    env = dict(os.environ, EFD_LIB=lib_path(name))
+    # NAME[@ARG,ARG...]: the variant's library plus its own bench.py arguments
+    lib, _, own = name.partition("@")
+    env = dict(os.environ, EFD_LIB=lib_path(lib))
+    own = [x for x in own.split(",") if x]
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline",
-                        *extra], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+                        *extra, *own], capture_output=True, text=True, timeout=300, env=env,
+                       cwd=ROOT)
     if r.returncode != 0:
         print(json.dumps({"variant": name, "error": r.returncode, "stderr": r.stderr[-1500:]}),
               flush=True)

@@ -32,12 +32,17 @@ def lib_path(name):
 
 
 def build(specs):
+    from emri_frequencydomainwaveforms_amd import _build
+    _build.build()   # the host objects (twin, upstream) every variant links, as the in-tree one
+    objs = [os.path.join(_build.OBJDIR, o)
+            for o in ("emrifd_cpu.o", "emrifd_host.o", "emrifd_modes.o")]
     os.makedirs(EXP, exist_ok=True)
     procs = []
     for spec in specs:
         name, _, flags = spec.partition(":")
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               *[f for f in flags.split(",") if f], "-o", lib_path(name), SRC]
+               *[f for f in flags.split(",") if f], "-o", lib_path(name), *objs, SRC,
+               "-lgomp", "-lmvec"]
         print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
     if any(p.wait() != 0 for p in procs):
