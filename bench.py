@@ -232,6 +232,9 @@ def main():
                     help="time emri_pe.py's likelihood instead (BASELINE configs 4 / 5): walker "
                          "half-steps through Likelihood (fused mode sum + logL), sharded over the "
                          "ranks by ShardedLikelihood (parameter broadcast + logL all-gather)")
+    ap.add_argument("--fused-group", type=int, default=0,
+                    help="--likelihood: walkers per fused group (Likelihood.FUSED_GROUP; 0 = its "
+                         "default)")
     ap.add_argument("--api-steps", type=int, default=2,
                     help="--likelihood: half-steps timed with the host upstream in the loop")
     args = ap.parse_args()
@@ -458,6 +461,8 @@ def bench_likelihood(args):
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     cfg = LIKE_CONFIGS[args.likelihood]
     s = pe.setup(**cfg)
+    if args.fused_group:
+        s.like.FUSED_GROUP = args.fused_group
     B = s.half_step
     batches = s.half_steps()
     if world > 1:

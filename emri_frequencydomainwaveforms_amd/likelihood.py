@@ -218,8 +218,11 @@ class Likelihood:
         return out.cpu().numpy()
 
     # walkers per fused group: one efd_modesum_prepare_batch and one efd_modesum_sum_loglike
-    # each; FUSED_DEPTH groups rotate so group i+1's preparation runs beside group i's sum
-    FUSED_GROUP = 8
+    # each; FUSED_DEPTH groups rotate so group i+1's preparation runs beside group i's sum.
+    # Balanced groups of at most 16 (EFD_BATCH_MAX): config 5's 64-walker half-steps (host-bound,
+    # 43-tile grids) ran 54-60 k logL/s in 4 groups against 40-51 k in 8 (5 interleaved rounds);
+    # config 4's 8 walkers are one group either way (groups of 4 or 3: -5 to -10%)
+    FUSED_GROUP = 16
     FUSED_DEPTH = 2
 
     def _get_ll_fused(self, tm, params, args, kwargs, out):

@@ -71,6 +71,36 @@ def test_prepare_batch_bitwise_equals_single(sources, caustic):
             assert st[0] > 0
 
 
+def test_prepare_batch_polarisations_bitwise(sources):
+    """BatchPreparer jobs summed with fused h+/hx (tools/configs.py's config-3 path) give bitwise
+    the polarisations of each waveform's own prepare + sum."""
+    freq_h = sources[0]["freq"]
+    freq = torch.as_tensor(freq_h, device="cuda")
+    nf = int(freq.numel())
+    k0 = int(np.searchsorted(freq_h, 0.0))
+    B = BatchPreparer(group=len(sources))
+    B.order_after_current()
+    for d in sources:
+        B.submit(_host(d), freq, True, d["prefactor"], k0=k0, prepare_only=True)
+    gi, jobs = B.flush()
+    outs = [(torch.empty(nf - k0, dtype=torch.complex128, device="cuda"),
+             torch.empty(nf - k0, dtype=torch.complex128, device="cuda")) for _ in sources]
+    sum_batch([(eng, dict(kw, hp=torch.view_as_real(o[0]), hc=torch.view_as_real(o[1])))
+               for (eng, kw), o in zip(jobs, outs)], stream=B.stream(gi).cuda_stream)
+    B.wait()
+    for d, (hp, hc) in zip(sources, outs):
+        h = _host(d)
+        inp = DeviceInputs.from_host(h["t"], h["amp"], h["phi_phi"], h["phi_r"], h["f_phi"],
+                                     h["f_r"], h["m"], h["n"], h["ylm_p"], h["ylm_m"])
+        eng = ModeSumEngine()
+        rp = torch.empty(nf - k0, dtype=torch.complex128, device="cuda")
+        rc = torch.empty_like(rp)
+        eng.launch(inp, freq, None, True, d["prefactor"], hp=torch.view_as_real(rp),
+                   hc=torch.view_as_real(rc), k0=k0)
+        assert eng.status()
+        assert torch.equal(hp, rp) and torch.equal(hc, rc)
+
+
 def test_prepare_batch_loglike_bitwise(sources):
     freq_h = sources[0]["freq"]
     freq = torch.as_tensor(freq_h, device="cuda")

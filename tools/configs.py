@@ -130,18 +130,54 @@ def config3(reps, slots=4):
         sweep()
     _sync()
     pipe.wait()
+    dev_pipe = (time.perf_counter() - t0) / reps
+
+    # batched: groups of 16 grid points, each one packed upload + efd_modesum_prepare_batch on
+    # a group stream and one efd_modesum_sum_batch writing every point's h+/hx (two groups in
+    # flight; a group's outputs and workspaces are reused after its sum's event)
+    from emri_frequencydomainwaveforms_amd.summation import BatchPreparer, sum_batch
+    G = 16
+    prep = BatchPreparer(group=G, depth=2)
+    gouts = [[(torch.empty_like(hp), torch.empty_like(hc)) for _ in range(G)]
+             for _ in range(2)]
+    s_sum = torch.cuda.Stream()
+
+    def sweep_batched():
+        prep.order_after_current()
+        s_sum.wait_stream(torch.cuda.current_stream())
+        for g0 in range(0, len(ws), G):
+            for w, host in zip(ws[g0:g0 + G], hosts[g0:g0 + G]):
+                prep.submit(host, freq, True, w["prefactor"], k0=k0, prepare_only=True)
+            gi, jobs = prep.flush()
+            s_sum.wait_stream(prep.stream(gi))
+            sum_batch([(eng, dict(kw, hp=o[0], hc=o[1])) for (eng, kw), o in zip(jobs, gouts[gi])],
+                      stream=s_sum.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(s_sum)
+            prep.release(gi, ev)
+        torch.cuda.current_stream().wait_stream(s_sum)
+    sweep_batched()
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sweep_batched()
+    _sync()
+    prep.wait()
     dev = (time.perf_counter() - t0) / reps
     K = [len(w["m"]) for w in ws]
     return {"config": "config3: 10x10 grid M=logspace(5,7) e0=linspace(0.1,0.6) mu=1e-5 M "
                       "Tobs=1yr dt=10s eps=1e-2", "waveforms": len(ws), "N_f": nf,
             "harmonics_min_max": [min(K), max(K)],
             "device_waveforms_per_s": len(ws) / dev, "device_ms_per_grid": dev * 1e3,
+            "pipeline_waveforms_per_s": len(ws) / dev_pipe,
             "api_waveforms_per_s": len(ws) / (host_s + dev),
             "host_upstream_s_per_grid": host_s, "pipeline_slots": slots,
-            "device_note": "100 waveforms back to back through WaveformPipeline (each "
-                           "waveform's upload + preparation + mode sum with h+/hx on one of "
-                           f"{slots} streams, several in flight); api adds the host stand-in "
-                           "upstream incl. the p0 root solve per point"}
+            "device_note": "100 waveforms in groups of 16: one packed upload and one "
+                           "efd_modesum_prepare_batch per group on a group stream, one "
+                           "efd_modesum_sum_batch writing each point's h+/hx, two groups in "
+                           "flight (pipeline_waveforms_per_s: round 2's WaveformPipeline, "
+                           f"each waveform's chain on one of {slots} streams); api adds the "
+                           "host stand-in upstream incl. the p0 root solve per point"}
 
 
 def _likelihood_setup(T, eps, downsample, nwalkers, seed=2601996):
@@ -189,9 +225,10 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
             "fused_likelihood": fused,
             "device_note": "Likelihood.get_ll over the half-step batch with the host upstream "
                            "memoised: " + (
-                               "per walker the input upload and preparation on a "
-                               "WaveformPipeline slot, per group of 8 walkers one mode-sum "
-                               "launch with the likelihood fused in (no template written)"
+                               "per balanced group of up to 16 walkers one packed input "
+                               "upload (efd_stage_batch), one efd_modesum_prepare_batch and "
+                               "one mode-sum launch with the likelihood fused in (no "
+                               "template written); two groups in flight"
                                if fused else
                                "per walker the FD template (input upload, mode sum with h+/hx "
                                "straight into a slot's buffer) + efd_loglike on one of "
