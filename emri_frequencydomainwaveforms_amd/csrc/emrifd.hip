@@ -1083,6 +1083,66 @@ __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
 }
 
 // One interval record of group h; `evals` = its (branch x bin) evaluation count.
+// EFD_SAFE_REC: a record whose every lane is known to pass the fast path's per-lane validity
+// tests -- t(g) inside the record's knot interval and F' of the record's sign, nonzero -- skips
+// them (Item::fdneg bit 1, header bit 25): one 64-bit compare and one class test per bin, with
+// their ballots and mask arithmetic. Certified here on the device, with the kernel's own
+// arithmetic: t(g) is monotonic over the record's g range (its derivative keeps one sign at the
+// range's ends and at the derivative's vertex), w = t(g) - t_j at the range's end bins (bitwise
+// the values k_modesum computes there) lies inside [0, dtj) with a 1e-6 dtj margin for the
+// interior bins' rounding, and F' keeps the record's sign over the whole interval with a margin
+// of 1e-12 of its terms. Fold and edge records (overshooting t(g), turning points) keep the
+// tests; a safe record's lanes would all have passed them, so the spectrum is bitwise the same.
+#ifndef EFD_SAFE_REC
+#define EFD_SAFE_REC 1
+#endif
+__device__ bool record_safe(const Item& it, const double* __restrict__ freq, int64_t lo0,
+                            int64_t hi0, int64_t lo1, int64_t hi1) {
+    // the g range of the lanes: s = 0 lanes k in [lo0, hi0) at g = -freq[k], s = 1 at +freq[k]
+    double ga = INFINITY, gb = -INFINITY;
+    if (hi0 > lo0) {
+        ga = fmin(ga, fmin(-freq[lo0], -freq[hi0 - 1]));
+        gb = fmax(gb, fmax(-freq[lo0], -freq[hi0 - 1]));
+    }
+    if (hi1 > lo1) {
+        ga = fmin(ga, fmin(freq[lo1], freq[hi1 - 1]));
+        gb = fmax(gb, fmax(freq[lo1], freq[hi1 - 1]));
+    }
+    if (!(ga <= gb)) return false;   // no lanes (or NaN)
+    // the fast path's w at both ends (its exact operations)
+    auto wat = [&](double g) {
+        const double u = g - it.gx;
+        const double tt = fma(fma(fma(it.ic[0], u, it.ic[1]), u, it.ic[2]), u, it.ic[3]);
+        return tt - it.tj;
+    };
+    const double wa = wat(ga), wb = wat(gb);
+    const double mg = 1e-6 * it.dtj;
+    if (!(fmin(wa, wb) >= mg && fmax(wa, wb) <= it.dtj - mg)) return false;
+    // monotonic t(u): t'(u) = 3 c0 u^2 + 2 c1 u + c2 of one sign at both ends and at its vertex
+    const double ua = ga - it.gx, ub = gb - it.gx;
+    auto dt = [&](double u) { return fma(fma(3.0 * it.ic[0], u, 2.0 * it.ic[1]), u, it.ic[2]); };
+    const double da = dt(ua), db = dt(ub);
+    if (!((da > 0.0 && db > 0.0) || (da < 0.0 && db < 0.0))) return false;
+    if (it.ic[0] != 0.0) {
+        const double uv = -it.ic[1] / (3.0 * it.ic[0]);
+        if (uv > ua && uv < ub) {
+            const double dv = dt(uv);
+            if (!((dv > 0.0) == (da > 0.0) && dv != 0.0)) return false;
+        }
+    }
+    // F'(w) = (fd0 w + fd1) w + fd2 of the record's sign on [0, dtj], away from 0
+    const double* f = it.fd;
+    const double scale = fabs(f[0]) * it.dtj * it.dtj + fabs(f[1]) * it.dtj + fabs(f[2]);
+    const double sg = (it.fdneg & 1) ? -1.0 : 1.0;
+    auto fq = [&](double x) { return sg * fma(fma(f[0], x, f[1]), x, f[2]); };
+    double fmn = fmin(fq(0.0), fq(it.dtj));
+    if (f[0] != 0.0) {
+        const double xv = -f[1] / (2.0 * f[0]);
+        if (xv > 0.0 && xv < it.dtj) fmn = fmin(fmn, fq(xv));
+    }
+    return fmn > 1e-12 * scale && isfinite(scale);
+}
+
 __device__ void build_item(
     const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
     const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int ni, int K,
@@ -1190,6 +1250,9 @@ __device__ void build_item(
     it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
     it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
     ranges[(size_t)h * ni + j] = make_int4((int)lo0, (int)hi0, (int)lo1, (int)hi1);
+#if EFD_SAFE_REC
+    if (record_safe(it, freq, lo0, hi0, lo1, hi1)) it.fdneg |= 2;
+#endif
     // branch x bin evaluations (on a paired grid one lane serves both the branch and its partner)
     const int mult = paired ? 1 + partner : 1;
     evals = (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
@@ -1456,10 +1519,22 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 // one FMA less on the longest dependency chain of an evaluation (k_modesum +1.2-1.6%, the
 // spectrum moves by 8e-12 of max|S| at config 2; -DEFD_CW_TWO_PART restores the second term).
 constexpr int SCTAB = 512;
+// EFD_COS_MM: the cosine on |r| <= pi/512 as COS_A - z/2 (z = r^2) with the constant chosen
+// minimax (max error 2.95e-11 = half the dropped z^2/24 at r = pi/512; mpmath), one FMA instead
+// of the r^4 Taylor form's two. 2.95e-11 of a term is far below the ~1e-9 rad rounding every
+// term's phase already carries (phases reach 1e7 rad). The slope stays -0.5 (an inline
+// constant: the free minimax slope, 7.4e-12, cost an SGPR pair and VGPR moves in the record
+// loop). COS_A is the constant callers pass as c0 (J <= 2 records fold rho - 1 into it:
+// fma(-v, v, COS_A) = COS_A rho to 2e-20).
+#ifndef EFD_COS_MM
+#define EFD_COS_MM 1
+#endif
+constexpr double COS_A = EFD_COS_MM ? 1.000000000029531 : 1.0;
+constexpr double COS_B = -0.5;
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
                                            double& s, double& c, double extra = 0.0,
                                            bool use_extra = false, double extra_scale = 1.0,
-                                           double c0 = 1.0) {
+                                           double c0 = COS_A) {
     constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
     constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
     constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
@@ -1488,7 +1563,11 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
 #endif
     // c0: the cosine polynomial's constant term (1, or a factor 1 + O(1e-9) folded in by the
     // caller: rho (1 + d) E to within |d| |sr| < 3e-12, see EFD_EARLY_MASK)
+#if EFD_COS_MM
+    const double cr = fma(z, COS_B, c0);
+#else
     const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), c0);
+#endif
     s = fma(t.x, cr, t.y * sr);
     c = fma(t.y, cr, -t.x * sr);
 }
@@ -1875,9 +1954,13 @@ struct RecSign {
     int32_t fdcls;   // v_cmp_class mask: F' normal or subnormal of the record's sign
     int32_t shift;   // sign(F') 3 pi / 4 in table steps
     double kth;      // theta = kth * min(|thn|, 1): KTH0 with the sign of F'
+    bool safe;       // every lane passes the interval and sign tests (EFD_SAFE_REC)
 };
-__device__ __forceinline__ RecSign rec_sign(bool fdneg) {
+// bits: Item::fdneg (bit 0: F' < 0, bit 1: safe record)
+__device__ __forceinline__ RecSign rec_sign(uint32_t bits) {
+    const bool fdneg = bits & 1u;
     RecSign r;
+    r.safe = EFD_SAFE_REC && (bits & 2u);
     r.fdcls = fdneg ? 0x018 : 0x180;
     r.shift = fdneg ? -192 : 192;
     r.kth = EFD_VSCALE ? (fdneg ? -KTH0 / VS : KTH0 / VS) : (fdneg ? -KTH0 : KTH0);
@@ -1919,14 +2002,20 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
     const double u = sfk - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     w = tt - it->tj;
-    uint64_t goodm = __builtin_amdgcn_ballot_w64((unsigned long long)__double_as_longlong(w) <
-                                                 (unsigned long long)__double_as_longlong(it->dtj));
     const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
 #if EFD_REC_SIGN
-    goodm &= class_mask(fd, rs.fdcls);
+    uint64_t goodm = ~0ull;
+    if (!rs.safe) {   // wave-uniform: a record k_items could not certify tests every lane
+        asm volatile("");
+        goodm = __builtin_amdgcn_ballot_w64((unsigned long long)__double_as_longlong(w) <
+                                            (unsigned long long)__double_as_longlong(it->dtj)) &
+                class_mask(fd, rs.fdcls);
+    }
 #else
+    uint64_t goodm = __builtin_amdgcn_ballot_w64((unsigned long long)__double_as_longlong(w) <
+                                                 (unsigned long long)__double_as_longlong(it->dtj));
     goodm &= __builtin_amdgcn_ballot_w64(afd > 0.0);
     const int shift = fd > 0.0 ? 192 : -192;
 #endif
@@ -1978,10 +2067,10 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
             thn = ww * fma(KTHN[1], uu, 1.0);
 #endif
             am = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm & goodm), ampm * r);
-            c0 = 1.0;
+            c0 = COS_A;
         } else {
 #if EFD_VSCALE
-            c0 = fma(-ww, ww, 1.0);   // 1 + KRH_1 w^2 = 1 - v^2
+            c0 = fma(-ww, ww, COS_A);   // (1 + KRH_1 w^2) COS_A = (1 - v^2) COS_A
 #else
             c0 = fma(KRH[1], ww * ww, 1.0);
 #endif
@@ -2499,7 +2588,7 @@ __device__ __forceinline__ void modesum_tile(
             static_assert(FAST_J < 8, "header: jser in 3 bits");
             constexpr int HB = TILE_LANES < 1024 ? 10 : 11;   // bits of a tile-relative bound
             constexpr uint32_t HM = (1u << HB) - 1u;
-            static_assert(TILE_LANES < 2048 && 2 * HB + 5 <= 32, "header: one 32-bit word");
+            static_assert(TILE_LANES < 2048 && 2 * HB + 6 <= 32, "header: one 32-bit word");
             uint32_t hdr = 0;
             if (lane < nin) {
                 const uint32_t kl = keys[c * NC + lane];
@@ -2572,7 +2661,10 @@ __device__ __forceinline__ void modesum_tile(
                     double wr[BPL], wi[BPL], w[BPL];
 #if EFD_SALU_MASKS
                     uint64_t needm[BPL], needany = 0;
-                    const RecSign rs = rec_sign((ha >> (2 * HB + 4)) & 1u);
+                    const RecSign rs = rec_sign((ha >> (2 * HB + 4)) & 3u);
+#ifdef EFD_EXP_COUNT   // [29]: wave-records of certified-safe records
+                    if (lane == 0 && rs.safe) atomicAdd(&g_exp_count[29], 1ull);
+#endif
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t base = w_lo + 64 * i;

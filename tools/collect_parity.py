@@ -14,7 +14,10 @@ def main(src, dst):
         out["records"][os.path.basename(f)[:-5]] = json.load(open(f))
     json.dump(out, open(dst, "w"), indent=1)
     for name, r in out["records"].items():
-        if "walkers" in r:
+        if "max_rel_off_extrap" in r:
+            print(f"{name:24s} linearity max dev {r['max_rel_off_extrap']:.2e} of max|S| off the "
+                  f"{r['extrap_bins']} extrapolated-term bins ({r['max_rel']:.2e} on them)")
+        elif "walkers" in r:
             print(f"{name:24s} walkers {r['walkers']:3d}  max |ll_gpu - ll_oracle| / bound "
                   f"{r['max_err_over_bound']:.2e}")
         else:

@@ -132,7 +132,7 @@ def child(name, ref_path):
              "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18", "cold_wave_evals", "cold_wave_lanes",
              "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1",
              "chunk_max_wave_evals", "chunk_wave_evals", "chunks", "segments",
-             "tile_hits"))}
+             "tile_hits", "safe_wave_evals"))}
         c = out["counters_per_launch"]
         if c["chunk_wave_evals"] > 0:
             # wave-time lost at the chunk barriers if every record evaluation cost the same
