@@ -2932,6 +2932,7 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
 // one workgroup per waveform, fixed order (a strided pass per thread, then a tree)
 struct LlBatch {
     const double* part[EFD_BATCH_MAX];
+    const Header* hdr[EFD_BATCH_MAX];
     double* out;
     int64_t ntiles;
     int32_t n;
@@ -2966,7 +2967,14 @@ __global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
         if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
     }
-    if (threadIdx.x == 0) lb.out[blockIdx.x] = -0.5 * 4.0 * red[0];
+    if (threadIdx.x == 0) {
+        // a walker whose workspace holds a device-side error flag gets a NaN log-likelihood
+        // (the flags stay set: efd_modesum_status_batch reports and clears them), so a caller
+        // that finds no NaN in the batch needs no status synchronisation
+        const Header* h = lb.hdr[blockIdx.x];
+        const bool bad = h->runs_overflow | h->bad_mn | h->bad_tile;
+        lb.out[blockIdx.x] = bad ? __longlong_as_double(0x7ff8000000000000LL) : -0.5 * 4.0 * red[0];
+    }
 }
 
 // K6: the tiles' record lists, built in the preparation phase (k_modesum DMAs them in). The same
@@ -3887,7 +3895,10 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         LlBatch lb{};
         lb.n = count;
         lb.ntiles = L0.ntiles;
-        for (int i = 0; i < count; ++i) lb.part[i] = batch.d[i].llpart;
+        for (int i = 0; i < count; ++i) {
+            lb.part[i] = batch.d[i].llpart;
+            lb.hdr[i] = (const Header*)workspace[i];
+        }
         lb.out = llout;
         hipLaunchKernelGGL(k_ll_final, dim3((unsigned)count), dim3(256), 0, st, lb);
         HIP_TRY(hipGetLastError());

@@ -184,8 +184,12 @@ class Likelihood:
                 h = self._as_channels(h_all[i])
                 self._red.loglike(h, self._d, self._w, out=out[i:i + 1])
         elif (getattr(tm, "can_pipeline", False) and self.fused_likelihood
-              and self._get_ll_fused(tm, params, args, kwargs, out)):
-            pass
+              and (host := self._get_ll_fused(tm, params, args, kwargs, out)) is not None):
+            if self.noise_has_been_added:
+                raise NotImplementedError
+            if self.use_gpu and self.return_cupy:
+                return out
+            return host
         elif getattr(tm, "can_pipeline", False):
             # several walkers in flight: each pipeline slot has its own template buffer,
             # stream and reduction scratch; walker i's template and logL run on one slot's
@@ -231,13 +235,16 @@ class Likelihood:
         (BatchPreparer), one upload and one efd_modesum_prepare_batch prepare the group on its
         stream, and one efd_modesum_sum_loglike on a sum stream writes the group's
         log-likelihoods into out (the templates never reach HBM). A group's workspaces are reused
-        only after the sum that read them (an event per group). Returns False, before queueing
-        anything, when the template's grid is not symmetric (the caller takes the per-walker
-        path)."""
+        only after the sum that read them (an event per group). Returns the log-likelihoods on
+        the host (copied out in the sum stream's order: one synchronisation per batch), or None,
+        before queueing anything, when the template's grid is not symmetric (the caller takes the
+        per-walker path). A walker whose preparation or sum raised a device-side error comes
+        back NaN from the kernel (efd_modesum_sum_loglike), and only then are the groups'
+        status flags read, which raises."""
         torch = self.torch
         from .summation import BatchPreparer
         if not self._fused_grid_ok(tm, kwargs):
-            return False
+            return None
         if hasattr(tm, "prefetch"):
             tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
         n = len(params)
@@ -270,14 +277,21 @@ class Likelihood:
                 ev = torch.cuda.Event()
                 ev.record(s_sum)
                 B.release(gi, ev)
+            pin = F.get("pin")
+            if pin is None or pin.numel() < n:
+                pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
+            with torch.cuda.stream(s_sum):
+                pin[:n].copy_(out[:n], non_blocking=True)
         finally:
             B._pending = []
             # `out` belongs to the current stream: nothing may still write it when it is
             # returned, or freed after an exception
             s_sum.synchronize()
-        B.wait()   # device-side errors of every group's workspaces (sticky across reuse)
+        host = pin[:n].numpy().copy()
+        if np.isnan(host).any():
+            B.wait()   # device-side errors of the groups' workspaces (sticky across reuse)
         cur.wait_stream(s_sum)
-        return True
+        return host
 
     def _fused_grid_ok(self, tm, kwargs):
         """Whether the template's grid for these kwargs is mirror-symmetric (the fused sum's

@@ -123,9 +123,12 @@ class MemoizedUpstream:
             wg.prefetch = lambda calls: 0   # the memo holds the upstream: nothing to prefetch
 
     def __call__(self, *args, **kwargs):
-        key = (tuple(float(a) if isinstance(a, (float, int, np.floating)) else a for a in args),
-               tuple(sorted((k, ("id", id(v)) if hasattr(v, "shape") else v)
-                            for k, v in kwargs.items())))
+        # submit_batch calls positionally with plain floats (and None / bool flags): the args
+        # tuple is the key, as prepare()'s own prefetch lookup keys on them
+        key = args if not kwargs else (
+            tuple(float(a) if isinstance(a, (float, int, np.floating)) else a for a in args),
+            tuple(sorted((k, ("id", id(v)) if hasattr(v, "shape") else v)
+                         for k, v in kwargs.items())))
         hit = self.memo.get(key)
         if hit is None:
             t0 = self._time()

@@ -131,6 +131,11 @@ def _staged_upload(arrays, dev, stream=None, staging=None):
     return [d[o:o + a.nbytes].view(dt[a.dtype]) for a, o in zip(arrays, offs)]
 
 
+# efd_modesum_workspace_bytes per (N_t, K, N_f): walkers repeat shapes, and the lookup is cheaper
+# than the ctypes call
+_WS_BYTES = {}
+
+
 class ModeSumEngine:
     """Owns the workspace and launches efd_modesum on the current torch stream."""
 
@@ -141,6 +146,7 @@ class ModeSumEngine:
         self.lib = _lib.load()
         self._ws = None
         self._ws_key = None
+        self._ws_cap, self._ws_dev = 0, None
         self._last_args = None
         self.last_contributions = None
 
@@ -148,10 +154,18 @@ class ModeSumEngine:
         """The workspace for (nt, K, nf), grown when too small. With `stream` (a torch stream)
         a new allocation is made on it, so the caching allocator ties the block to the stream
         that uses it (WaveformPipeline slots)."""
+        key = (nt, K, nf)
+        nbytes = _WS_BYTES.get(key)
+        if nbytes is None:
+            nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf))
+            if nbytes == 0:
+                raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
+            if len(_WS_BYTES) > 65536:
+                _WS_BYTES.clear()
+            _WS_BYTES[key] = nbytes
+        if self._ws is not None and self._ws_cap >= nbytes and self._ws_dev == device:
+            return self._ws   # the walker-batch fast path: no torch calls
         torch = _torch()
-        nbytes = int(self.lib.efd_modesum_workspace_bytes(nt, K, nf))
-        if nbytes == 0:
-            raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
         if self._ws is None or self._ws.numel() < nbytes or self._ws.device != device:
             old = self._ws if self._ws is not None and self._ws.device == device else None
             self._ws = None
@@ -167,6 +181,7 @@ class ModeSumEngine:
                 else:
                     ws[:64].zero_()
             self._ws = ws
+        self._ws_cap, self._ws_dev = self._ws.numel(), self._ws.device
         return self._ws
 
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
@@ -622,14 +637,20 @@ class BatchPreparer:
                                 accumulate=1 if acc else 0, k0=k0)
         if any(p[2] != sym or p[4] != k0 or p[5] != acc for p in pend):
             raise ValueError("flush: grid symmetry, k0 and accumulate must agree in a group")
-        src = np.empty((n, 10), dtype=np.uint64)
-        shape = np.empty((n, 2), dtype=np.int32)
-        scale = np.empty((n, 2), dtype=np.float64)
         keep = []    # arrays converted here stay alive until the staging copy below
+        fast = [p[0].get("_src") for p in pend]
+        scale = np.array([(p[3].real, p[3].imag) for p in pend], dtype=np.float64)
+        if all(f is not None for f in fast):
+            # the native upstream's walkers (prepare() records their arrays' addresses): one
+            # conversion for the group instead of row by row
+            src = np.array(fast, dtype=np.uint64)
+            shape = np.array([p[0]["_shape"] for p in pend], dtype=np.int32)
+        else:
+            src = np.empty((n, 10), dtype=np.uint64)
+            shape = np.empty((n, 2), dtype=np.int32)
         for i, (host, _, _, sc, _, _) in enumerate(pend):
-            fast = host.get("_src")
-            if fast is not None:
-                src[i] = fast
+            if fast[i] is not None:
+                src[i] = fast[i]
                 shape[i] = host["_shape"]
             else:
                 amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
@@ -647,7 +668,6 @@ class BatchPreparer:
                 keep.append(arrays)
                 src[i] = [a.ctypes.data for a in arrays]
                 shape[i] = (nt, K)
-            scale[i] = (sc.real, sc.imag)
         total = ctypes.c_size_t(0)
         for attempt in range(2):
             pin = G["pin"]
@@ -673,13 +693,15 @@ class BatchPreparer:
         G["pin_done"].record(st)
         A, pw, pb = G["args"], G["pw"], G["pb"]
         jobs = []
-        for i in range(n):
+        dev = freq.device
+        for i, (nt_i, K_i) in enumerate(shape.tolist()):
             eng = G["engines"][i]
-            ws = eng._workspace(int(shape[i, 0]), int(shape[i, 1]), nf, freq.device, stream=st)
+            ws = eng._workspace(nt_i, K_i, nf, dev, stream=st)
             pw[i] = ws.data_ptr()
-            pb[i] = ws.numel()
-            eng._last_args = A[i]
-            jobs.append((eng, dict(freq=freq, k0=k0, grid_symmetric=sym, _args=A[i])))
+            pb[i] = eng._ws_cap
+            a_i = A[i]
+            eng._last_args = a_i
+            jobs.append((eng, {"freq": freq, "k0": k0, "grid_symmetric": sym, "_args": a_i}))
         _lib.check(self.lib.efd_modesum_prepare_batch(G["pa"], ctypes.cast(pw, ctypes.POINTER(
             ctypes.c_void_p)), pb, n, st.cuda_stream), "efd_modesum_prepare_batch", self.lib)
         G["used"] = True

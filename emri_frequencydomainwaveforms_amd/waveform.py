@@ -341,19 +341,23 @@ class GenerateEMRIWaveform:
         if not sym:
             raise ValueError("submit_batch needs a symmetric grid (the fused likelihood's)")
         kc = cw._k0
+        submit = preparer.submit
         for prm in np.asarray(params, dtype=np.float64).reshape(-1, 14).tolist():
             M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
             theta, phi, rot = self._angles(qS, phiS, qK, phiK)
             d = gen.prepare(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
                             mode_selection, include_minus_m)
+            scale = rot * (mu * MRSUN_SI / (dist * Gpc))   # the spectrum path's rounding
+            if "_src" in d:
+                # the native upstream recorded its arrays' addresses: the preparer stages them
+                # straight from prepare()'s dict
+                submit(d, freq, True, scale, k0=kc, prepare_only=True)
+                continue
             K = len(d["m"])
             y = d["ylms"]
-            preparer.submit(dict(t=d["t"], amp=d["teuk"], phi_phi=d["Phi_phi"],
-                                 phi_r=d["Phi_r"], f_phi=d["f_phi"], f_r=d["f_r"], m=d["m"],
-                                 n=d["n"], ylm_p=y[:K], ylm_m=y[K:], _src=d.get("_src"),
-                                 _shape=d.get("_shape"), _keep=d),
-                            freq, True, rot * (mu * MRSUN_SI / (dist * Gpc)), k0=kc,
-                            prepare_only=True)
+            submit(dict(t=d["t"], amp=d["teuk"], phi_phi=d["Phi_phi"], phi_r=d["Phi_r"],
+                        f_phi=d["f_phi"], f_r=d["f_r"], m=d["m"], n=d["n"], ylm_p=y[:K],
+                        ylm_m=y[K:], _keep=d), freq, True, scale, k0=kc, prepare_only=True)
 
     def prefetch(self, params, T=1.0, dt=10.0, eps=1e-5, mode_selection=None,
                  include_minus_m=True, **kwargs):

@@ -164,7 +164,10 @@ int efd_modesum_prepare_batch(const efd_modesum_args* const* a, void* const* wor
  * grid_symmetric = 1, accumulate = 0 and the same k0; hp/hc/out of a[i] are still written when
  * non-NULL. out: count device doubles. Per-tile partials live in each workspace; the final
  * reduction has a fixed order (bitwise reproducible; equal to efd_loglike on the written
- * templates to rounding). An extension for batched likelihood callers.
+ * templates to rounding). A waveform whose workspace holds a device-side error flag (see
+ * efd_modesum_status) gets out[i] = NaN, and its flags stay set: a caller that finds no NaN
+ * needs no status synchronisation, one that does calls efd_modesum_status_batch for the
+ * message. An extension for batched likelihood callers.
  */
 int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* workspace,
                             const size_t* workspace_bytes, int32_t count, const double* d,

@@ -11,6 +11,6 @@ for c in 4 5; do
   tail -3 $O/host_c$c.txt
 done
 for c in config4 config5; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run -- python bench.py --likelihood $c --steps 6 --warmup 2 --api-steps 0 > $O/prof_$c.log 2>&1 || { tail -20 $O/prof_$c.log; exit 2; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o run -- python bench.py --likelihood $c --steps 6 --warmup 2 --api-steps 0 > $O/prof_$c.log 2>&1 || { tail -20 $O/prof_$c.log; exit 2; }
 done
 find $O -name "*kernel_stats.csv" | head
