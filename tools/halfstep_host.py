@@ -1,0 +1,82 @@
+"""Host time of one fused-likelihood half-step by phase (config 4 / 5, memoised upstream).
+
+    python tools/halfstep_host.py config4|config5
+
+Runs bench.py's likelihood setup (pe.setup) with a copy of Likelihood._get_ll_fused that adds
+timers between its phases (grid check and prefetch, stream setup, submit_batch, flush,
+sum_loglike and events, the final synchronisation, the status check) and prints microseconds
+per half-step. Keep the copy in step with likelihood.py when that changes.
+"""
+import sys, time, json, collections
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+import numpy as np, torch
+import bench
+from emri_frequencydomainwaveforms_amd import pe, likelihood as L
+from emri_frequencydomainwaveforms_amd.summation import BatchPreparer
+cfg = bench.LIKE_CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "config5"]
+s = pe.setup(**cfg)
+batches = s.half_steps()
+memo = pe.MemoizedUpstream(s.few.waveform_generator)
+acc = collections.defaultdict(float)
+pc = time.perf_counter
+def fused(self, tm, params, args, kwargs, out):
+    t0 = pc()
+    if not self._fused_grid_ok(tm, kwargs):
+        return False
+    if hasattr(tm, "prefetch"):
+        tm.prefetch(params, *args, **kwargs)
+    t1 = pc(); acc["grid+prefetch"] += t1 - t0
+    n = len(params)
+    ngroups = -(-n // self.FUSED_GROUP)
+    G = -(-n // ngroups)
+    caustic = "uniform"
+    F = self._fused
+    if F is None:
+        F = self._fused = dict(prep=BatchPreparer(max(G, self.FUSED_GROUP), self.FUSED_DEPTH, caustic=caustic, device=self.device), stream=torch.cuda.Stream(self.device))
+    B, s_sum = F["prep"], F["stream"]
+    cur = torch.cuda.current_stream(self.device)
+    B.order_after_current()
+    s_sum.wait_stream(cur)
+    t2 = pc(); acc["setup"] += t2 - t1
+    batch = tm.submit_batch
+    for g0 in range(0, n, G):
+        ta = pc()
+        batch(B, params[g0:g0 + G], *args, **kwargs)
+        tb = pc(); acc["submit_batch"] += tb - ta
+        gi, jobs = B.flush()
+        tc = pc(); acc["flush"] += tc - tb
+        s_sum.wait_stream(B.stream(gi))
+        B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)], s_sum.cuda_stream)
+        ev = torch.cuda.Event(); ev.record(s_sum); B.release(gi, ev)
+        td = pc(); acc["sum+events"] += td - tc
+    pin = F.get("pin")
+    if pin is None or pin.numel() < n:
+        pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
+    with torch.cuda.stream(s_sum):
+        pin[:n].copy_(out[:n], non_blocking=True)
+    t3 = pc()
+    B._pending = []
+    s_sum.synchronize()
+    t4 = pc(); acc["sync"] += t4 - t3
+    host = pin[:n].numpy().copy()
+    if np.isnan(host).any():
+        B.wait()
+    cur.wait_stream(s_sum)
+    t5 = pc(); acc["status"] += t5 - t4
+    return host
+L.Likelihood._get_ll_fused = fused
+orig_get_ll = L.Likelihood.get_ll
+def get_ll(self, *a, **k):
+    t0 = pc(); r = orig_get_ll(self, *a, **k); acc["get_ll_total"] += pc() - t0; return r
+L.Likelihood.get_ll = get_ll
+for i in range(5):
+    s.like(batches[i % len(batches)], **s.kwargs)
+torch.cuda.synchronize()
+acc.clear()
+N = 40
+t0 = pc()
+for i in range(N):
+    s.like(batches[i % len(batches)], **s.kwargs)
+wall = pc() - t0
+print(json.dumps({"cfg": sys.argv[1:], "walkers": s.half_step, "ms_per_half_step": wall / N * 1e3,
+                  "us_per_half_step": {k: v / N * 1e6 for k, v in acc.items()}}, indent=1))
