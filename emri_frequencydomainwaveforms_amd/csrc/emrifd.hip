@@ -244,7 +244,9 @@ struct PrepDesc {
     double sc_re, sc_im;
     int32_t nt, K;
     int32_t lists;   // 1: prebuilt tile lists (k_tile_keys), 3: and cost-ordered dispatch
-    int32_t pad;
+    int32_t pcr;     // bit 0: k_prep_pcr_b builds the trajectory and inverse splines, bit 1:
+                     // and the amplitude splines (else k_prep_b's roles); set per waveform from
+                     // its own (N_t, K), so a workspace never depends on its batch
 };
 struct PrepBatch {
     PrepDesc d[EFD_BATCH_MAX];
@@ -392,6 +394,135 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
 // derivative of a cubic piece at w (scipy evaluates c2 + 2 c1 w + 3 c0 w^2 by power sum)
 __device__ __forceinline__ double dcubic(const double* c, double w) {
     return (c[2] + (2.0 * c[1]) * w) + (3.0 * c[0]) * (w * w);
+}
+
+// ----------------------------------------------------------------------------------------
+// The same not-a-knot system solved by one wave with parallel cyclic reduction (EFD_PCR).
+// spline_not_a_knot's Thomas sweeps are serial chains of ~2n dependent steps per interpolant,
+// with CP/DP round trips through global memory: k_prep took 60-75 us at N_t ~ 100 (the longest
+// kernel of a walker's preparation, and the preparation is the latency of small waveforms).
+// Here every knot row is a lane's: scipy's two boundary rows are eliminated into rows 1 and
+// n-2 (row 0: dx_1 s_0 + (x_2 - x_0) s_1 = r_0, and a_1 = dx_1, so s_0 drops out of row 1
+// exactly; the same at the other end), the remaining tridiagonal system in s_1 .. s_{n-2}
+// (diagonally dominant: b = 2 (a + c) inside) is normalised to b = 1 and reduced in
+// ceil(log2(n - 2)) PCR steps, each row combining its neighbours at distance h:
+//   row_k - A_k row_{k-h} - C_k row_{k+h}, renormalised,
+// after which every row reads s_k = R_k. The boundary slopes follow from rows 0 and n-1, and
+// the interval coefficients are scipy's PPoly construction, in parallel. The slopes agree with
+// the Thomas solve to rounding (both are stable on this matrix).
+// L: LDS scratch of 7 n doubles; at exit L[0, n) = x, L[n, 2n) = y, L[4n, 5n) = the knot
+// slopes s_i. Called by every lane of a one-wave (64-thread) workgroup, 4 <= n <= PCR_NMAX.
+// ----------------------------------------------------------------------------------------
+#ifndef EFD_PCR
+#define EFD_PCR 1
+#endif
+constexpr int PCR_RPL = 8;                 // rows per lane
+constexpr int PCR_NMAX = 64 * PCR_RPL;     // knots; longer trajectories take the Thomas kernel
+// Waveforms of PCR_MAX_K harmonics or more keep the Thomas kernel's amplitude role (one lane per
+// interpolant, k_prep_b): their preparation runs beside the previous batch's mode sum, where
+// its length is hidden and its CU time is not. One wave per interpolant is ~10x the Thomas
+// kernel's wave-time, and with every role on PCR config 2 (3,020 harmonics: 3,139 waves of
+// ~10 us, 2,508 of them amplitude splines) lost 1.2% of its rate (paired A/B, ratio 0.988) while
+// the latency-bound walker batches gained 6.6% (config 4) and 8.7% (config 5). The trajectory
+// and inverse splines (the phases) always take one path for a given N_t, so a harmonic subset
+// and the full set share them (the linearity test's 1e-12 bound).
+#ifndef PCR_MAX_K
+#define PCR_MAX_K 1024
+#endif
+template <class FX, class FY, class FOUT>
+__device__ void pcr_not_a_knot(int n, FX X, FY Y, FOUT OUT, double* L) {
+    const int lane = threadIdx.x;
+    double* xs = L;
+    double* ys = L + n;
+    double* dx = L + 2 * n;
+    double* sl = L + 3 * n;
+    double* A = L + 4 * n;
+    double* C = L + 5 * n;
+    double* R = L + 6 * n;
+    for (int i = lane; i < n; i += 64) {
+        xs[i] = X(i);
+        ys[i] = Y(i);
+    }
+    __syncthreads();
+    for (int i = lane; i < n - 1; i += 64) {
+        const double d = xs[i + 1] - xs[i];
+        dx[i] = d;
+        sl[i] = (ys[i + 1] - ys[i]) / d;
+    }
+    __syncthreads();
+    const int m = n - 2;   // unknowns s_1 .. s_{n-2}: interior row k holds s_{k+1}
+    // scipy's boundary rows: row 0 = (dx_1, x_2 - x_0 | r0), row n-1 = (x_{n-1} - x_{n-3}, dx_{n-3} | rl)
+    const double d0 = xs[2] - xs[0];
+    const double r0 = ((dx[0] + 2.0 * d0) * dx[1] * sl[0] + dx[0] * dx[0] * sl[1]) / d0;
+    const double dl = xs[n - 1] - xs[n - 3];
+    const double rl = (dx[n - 2] * dx[n - 2] * sl[n - 3] +
+                       (2.0 * dl + dx[n - 2]) * dx[n - 3] * sl[n - 2]) / dl;
+    for (int k = lane; k < m; k += 64) {
+        const int i = k + 1;
+        double a = dx[i], b = 2.0 * (dx[i - 1] + dx[i]), c = dx[i - 1];
+        double r = 3.0 * (dx[i] * sl[i - 1] + dx[i - 1] * sl[i]);
+        if (i == 1) {       // a_1 = dx_1 = row 0's diagonal: a_1 s_0 = r0 - d0 s_1
+            b -= d0;
+            a = 0.0;
+            r -= r0;
+        }
+        if (i == n - 2) {   // c_{n-2} = dx_{n-3} = row n-1's diagonal: c s_{n-1} = rl - dl s_{n-2}
+            b -= dl;
+            c = 0.0;
+            r -= rl;
+        }
+        const double inv = spl_rcp(b);
+        A[k] = a * inv;
+        C[k] = c * inv;
+        R[k] = r * inv;
+    }
+    __syncthreads();
+    for (int h = 1; h < m; h <<= 1) {
+        double na[PCR_RPL], nc[PCR_RPL], nr[PCR_RPL];
+#pragma unroll
+        for (int j = 0; j < PCR_RPL; ++j) {
+            if (64 * j >= m) break;    // wave-uniform
+            const int k = lane + 64 * j;
+            if (k < m) {
+                const double ak = A[k], ck = C[k], rk = R[k];
+                double al = 0.0, cl = 0.0, rlf = 0.0, ar = 0.0, cr = 0.0, rr = 0.0;
+                if (k >= h) { al = A[k - h]; cl = C[k - h]; rlf = R[k - h]; }
+                if (k + h < m) { ar = A[k + h]; cr = C[k + h]; rr = R[k + h]; }
+                const double inv = spl_rcp(fma(-ck, ar, fma(-ak, cl, 1.0)));
+                na[j] = -(ak * al) * inv;
+                nc[j] = -(ck * cr) * inv;
+                nr[j] = fma(-ck, rr, fma(-ak, rlf, rk)) * inv;
+            }
+        }
+        __syncthreads();   // every row's neighbours read before any row is overwritten
+#pragma unroll
+        for (int j = 0; j < PCR_RPL; ++j) {
+            if (64 * j >= m) break;
+            const int k = lane + 64 * j;
+            if (k < m) { A[k] = na[j]; C[k] = nc[j]; R[k] = nr[j]; }
+        }
+        __syncthreads();
+    }
+    double* S = A;         // knot slopes s_i (A is spent)
+    for (int k = lane; k < m; k += 64) S[k + 1] = R[k];
+    __syncthreads();
+    if (lane == 0) {
+        S[0] = (r0 - d0 * S[1]) / dx[1];
+        S[n - 1] = (rl - dl * S[n - 2]) / dx[n - 3];
+    }
+    __syncthreads();
+    // scipy's PPoly coefficients per interval (spline_not_a_knot's back-substitution formulas)
+    for (int i = lane; i < n - 1; i += 64) {
+        const double si = S[i], sn = S[i + 1];
+        const double rdx = spl_rcp(xs[i + 1] - xs[i]);
+        const double s_l = (ys[i + 1] - ys[i]) * rdx;
+        const double tt = (si + sn - 2.0 * s_l) * rdx;
+        OUT(i, 0, tt * rdx);
+        OUT(i, 1, (s_l - si) * rdx - tt);
+        OUT(i, 2, si);
+        OUT(i, 3, ys[i]);
+    }
+    __syncthreads();
 }
 
 // ----------------------------------------------------------------------------------------
@@ -967,11 +1098,157 @@ __global__ __launch_bounds__(64) void k_prep_b(const PrepBatch B) {
     PREP_WALKER(B);
     const int nb_amp = (4 * D.K + 63) / 64, nb_inv = (D.K + 63) / 64;
     if ((int)blockIdx.x >= 1 + nb_amp + nb_inv) return;
+    if (D.pcr & 1) {   // k_prep_pcr_b has the trajectory and inverse roles (and maybe this one)
+        const int b = blockIdx.x;
+        if (b == 0 || b >= 1 + nb_amp || (D.pcr & 2)) return;
+    }
     prep_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ws_at<double>(W, L.gamp),
               ws_at<int32_t>(W, L.gm), ws_at<int32_t>(W, L.gn), D.nt, D.K, nb_amp,
               ws_at<double>(W, L.coefT), ws_at<double>(W, L.kslope), ws_at<double>(W, L.tscratch),
               ws_at<double>(W, L.coefA), ws_at<int32_t>(W, L.runs), ws_at<Item>(W, L.items),
               ws_at<double>(W, L.invcp), ws_at<double>(W, L.invdp), ws_at<Header>(W, L.header));
+}
+
+// K1-K3 with one wave per interpolant (EFD_PCR): blocks [0, 4) the trajectory splines (Phi_phi,
+// Phi_r, f_phi, f_r; the f_phi and f_r blocks go on to f_phi', f_r' from their own knot
+// slopes), [4, 4 + K) the inverse splines of group h = b - 4 < G, [4 + K, 4 + 5K) the group
+// amplitude splines (interpolant q = b - 4 - K < 4G; only when Item::pcr bit 1 is set, else the
+// grid stops at 4 + K). Blocks past this waveform's G leave at once.
+// The same coefficients as k_prep's (scipy's construction, to rounding); for 4 <= N_t <=
+// PCR_NMAX (the host takes k_prep_b otherwise). Dynamic LDS: 9 N_t doubles.
+__device__ __forceinline__ void prep_pcr_body(
+    const double* __restrict__ t, const double* __restrict__ phi_phi,
+    const double* __restrict__ phi_r, const double* __restrict__ f_phi,
+    const double* __restrict__ f_r, const double* __restrict__ gamp,
+    const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int nt, int K,
+    double* __restrict__ coefT, double* __restrict__ kslope, double* __restrict__ coefA,
+    int32_t* __restrict__ runs, Item* __restrict__ items, double* __restrict__ invcp,
+    double* __restrict__ invdp, Header* __restrict__ hdr) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    auto X = [&](int i) { return t[i]; };
+    if (b < 4) {
+        // trajectory spline q; q = 2, 3 continue with the derivative splines 4, 5
+        const double* y = b == 0 ? phi_phi : b == 1 ? phi_r : b == 2 ? f_phi : f_r;
+        int q = b;
+        auto Y = [&](int i) { return y[i]; };
+        auto OUT = [&](int i, int c, double v) { coefT[((size_t)i * 4 + c) * 8 + q] = v; };
+        pcr_not_a_knot(nt, X, Y, OUT, lds);
+        if (b < 2) return;
+        // knot values of the derivative, as k_prep takes them: c2 of each interval, and scipy's
+        // derivative of the last piece at the last knot (the slopes stay in LDS at [4 nt, 5 nt))
+        double* v = lds + 7 * nt;
+        const double* xs = lds;
+        const double* ys = lds + nt;
+        const double* S = lds + 4 * nt;
+        for (int i = lane; i < nt; i += 64) {
+            double vi;
+            if (i < nt - 1) {
+                vi = S[i];
+            } else {
+                const double si = S[nt - 2], sn = S[nt - 1];
+                const double rdx = spl_rcp(xs[nt - 1] - xs[nt - 2]);
+                const double s_l = (ys[nt - 1] - ys[nt - 2]) * rdx;
+                const double tt = (si + sn - 2.0 * s_l) * rdx;
+                const double c[4] = {tt * rdx, (s_l - si) * rdx - tt, si, ys[nt - 2]};
+                vi = dcubic(c, xs[nt - 1] - xs[nt - 2]);
+            }
+            v[i] = vi;
+            kslope[(size_t)(b - 2) * nt + i] = vi;
+        }
+        __syncthreads();
+        q = b + 2;
+        auto YV = [&](int i) { return v[i]; };
+        pcr_not_a_knot(nt, X, YV, OUT, lds);
+        return;
+    }
+    const int G = hdr->groups;
+    if (b >= 4 + K) {
+        const int q = b - 4 - K;
+        if (q >= 4 * G) return;
+        const size_t ninterp = (size_t)4 * K;
+        auto Y = [&](int i) { return gamp[(size_t)i * ninterp + q]; };
+        auto OUT = [&](int i, int c, double v) { coefA[((size_t)i * 4 + c) * ninterp + q] = v; };
+        pcr_not_a_knot(nt, X, Y, OUT, lds);
+        return;
+    }
+    const int h = b - 4;   // (m, n) group
+    if (h >= G) return;
+    const int m = gm[h], n = gn[h];
+    const int ni = nt - 1;
+    Item* it = items + (size_t)h * ni;
+    int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
+    double* Fv = lds + 8 * nt;     // F at the knots (PCR uses [0, 7 npts))
+    int* sgv = reinterpret_cast<int*>(lds + 7 * nt);   // sign of F_{j+1} - F_j
+    for (int i = lane; i < nt; i += 64) Fv[i] = knotF(f_phi, f_r, m, n, i);
+    __shared__ int rrs[4 * MAXRUNS];
+    __shared__ int nrun_s;
+    __syncthreads();
+    for (int j = lane; j < ni; j += 64) {
+        const double F0 = Fv[j], F1 = Fv[j + 1];
+        sgv[j] = (F1 > F0) ? 1 : ((F1 < F0) ? -1 : 0);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        // maximal strictly monotonic runs, as inverse_splines scans them
+        for (int r = 0; r < MAXRUNS; ++r) {
+            rr[4 * r] = rr[4 * r + 1] = rr[4 * r + 2] = 0;
+            rrs[4 * r] = rrs[4 * r + 1] = rrs[4 * r + 2] = 0;
+        }
+        int nrun = 0, cur_sign = 0, ja = 0;
+        for (int j = 0; j <= ni; ++j) {
+            const int sg = j < ni ? sgv[j] : 0;
+            if (sg != cur_sign || j == ni) {
+                if (cur_sign != 0) {
+                    if (nrun < MAXRUNS) {
+                        rr[4 * nrun] = rrs[4 * nrun] = ja;
+                        rr[4 * nrun + 1] = rrs[4 * nrun + 1] = j;
+                        rr[4 * nrun + 2] = rrs[4 * nrun + 2] = cur_sign;
+                        ++nrun;
+                    } else {
+                        atomicOr(&hdr->runs_overflow, 1);
+                    }
+                }
+                cur_sign = sg;
+                ja = j;
+            }
+        }
+        nrun_s = nrun;
+    }
+    __syncthreads();
+    const int nrun = nrun_s;
+    for (int r = 0; r < nrun; ++r) {
+        const int a = rrs[4 * r], bb = rrs[4 * r + 1], sg = rrs[4 * r + 2];
+        const int npts = bb - a + 1;
+        auto KI = [&](int qq) { return sg > 0 ? a + qq : bb - qq; };
+        auto XF = [&](int qq) { return Fv[KI(qq)]; };
+        auto YT = [&](int qq) { return t[KI(qq)]; };
+        auto OUT = [&](int qq, int c, double v) {
+            const int jf = sg > 0 ? a + qq : bb - 1 - qq;
+            it[jf].ic[c] = v;
+            if (c == 3) it[jf].gx = XF(qq);
+        };
+        if (npts >= 4) {
+            pcr_not_a_knot(npts, XF, YT, OUT, lds);
+        } else {
+            if (lane == 0) {   // 2 or 3 knots: the closed forms (no scratch)
+                auto CP = [&](int qq) -> double& { return invcp[(size_t)(a + qq) * K + h]; };
+                auto DP = [&](int qq) -> double& { return invdp[(size_t)(a + qq) * K + h]; };
+                spline_not_a_knot(npts, XF, YT, CP, DP, OUT);
+            }
+            __syncthreads();
+        }
+    }
+}
+__global__ __launch_bounds__(64) void k_prep_pcr_b(const PrepBatch B) {
+    PREP_WALKER(B);
+    if (!(D.pcr & 1) || (int)blockIdx.x >= 4 + ((D.pcr & 2) ? 5 : 1) * D.K) return;
+    prep_pcr_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ws_at<double>(W, L.gamp),
+                  ws_at<int32_t>(W, L.gm), ws_at<int32_t>(W, L.gn), D.nt, D.K,
+                  ws_at<double>(W, L.coefT), ws_at<double>(W, L.kslope), ws_at<double>(W, L.coefA),
+                  ws_at<int32_t>(W, L.runs), ws_at<Item>(W, L.items), ws_at<double>(W, L.invcp),
+                  ws_at<double>(W, L.invdp), ws_at<Header>(W, L.header));
 }
 
 __global__ __launch_bounds__(64) void k_spline_shared(const double* __restrict__ x, int n,
@@ -3617,7 +3894,8 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         return fail(EFD_ERR_ARG, F + ": count out of range [1, EFD_BATCH_MAX]");
     PrepBatch B{};
     B.n = count;
-    int ntmax = 0, Kmax = 0, nimax = 0;
+    int ntmax = 0, Kmax = 0, nimax = 0, ntmax_pcr = 0, pcr_blocks = 0;
+    bool any_pcr = false, any_thomas = false;
     int64_t items_max = 0, ntiles = 0;
     bool any_lists = false, any_order = false;
     for (int i = 0; i < count; ++i) {
@@ -3644,6 +3922,14 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         d.lists = use_prebuilt(ai->K) ? (use_cost_order(L, ai->K) ? 3 : 1) : 0;
         any_lists |= d.lists != 0;
         any_order |= d.lists == 3;
+        const bool pcr = EFD_PCR && ai->nt >= 4 && ai->nt <= PCR_NMAX;
+        d.pcr = pcr ? (ai->K < PCR_MAX_K ? 3 : 1) : 0;
+        if (pcr) {
+            any_pcr = true;
+            ntmax_pcr = std::max(ntmax_pcr, ai->nt);
+            pcr_blocks = std::max(pcr_blocks, 4 + (d.pcr == 3 ? 5 : 1) * ai->K);
+        }
+        if (d.pcr != 3) any_thomas = true;
         ntmax = std::max(ntmax, ai->nt);
         Kmax = std::max(Kmax, ai->K);
         nimax = std::max(nimax, ai->nt - 1);
@@ -3678,10 +3964,17 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
     // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
     // grids sized for G = K, blocks past the device-side G return at once)
     if (!(skip & 2)) {
-        const int nb = 1 + (4 * Kmax + 63) / 64 + (Kmax + 63) / 64;
-        hipLaunchKernelGGL(k_prep_b, dim3(nb, 1, nz), dim3(64), sizeof(double) * 7 * ntmax, st,
-                           B);
-        HIP_TRY(hipGetLastError());
+        if (any_pcr) {   // one wave per interpolant, parallel cyclic reduction (prep_pcr_body)
+            hipLaunchKernelGGL(k_prep_pcr_b, dim3(pcr_blocks, 1, nz), dim3(64),
+                               sizeof(double) * 9 * ntmax_pcr, st, B);
+            HIP_TRY(hipGetLastError());
+        }
+        if (any_thomas) {
+            const int nb = 1 + (4 * Kmax + 63) / 64 + (Kmax + 63) / 64;
+            hipLaunchKernelGGL(k_prep_b, dim3(nb, 1, nz), dim3(64), sizeof(double) * 7 * ntmax,
+                               st, B);
+            HIP_TRY(hipGetLastError());
+        }
 #ifdef EFD_EXP_PREP_ROLE
         return EFD_OK;   // timing experiment: the later stages would read partial data
 #endif
