@@ -32,6 +32,9 @@ the committed profile, per SPA evaluation, times this run's evaluations) / launc
 scatter-formulation bytes (32 B per SPA contribution) are reported as scatter_equiv_gbs, a
 secondary figure: the kernel never issues that traffic.
 
+few_gen: the drivers' whole GenerateEMRIWaveform call on the same source, one at a time (host
+upstream + device pipeline; rank 0 at N = 1), next to the batched device rate.
+
 cpu_baseline: the host twin efd_modesum_cpu (the same algorithm in C++17 + OpenMP, kind "twin")
 on this host: all cores on full waveforms, and 1 thread on a subset of harmonics extrapolated by
 SPA evaluation count (single_thread). cpu_reference: the oracle's C restatement (per harmonic
@@ -165,6 +168,47 @@ def cpu_baseline(w, seconds=10.0):
                                         f"by evaluation count"},
             "implementation": "efd_modesum_cpu (csrc/emrifd_cpu.cpp): the HIP path's algorithm "
                               "on the host, C++17 + OpenMP, -O3 -march=x86-64-v4"}
+
+
+def few_gen_timing(w, reps=10, caustic="uniform"):
+    """The drivers' whole call (events around the full few_gen-equivalent
+    call; check_mode_by_mode.py:221-229 times `few_gen(*injection_in, **kw)`): the
+    GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", output_type="fd") call on config 2's
+    source, host upstream (the C++ stand-in trajectory, amplitudes and selection: NOT FEW
+    physics) + upload + preparation + mode sum, the two-sided spectrum on the device. 1 warm-up
+    + `reps` calls, each bracketed by HIP events on the current stream and a host clock around
+    the call and its synchronisation; medians."""
+    import torch
+    from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform
+    few = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux",
+                               sum_kwargs=dict(pad_output=True, output_type="fd", odd_len=True),
+                               use_gpu=True, return_list=False, caustic=caustic)
+    P = w["params"]
+    # M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0; the sky and
+    # spin angles put the source-frame viewing angles at the workload's (theta, phi) = (pi/3,
+    # -pi/2): -R.S = cos(pi/3), so the same ~3,000 harmonics survive eps = 1e-5
+    args = (P["M"], P["mu"], 0.0, P["p0"], P["e0"], 1.0, 1.0, np.pi / 3, 0.0, np.pi / 3, np.pi,
+            0.0, 0.0, 0.0)
+    kw = dict(T=P["T"], dt=P["dt"], eps=P["eps"])
+    S = few(*args, **kw)
+    torch.cuda.synchronize()
+    wall, dev = [], []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        a.record()
+        S = few(*args, **kw)
+        b.record()
+        torch.cuda.synchronize()
+        wall.append(time.perf_counter() - t0)
+        dev.append(a.elapsed_time(b) * 1e-3)
+    ms = float(np.median(wall)) * 1e3
+    return {"value": 1e3 / ms, "unit": "waveforms/s", "ms_per_call": ms,
+            "events_ms_per_call": float(np.median(dev)) * 1e3, "reps": reps,
+            "harmonics": int(len(few.waveform_generator.last_modes[0])), "bins": int(S.numel()),
+            "note": "GenerateEMRIWaveform(...)(14 params, T=2, dt=10, eps=1e-5): host stand-in "
+                    "upstream (C++, one call at a time) + device pipeline, serial; the batch "
+                    "value overlaps many waveforms and excludes the upstream"}
 
 
 def cpu_reference(w, seconds=5.0):
@@ -373,9 +417,12 @@ def main():
         # output-stationary kernel never makes those accesses, so it exceeds HBM "peak")
         scatter_gbs = B * b_alg / (kern_ms * 1e-3) / 1e9
         roof = fp64_roofline(B, n_eval, kern_ms, args.caustic)
-        cpu = None
-        cpu = cpu_ref = None
+        cpu = cpu_ref = api = None
         if world == 1 and not args.no_cpu_baseline:
+            try:
+                api = few_gen_timing(w, caustic=args.caustic)
+            except Exception as exc:  # not part of the metric: never kill the GPU measurement
+                api = {"value": None, "error": repr(exc)}
             try:
                 cpu = cpu_baseline(w, seconds=args.cpu_seconds)
             except Exception as exc:  # the baseline must not kill the GPU measurement
@@ -424,6 +471,7 @@ def main():
                 "sum_gap_ms": gap_ms}),
             "cpu_baseline": cpu,
             "cpu_reference": cpu_ref,
+            "few_gen": api,
         }
         print(json.dumps(line))
     if world > 1:
