@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = (
     "efd_host_trajectory",
     "efd_host_p_at_t",
     "efd_host_modes",
+    "efd_host_set_threads",
 )
 
 
@@ -224,6 +225,15 @@ def load(path=None):
         lib.efd_host_modes.restype = ctypes.c_int
         lib.efd_host_modes.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, dbl, vp,
                                        ctypes.POINTER(i32), vp, i64]
+        lib.efd_host_set_threads.restype = ctypes.c_int
+        lib.efd_host_set_threads.argtypes = [i32]
+        # the loading (main) thread's one-at-a-time upstream calls spread their knots over the
+        # host cores; the prefetch pool's threads keep one each (the setting is per thread)
+        import threading
+        if threading.current_thread() is threading.main_thread():
+            n = len(os.sched_getaffinity(0))
+            n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16)
+            lib.efd_host_set_threads(max(1, n))
     _ = dbl
     if path is None:
         _lib = lib

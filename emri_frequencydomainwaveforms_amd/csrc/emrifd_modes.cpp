@@ -19,6 +19,8 @@
 #include <cstring>
 #include <vector>
 
+#include <omp.h>
+
 #include "../../include/emrifd.h"
 
 namespace {
@@ -37,7 +39,16 @@ void magnitudes(double p, double e, int nm, const double* c1, const double* dn, 
         mag[k] = std::exp(LN10 * (x - 1.0 - decay)) + std::exp(LN10 * (x - 3.6 - 0.085 * decay));
     }
 }
+// threads for one efd_host_modes call, per calling thread (efd_host_set_threads): the API's
+// one-at-a-time calls split the knots over the host cores, while the prefetch pool's threads
+// (which never set it) run their walkers on one core each
+thread_local int t_threads = 1;
 }  // namespace
+
+extern "C" int efd_host_set_threads(int32_t n) {
+    t_threads = n < 1 ? 1 : n;
+    return EFD_OK;
+}
 
 extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, const int32_t* l,
                               const int32_t* m, const int32_t* n, const double* phase0,
@@ -61,17 +72,24 @@ extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, cons
     }
     const int np_ = nm + (int)partner_of.size();
     std::vector<unsigned char> kept(nm, 0);
-    std::vector<double> mag(nm), pw(np_);
-    std::vector<int32_t> idx(np_), cut(np_);
-    std::vector<int16_t> ex(np_);
     constexpr int NB = 2048;                      // binary exponents of non-negative doubles
-    std::vector<double> bsum(NB);
-    std::vector<int32_t> bcnt(NB);
     auto expo = [](double v) {
         uint64_t u;
         std::memcpy(&u, &v, 8);
         return (int)((u >> 52) & 2047u);
     };
+    // the knots' selections are independent and their union is order-free: any thread count
+    // gives the same kept set
+    const int nth = std::max(1, std::min(t_threads, nt / 4));
+#pragma omp parallel num_threads(nth) if (nth > 1)
+    {
+    std::vector<unsigned char> kept_l(nm, 0);
+    std::vector<double> mag(nm), pw(np_);
+    std::vector<int32_t> idx(np_), cut(np_);
+    std::vector<int16_t> ex(np_);
+    std::vector<double> bsum(NB);
+    std::vector<int32_t> bcnt(NB);
+#pragma omp for schedule(static)
     for (int i = 0; i < nt; ++i) {
         magnitudes(p[i], e[i], nm, c1.data(), dn.data(), dm.data(), hl.data(), jitter, mag.data());
         double total = 0.0;
@@ -116,8 +134,11 @@ extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, cons
         if (lo == 0 && np_ > 0) lo = 1;   // the largest is always kept
         for (int k = 0; k < lo; ++k) {
             const int q = idx[k];
-            kept[q < nm ? q : partner_of[q - nm]] = 1;
+            kept_l[q < nm ? q : partner_of[q - nm]] = 1;
         }
+    }
+#pragma omp critical
+    for (int k = 0; k < nm; ++k) kept[k] |= kept_l[k];
     }
     int K = 0;
     for (int k = 0; k < nm; ++k)
@@ -126,14 +147,17 @@ extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, cons
     if (!teuk) return EFD_OK;
     if ((int64_t)K * nt * 2 > teuk_cap) return EFD_ERR_WORKSPACE;
     // complex amplitudes of the kept modes, [nt][K] (FEW teuk_modes layout)
-    std::vector<double> kc1(K), kdn(K), kdm(K), khl(K), kjit(K), kph(K), kdr(K), kmg(K), kph2(K),
-        kc(K), ks(K);
+    std::vector<double> kc1(K), kdn(K), kdm(K), khl(K), kjit(K), kph(K), kdr(K);
     for (int j = 0; j < K; ++j) {
         const int k = keep[j];
         kc1[j] = c1[k]; kdn[j] = dn[k]; kdm[j] = dm[k]; khl[j] = hl[k]; kjit[j] = jitter[k];
         kph[j] = phase0[k];
         kdr[j] = 0.2 * (double)(l[k] - m[k] + 1);
     }
+#pragma omp parallel num_threads(nth) if (nth > 1)
+    {
+    std::vector<double> kmg(K), kph2(K), kc(K), ks(K);
+#pragma omp for schedule(static)
     for (int i = 0; i < nt; ++i) {
         magnitudes(p[i], e[i], K, kc1.data(), kdn.data(), kdm.data(), khl.data(), kjit.data(),
                    kmg.data());
@@ -150,6 +174,7 @@ extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, cons
             row[2 * j] = kmg[j] * kc[j];
             row[2 * j + 1] = kmg[j] * ks[j];
         }
+    }
     }
     return EFD_OK;
 }

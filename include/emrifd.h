@@ -339,6 +339,9 @@ int efd_host_modes(const double* p, const double* e, int32_t nt, const int32_t* 
                    const int32_t* m, const int32_t* n, const double* phase0, const double* jitter,
                    int32_t nmodes, const double* ylm_p, const double* ylm_m, double eps,
                    int32_t* keep, int32_t* nkeep, double* teuk, int64_t teuk_cap);
+/* Threads the calling thread's later efd_host_modes calls spread their knots over (default 1;
+ * the setting is per calling thread). Any count gives bitwise the same results. */
+int efd_host_set_threads(int32_t n);
 
 /*
  * Host staging of a walker batch for efd_modesum_prepare_batch (not part of the reference's
