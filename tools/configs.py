@@ -165,12 +165,32 @@ def config3(reps, slots=4):
     prep.wait()
     dev = (time.perf_counter() - t0) / reps
     K = [len(w["m"]) for w in ws]
+    # the drivers' scan (check_mode_by_mode.py:183-229): per point the p0 root solve
+    # (get_p_at_t) and the whole few_gen call, one at a time, native upstream
+    from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
+    from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform
+    few = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux", sum_kwargs=SUM_KW,
+                               use_gpu=True, return_list=True)
+    traj = EMRIInspiral()
+
+    def api_sweep():
+        for M in Ms:
+            for e0 in e0s:
+                p0 = float(get_p_at_t(traj, 0.99 * T, [M, 1e-5 * M, 0.0, e0, 1.0]))
+                few(*_params(M, 1e-5 * M, p0, e0), T=T, dt=dt, eps=eps)
+    api_sweep()
+    _sync()
+    t0 = time.perf_counter()
+    api_sweep()
+    _sync()
+    api = time.perf_counter() - t0
     return {"config": "config3: 10x10 grid M=logspace(5,7) e0=linspace(0.1,0.6) mu=1e-5 M "
                       "Tobs=1yr dt=10s eps=1e-2", "waveforms": len(ws), "N_f": nf,
             "harmonics_min_max": [min(K), max(K)],
             "device_waveforms_per_s": len(ws) / dev, "device_ms_per_grid": dev * 1e3,
             "pipeline_waveforms_per_s": len(ws) / dev_pipe,
-            "api_waveforms_per_s": len(ws) / (host_s + dev),
+            "api_waveforms_per_s": len(ws) / api,
+            "api_note": "per point: native get_p_at_t + the whole few_gen call, serial",
             "host_upstream_s_per_grid": host_s, "pipeline_slots": slots,
             "device_note": "100 waveforms in groups of 16: one packed upload and one "
                            "efd_modesum_prepare_batch per group on a group stream, one "
