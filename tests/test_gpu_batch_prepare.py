@@ -187,3 +187,29 @@ def test_status_batch_names_failing_waveform(sources):
     rc = lib.efd_modesum_status_batch((ctypes.c_void_p * 3)(*wss), 3, flags,
                                       B.stream(0).cuda_stream)
     assert rc == _lib.EFD_OK and list(flags) == [0, 0, 0]
+
+
+def test_fused_loglike_marks_failing_walker_nan(sources):
+    """efd_modesum_sum_loglike writes NaN for a walker whose workspace holds a device-side error
+    flag (here |m| > 255 on walker 2) and leaves the flag set, so the batched likelihood needs a
+    status read only when a NaN comes back (likelihood.py: one synchronisation per batch)."""
+    freq = torch.as_tensor(sources[0]["freq"], device="cuda")
+    nf = int(freq.numel())
+    B = BatchPreparer(group=3, depth=1)
+    for i in range(3):
+        h = _host(sources[i])
+        if i == 2:
+            h["m"] = h["m"].copy()
+            h["m"][0] = 300
+        B.submit(h, freq, True, sources[i]["prefactor"], prepare_only=True)
+    gi, jobs = B.flush()
+    cur = torch.cuda.current_stream()
+    cur.wait_stream(B.stream(gi))
+    d = torch.zeros((2, nf), dtype=torch.complex128, device="cuda")
+    w = torch.ones((2, nf), dtype=torch.float64, device="cuda")
+    out = torch.full((3,), 1.0, dtype=torch.float64, device="cuda")
+    B.sum_loglike(gi, d, w, out, cur.cuda_stream)
+    ll = out.cpu().numpy()
+    assert np.isnan(ll[2]) and np.all(np.isfinite(ll[:2])) and np.all(ll[:2] < 0.0)
+    with pytest.raises(_lib.EFDError, match="waveform 2 of the batch"):
+        B.wait()

@@ -109,3 +109,30 @@ def test_prepare_native_vs_numpy_and_prefetch():
         for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
             np.testing.assert_array_equal(got[k], ref[k])
     assert not wn._prefetched
+
+
+def test_host_modes_threads_bitwise():
+    """efd_host_set_threads: a one-at-a-time efd_host_modes call split over threads (the API's
+    path) keeps bitwise the kept set and complex amplitudes of the one-thread call (the prefetch
+    pool's path)."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.waveform import FastSchwarzschildEccentricFlux
+    lib = _lib.load()
+    g = FastSchwarzschildEccentricFlux(sum_kwargs=dict(output_type="fd"))
+    tr = g.inspiral_generator
+    if tr.lib is None:
+        pytest.skip("native upstream not built")
+    t, p, e = tr.with_frequencies(1e6, 10.0, 0.0, 10.0, 0.35, 1.0, T=1.0)[:3]
+    y = g._ylms(np.pi / 3, -np.pi / 2)
+    amp = g.amplitude_generator
+    res = []
+    try:
+        for n in (1, 3, 8):
+            lib.efd_host_set_threads(n)
+            keep, teuk = amp.select(p, e, y, 1e-4, lib=lib)
+            res.append((keep.copy(), teuk.copy()))
+    finally:
+        lib.efd_host_set_threads(1)
+    for keep, teuk in res[1:]:
+        np.testing.assert_array_equal(keep, res[0][0])
+        np.testing.assert_array_equal(teuk, res[0][1])
