@@ -79,7 +79,9 @@ def test_short_trajectories(base, nt):
     _check(d)
 
 
-@pytest.mark.parametrize("nt", [257, 1024])
+# 512 / 513: the last knot count the preparation's parallel-cyclic-reduction splines take and
+# the first that goes back to the Thomas kernel (emrifd.hip PCR_NMAX)
+@pytest.mark.parametrize("nt", [257, 512, 513, 1024])
 def test_long_trajectories(base, nt):
     t = base["t"]
     d = _resample(base, np.linspace(t[0], t[-1], nt))
