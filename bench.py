@@ -279,6 +279,9 @@ def main():
     ap.add_argument("--fused-group", type=int, default=0,
                     help="--likelihood: walkers per fused group (Likelihood.FUSED_GROUP; 0 = its "
                          "default)")
+    ap.add_argument("--no-tile-constants", action="store_true",
+                    help="--likelihood: empty tiles recompute their logL partial (the A/B "
+                         "baseline of efd_loglike_tile_constants)")
     ap.add_argument("--api-steps", type=int, default=2,
                     help="--likelihood: half-steps timed with the host upstream in the loop")
     args = ap.parse_args()
@@ -511,6 +514,8 @@ def bench_likelihood(args):
     s = pe.setup(**cfg)
     if args.fused_group:
         s.like.FUSED_GROUP = args.fused_group
+    if args.no_tile_constants:
+        s.like.fused_tile_constants = False
     B = s.half_step
     batches = s.half_steps()
     if world > 1:
@@ -559,7 +564,8 @@ def bench_likelihood(args):
                        "N_f": s.info.get("N_f"), "N_f_downsampled": s.info.get("N_f_downsampled"),
                        "p0": s.info["p0"], "parallelism": f"walker shards x{world} (RCCL "
                        "broadcast of params + all-gather of logL)" if world > 1 else "1 GPU",
-                       "fused_likelihood": bool(s.like.fused_likelihood)},
+                       "fused_likelihood": bool(s.like.fused_likelihood),
+                       "tile_constants": bool(s.like.fused_tile_constants)},
             "api_loglikes_per_s": args.api_steps * B / api,
             "host_upstream_ms_per_walker": memo.host_s / max(1, len(memo.memo)) * 1e3,
             "ll_truth_walker_sample": float(np.asarray(ll)[0]),

@@ -34,6 +34,9 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_sum",
     "efd_modesum_sum_batch",
     "efd_modesum_sum_loglike",
+    "efd_loglike_tile_count",
+    "efd_loglike_tile_constants",
+    "efd_modesum_sum_loglike_ex",
     "efd_modesum_status",
     "efd_modesum_contributions",
     "efd_modesum_stats",
@@ -170,6 +173,15 @@ def load(path=None):
         lib.efd_modesum_sum_loglike.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
                                                 ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp,
                                                 vp, vp, vp]
+    if hasattr(lib, "efd_modesum_sum_loglike_ex"):
+        lib.efd_loglike_tile_count.restype = i64
+        lib.efd_loglike_tile_count.argtypes = [i64]
+        lib.efd_loglike_tile_constants.restype = ctypes.c_int
+        lib.efd_loglike_tile_constants.argtypes = [vp, vp, i64, i64, vp, vp]
+        lib.efd_modesum_sum_loglike_ex.restype = ctypes.c_int
+        lib.efd_modesum_sum_loglike_ex.argtypes = [ctypes.POINTER(ctypes.POINTER(ModesumArgs)),
+                                                   ctypes.POINTER(vp), ctypes.POINTER(sz), i32,
+                                                   vp, vp, vp, vp, vp]
     lib.efd_modesum_status.restype = ctypes.c_int
     lib.efd_modesum_status.argtypes = [vp, vp]
     if hasattr(lib, "efd_stage_batch"):

@@ -2580,6 +2580,9 @@ __device__ __forceinline__ void modesum_tile(
     // the tile writes sum_c sum_j |d[c][j] - h_c[j] w[c][j]|^2 over its bins j >= k0 to
     // llpart[tile]. lld = NULL: not computed.
     const double* __restrict__ lld, const double* __restrict__ llw, double* __restrict__ llpart,
+    // fused likelihood: the partial of a tile with no record (h = 0 on its bins), the same for
+    // every walker (efd_loglike_tile_constants); NULL: such tiles compute it
+    const double* __restrict__ llconst,
     int64_t b) {   // b: this workgroup's place in the waveform's dispatch order
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
@@ -2640,6 +2643,17 @@ __device__ __forceinline__ void modesum_tile(
     // table and the build below is skipped. Same keys in the same order as the build below, so
     // the sum is bitwise the in-kernel build's.
     const int pre = tcnt != nullptr ? tcnt[tile] : -1;
+    // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces). A
+    // prebuilt list brings it in with the keys; otherwise it comes in with the first stage of
+    // records, so a tile without records never loads it (tab = table issued: block-uniform)
+    static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
+#define EFD_TABLE_DMA()                                                                       \
+    do {                                                                                      \
+        _Pragma("unroll") for (int rd_ = 0; rd_ < SCTAB / TILE; ++rd_)                        \
+            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd_ * TILE + tid,                \
+                   reinterpret_cast<uint4*>(sctab) + rd_ * TILE + wave * 64);                 \
+    } while (0)
+    bool tab = false;
     if (pre > 0) {
         static_assert(KEYCAP % (4 * TILE) == 0, "key copy: whole rounds of 16-B pieces");
 #pragma unroll
@@ -2649,14 +2663,8 @@ __device__ __forceinline__ void modesum_tile(
                 glds16(reinterpret_cast<const uint4*>(tkeys + (size_t)tile * KEYCAP) + pc,
                        reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
         }
-    }
-    {
-        // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces)
-        static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
-#pragma unroll
-        for (int rd = 0; rd < SCTAB / TILE; ++rd)
-            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
-                   reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
+        EFD_TABLE_DMA();
+        tab = true;
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
         __syncthreads();
     }
@@ -2846,6 +2854,10 @@ __device__ __forceinline__ void modesum_tile(
         // ---- evaluate the nkeys records in chunks of NC through the double-buffered stage
         const int cnt = nkeys;
         const int nchunk = (cnt + NC - 1) / NC;
+        if (!tab) {   // the first records of a built list: the table comes in with their stage
+            EFD_TABLE_DMA();
+            tab = true;
+        }
         EFD_GLDS(0, 0);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's LDS-DMA pieces landed
         __syncthreads();
@@ -3021,6 +3033,13 @@ __device__ __forceinline__ void modesum_tile(
         if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
+#undef EFD_TABLE_DMA
+    if (PAIRED && llconst != nullptr && !tab && out == nullptr && hp == nullptr) {
+        // no record reached this tile: h = 0 on its bins, whose likelihood partial is the
+        // walker-independent one k_ll_tile_const computed with this epilogue's arithmetic
+        if (tid == 0) llpart[tile] = llconst[tile];
+        return;
+    }
     if (s_cur)
 #pragma unroll
         for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
@@ -3131,7 +3150,7 @@ __attribute__((amdgpu_num_vgpr(EFD_MODESUM_VGPRS)))
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 #endif
 void k_modesum(EFD_MODESUM_PARAMS) {
-    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, nullptr, nullptr, nullptr,
+    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, nullptr, nullptr, nullptr, nullptr,
                                        (int64_t)blockIdx.x);
 }
 
@@ -3181,7 +3200,7 @@ template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t ntiles,
                      int accumulate_out, const double* __restrict__ lld,
-                     const double* __restrict__ llw) {
+                     const double* __restrict__ llw, const double* __restrict__ llconst) {
     const int n = batch.n;
     int w;
     int64_t pos;
@@ -3202,7 +3221,73 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
     modesum_tile<PAIRED, CAUSTIC, BPL>(
         d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt, d.K,
         d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm, d.segbase, d.stb0,
-        d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld, llw, d.llpart, pos);
+        d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld, llw, d.llpart, llconst, pos);
+}
+
+// The fused likelihood's partial of a tile whose waveform has no record on it (every bin's
+// h = 0): modesum_tile's epilogue with zero accumulators, the same operations in the same order,
+// so a tile that takes it (llconst) gives bitwise what computing it would. Depends on the grid
+// (nf, the paired tile layout), k0, d and w only: once per likelihood.
+template <int BPL>
+__global__ __launch_bounds__(TILE) void k_ll_tile_const(const double* __restrict__ lld,
+                                                        const double* __restrict__ llw,
+                                                        int64_t nf, int64_t nlanes, int64_t k0,
+                                                        double* __restrict__ llconst) {
+    const int64_t tile = blockIdx.x;
+    // modesum_tile's FP modes, so the epilogue's arithmetic rounds the same
+#if EFD_FTZ_SELECT
+    __builtin_amdgcn_s_setreg(1 | (6 << 6) | (1 << 11), 0);
+#endif
+#if EFD_OMOD
+    __builtin_amdgcn_s_setreg(1 | (9 << 6), 0);
+#endif
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
+    double llacc = 0.0;
+#pragma unroll
+    for (int i = 0; i < BPL; ++i) {
+        const int64_t k = w_lo + 64 * i + lane;
+        if (k >= nlanes) continue;
+        const int64_t km = nf - 1 - k;
+        double2 sk = make_double2(0.0, 0.0);
+        double2 sm = make_double2(0.0, 0.0);
+        if (km == k) {
+            sk.x += sm.x;
+            sk.y += sm.y;
+            sm = sk;
+        }
+        auto put = [&](int64_t j, double2 a, double2 b) {
+            if (j < k0) return;
+            double2 vp = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+            double2 vc = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+            {
+#pragma clang fp contract(off)
+                const int64_t q = j - k0, nb = nf - k0;
+                const double2 d0 = reinterpret_cast<const double2*>(lld)[q];
+                const double2 d1 = reinterpret_cast<const double2*>(lld)[nb + q];
+                const double w0 = llw[q], w1 = llw[nb + q];
+                const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
+                const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
+                llacc = fma(r0, r0, fma(i0, i0, llacc));
+                llacc = fma(r1, r1, fma(i1, i1, llacc));
+            }
+        };
+        put(km, sm, sk);
+        if (km != k) put(k, sk, sm);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) llacc += __shfl_xor(llacc, o, 64);
+    __shared__ double llw4[NWAVE];
+    if (lane == 0) llw4[wave] = llacc;
+    __syncthreads();
+    if (tid == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) t += llw4[w];
+        llconst[tile] = t;
+    }
 }
 
 // Fused likelihood, second stage: waveform i's out[i] = -1/2 * 4 * (sum of its tiles' partials),
@@ -4107,7 +4192,7 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
 // write their likelihood partials, k_ll_final turns each waveform's into out[i])
 int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const* workspace,
                    const size_t* workspace_bytes, int32_t count, const double* d, const double* w,
-                   double* llout, void* stream) {
+                   double* llout, void* stream, const double* llconst = nullptr) {
     const std::string F(fn);
     if (!a || !workspace || !workspace_bytes)
         return fail(EFD_ERR_ARG, F + ": NULL argument");
@@ -4174,7 +4259,7 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
     if (a[0]->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a[0]->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
     hipLaunchKernelGGL((k_modesum_batch<P, C, BPL>), grid, block, 0, st, batch, a[0]->nf,       \
-                       L0.nlanes, L0.ntiles, acc, d, w)
+                       L0.nlanes, L0.ntiles, acc, d, w, d ? llconst : nullptr)
     if (a[0]->grid_symmetric) {
         if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
         else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
@@ -4212,6 +4297,35 @@ int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* works
     if (!d || !w || !out) return fail(EFD_ERR_ARG, "efd_modesum_sum_loglike: NULL d, w or out");
     return sum_batch_impl("efd_modesum_sum_loglike", a, workspace, workspace_bytes, count, d, w,
                           out, stream);
+}
+
+int64_t efd_loglike_tile_count(int64_t nf) {
+    if (nf < 1) return 0;
+    return make_layout(2, 1, nf, 1).ntiles;
+}
+
+int efd_loglike_tile_constants(const double* d, const double* w, int64_t nf, int64_t k0,
+                               double* tile_const, void* stream) {
+    if (!d || !w || !tile_const)
+        return fail(EFD_ERR_ARG, "efd_loglike_tile_constants: NULL d, w or tile_const");
+    if (nf < 1 || k0 < 0 || k0 >= nf)
+        return fail(EFD_ERR_ARG, "efd_loglike_tile_constants: need nf >= 1 and 0 <= k0 < nf");
+    const Layout L = make_layout(2, 1, nf, 1);
+    if (L.ntiles > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, "efd_loglike_tile_constants: grid too large");
+    hipLaunchKernelGGL(k_ll_tile_const<BPL>, dim3((unsigned)L.ntiles), dim3(TILE), 0,
+                       (hipStream_t)stream, d, w, nf, L.nlanes, k0, tile_const);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
+int efd_modesum_sum_loglike_ex(const efd_modesum_args* const* a, void* const* workspace,
+                               const size_t* workspace_bytes, int32_t count, const double* d,
+                               const double* w, const double* tile_const, double* out,
+                               void* stream) {
+    if (!d || !w || !out)
+        return fail(EFD_ERR_ARG, "efd_modesum_sum_loglike_ex: NULL d, w or out");
+    return sum_batch_impl("efd_modesum_sum_loglike_ex", a, workspace, workspace_bytes, count, d,
+                          w, out, stream, tile_const);
 }
 
 int efd_modesum_status(const void* workspace, void* stream) {

@@ -63,6 +63,7 @@ class Likelihood:
         # no template is written; False keeps one template buffer + efd_loglike per walker
         self.fused_likelihood = True
         self._fused = None
+        self._tile_const = None
         self._specific_likelihood_setup()
 
     def _specific_likelihood_setup(self):
@@ -164,6 +165,7 @@ class Likelihood:
             w[:, 0] = 0.0
         self._d, self._w = d, w
         self._w_templ = w
+        self._tile_const = None   # (their tile constants are made again on the next call)
         tm = self.template_model
         mask = getattr(tm, "non_zero_mask", None)
         if mask is not None and getattr(tm, "can_fill", False):
@@ -272,8 +274,9 @@ class Likelihood:
                                   **kwargs)
                 gi, jobs = B.flush()
                 s_sum.wait_stream(B.stream(gi))
+                tc = self._tile_constants(jobs[0][1], s_sum)
                 B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)],
-                              s_sum.cuda_stream)
+                              s_sum.cuda_stream, tile_const=tc)
                 ev = torch.cuda.Event()
                 ev.record(s_sum)
                 B.release(gi, ev)
@@ -292,6 +295,24 @@ class Likelihood:
             B.wait()   # device-side errors of the groups' workspaces (sticky across reuse)
         cur.wait_stream(s_sum)
         return host
+
+    # tiles no harmonic reaches take a precomputed partial instead of re-reading d and w
+    # (efd_loglike_tile_constants; bitwise the same logL)
+    fused_tile_constants = True
+
+    def _tile_constants(self, job, stream):
+        """The fused sum's per-tile constants for (d, w_templ) on this grid, made once on
+        `stream` (ordered after the data's creation: the caller's stream waits on current)."""
+        if not self.fused_tile_constants:
+            return None
+        from .summation import loglike_tile_constants
+        nf, k0 = int(job["freq"].numel()), int(job.get("k0", 0))
+        key = (nf, k0, id(self._d), id(self._w_templ))
+        tc = self._tile_const
+        if tc is None or tc[0] != key:
+            tc = self._tile_const = (key, loglike_tile_constants(
+                self._d, self._w_templ, nf, k0, stream.cuda_stream))
+        return tc[1]
 
     def _fused_grid_ok(self, tm, kwargs):
         """Whether the template's grid for these kwargs is mirror-symmetric (the fused sum's

@@ -339,7 +339,34 @@ def _check_ll_io(torch, d, w, out, nb, n):
                          f"out float64 [>= {n}], contiguous")
 
 
-def sum_batch_loglike(jobs, d, w, out, stream=None):
+def loglike_tile_constants(d, w, nf, k0, stream=None, lib=None):
+    """efd_loglike_tile_constants: the fused likelihood's partial of every tile on which a
+    template is zero (float64 [efd_loglike_tile_count(nf)] on d's device). They depend on d, w
+    and the grid only; sum_batch_loglike / BatchPreparer.sum_loglike take them as tile_const and
+    then skip the d, w reads of the tiles no harmonic reaches, bitwise the same logL."""
+    torch = _torch()
+    lib = lib or _lib.load()
+    nb = int(nf) - int(k0)
+    _check_ll_io(torch, d, w, torch.empty(1, dtype=torch.float64), nb, 1)
+    nt = int(lib.efd_loglike_tile_count(int(nf)))
+    tc = torch.empty(nt, dtype=torch.float64, device=d.device)
+    st = stream if stream is not None else torch.cuda.current_stream(d.device).cuda_stream
+    _lib.check(lib.efd_loglike_tile_constants(torch.view_as_real(d).data_ptr(), w.data_ptr(),
+                                              int(nf), int(k0), tc.data_ptr(), st),
+               "efd_loglike_tile_constants", lib)
+    return tc
+
+
+def _tile_const_ptr(tile_const, nf, lib):
+    if tile_const is None:
+        return None
+    if (tile_const.dtype != _torch().float64 or not tile_const.is_contiguous()
+            or tile_const.numel() != int(lib.efd_loglike_tile_count(int(nf)))):
+        raise ValueError("tile_const: loglike_tile_constants' output for this grid")
+    return tile_const.data_ptr()
+
+
+def sum_batch_loglike(jobs, d, w, out, stream=None, tile_const=None):
     """Mode sums of several prepared waveforms with the likelihood fused into the sum
     (efd_modesum_sum_loglike): out[i] = -1/2 * 4 * sum |d - h_i w|^2 over both channels, h_i
     the waveform's [h+, hx] over the f >= 0 bins, never written to HBM.
@@ -347,7 +374,7 @@ def sum_batch_loglike(jobs, d, w, out, stream=None):
     jobs: as sum_batch, every one on a symmetric grid with the same k0 (the likelihood's
     f >= 0 start) and accumulate off. d: complex128 [2][nf - k0], w: float64 [2][nf - k0]
     (contiguous, on the device), out: float64 [len(jobs)] on the device (written in stream
-    order, no host synchronisation).
+    order, no host synchronisation). tile_const: loglike_tile_constants(d, w, nf, k0), or None.
     """
     import ctypes
     torch = _torch()
@@ -373,9 +400,10 @@ def sum_batch_loglike(jobs, d, w, out, stream=None):
     pb = (ctypes.c_size_t * n)(*[ws.numel() for ws in wss])
     lib = jobs[0][0].lib
     st = stream if stream is not None else torch.cuda.current_stream(freq.device).cuda_stream
-    _lib.check(lib.efd_modesum_sum_loglike(pa, pw, pb, n, torch.view_as_real(d).data_ptr(),
-                                           w.data_ptr(), out.data_ptr(), st),
-               "efd_modesum_sum_loglike", lib)
+    tc = _tile_const_ptr(tile_const, freq.numel(), lib)
+    _lib.check(lib.efd_modesum_sum_loglike_ex(pa, pw, pb, n, torch.view_as_real(d).data_ptr(),
+                                              w.data_ptr(), tc, out.data_ptr(), st),
+               "efd_modesum_sum_loglike_ex", lib)
     return wss
 
 
@@ -709,9 +737,10 @@ class BatchPreparer:
         self.last_jobs = jobs
         return gi, jobs
 
-    def sum_loglike(self, gi, d, w, out, stream):
-        """efd_modesum_sum_loglike over group gi's last flush (its argument and workspace
-        arrays as they are, no per-walker rebuilding); d, w, out as sum_batch_loglike."""
+    def sum_loglike(self, gi, d, w, out, stream, tile_const=None):
+        """efd_modesum_sum_loglike(_ex) over group gi's last flush (its argument and workspace
+        arrays as they are, no per-walker rebuilding); d, w, out, tile_const as
+        sum_batch_loglike."""
         import ctypes
         torch = _torch()
         G = self.groups[gi]
@@ -719,10 +748,16 @@ class BatchPreparer:
         A = G["args"]
         nb = int(A[0].nf) - int(A[0].k0)
         _check_ll_io(torch, d, w, out, nb, n)
-        _lib.check(self.lib.efd_modesum_sum_loglike(
-            G["pa"], ctypes.cast(G["pw"], ctypes.POINTER(ctypes.c_void_p)), G["pb"], n,
-            torch.view_as_real(d).data_ptr(), w.data_ptr(), out.data_ptr(), stream),
-            "efd_modesum_sum_loglike", self.lib)
+        if tile_const is None:
+            _lib.check(self.lib.efd_modesum_sum_loglike(
+                G["pa"], ctypes.cast(G["pw"], ctypes.POINTER(ctypes.c_void_p)), G["pb"], n,
+                torch.view_as_real(d).data_ptr(), w.data_ptr(), out.data_ptr(), stream),
+                "efd_modesum_sum_loglike", self.lib)
+        else:   # (checked by the caller that made them for this grid: no per-call recount)
+            _lib.check(self.lib.efd_modesum_sum_loglike_ex(
+                G["pa"], ctypes.cast(G["pw"], ctypes.POINTER(ctypes.c_void_p)), G["pb"], n,
+                torch.view_as_real(d).data_ptr(), w.data_ptr(), tile_const.data_ptr(),
+                out.data_ptr(), stream), "efd_modesum_sum_loglike_ex", self.lib)
 
     def release(self, gi, event):
         """The group's workspaces and inputs are free again once `event` (recorded after the sum

@@ -173,6 +173,27 @@ int efd_modesum_sum_loglike(const efd_modesum_args* const* a, void* const* works
                             const size_t* workspace_bytes, int32_t count, const double* d,
                             const double* w, double* out, void* stream);
 
+/*
+ * The fused likelihood's per-tile constants: for each tile of the symmetric grid's paired layout
+ * (efd_loglike_tile_count(nf) tiles), that tile's partial of efd_modesum_sum_loglike's sum when
+ * the template is zero on all of its bins. They depend on (d, w, nf, k0) only, so a likelihood
+ * computes them once; efd_modesum_sum_loglike_ex then gives a tile no harmonic reaches this value
+ * instead of re-reading d and w there (at a high f_max most tiles of a sparse spectrum are empty).
+ * The result is bitwise efd_modesum_sum_loglike's: the constants are that epilogue's arithmetic on
+ * zero sums. tile_const: efd_loglike_tile_count(nf) device doubles. Extensions for batched
+ * likelihood callers (likelihood.py:246-274).
+ */
+int64_t efd_loglike_tile_count(int64_t nf);
+int efd_loglike_tile_constants(const double* d, const double* w, int64_t nf, int64_t k0,
+                               double* tile_const, void* stream);
+
+/* efd_modesum_sum_loglike with the constants of efd_loglike_tile_constants for the same d, w,
+ * nf and k0 (tile_const NULL: efd_modesum_sum_loglike). */
+int efd_modesum_sum_loglike_ex(const efd_modesum_args* const* a, void* const* workspace,
+                               const size_t* workspace_bytes, int32_t count, const double* d,
+                               const double* w, const double* tile_const, double* out,
+                               void* stream);
+
 /* Synchronises `stream` and reports errors detected on the device by the calls on this
  * workspace since the previous efd_modesum_status (the flags are sticky across preparations, so
  * a workspace reused by several waveforms before its status is read loses none): a harmonic

@@ -213,3 +213,47 @@ def test_fused_loglike_marks_failing_walker_nan(sources):
     assert np.isnan(ll[2]) and np.all(np.isfinite(ll[:2])) and np.all(ll[:2] < 0.0)
     with pytest.raises(_lib.EFDError, match="waveform 2 of the batch"):
         B.wait()
+
+
+@pytest.mark.parametrize("dt", [20.0, 2.0])
+def test_fused_loglike_tile_constants_bitwise(sources, dt):
+    """efd_modesum_sum_loglike_ex with efd_loglike_tile_constants gives bitwise the logL of
+    efd_modesum_sum_loglike: the tiles no harmonic reaches take the precomputed partial, made
+    with the epilogue's own arithmetic on zero sums. dt = 2 s puts Nyquist ten times above the
+    sources' highest harmonic, so most tiles take it."""
+    from emri_frequencydomainwaveforms_amd.summation import fd_grid, loglike_tile_constants
+    freq_h = fd_grid(0.02, dt)
+    freq = torch.as_tensor(freq_h, device="cuda")
+    nf = int(freq.numel())
+    k0 = int(np.searchsorted(freq_h, 0.0))
+    nb = nf - k0
+    rng = np.random.default_rng(11)
+    d = torch.as_tensor(rng.standard_normal((2, nb)) + 1j * rng.standard_normal((2, nb)),
+                        device="cuda") * 1e-22
+    w = torch.as_tensor(rng.uniform(0.5, 2.0, (2, nb)) * 1e40, device="cuda")
+    w[:, 0] = 0.0   # a zeroed bin, as Likelihood's start_ind
+    tc = loglike_tile_constants(d, w, nf, k0)
+    lib = _lib.load()
+    assert tc.numel() == lib.efd_loglike_tile_count(nf)
+    B = BatchPreparer(group=len(sources), depth=1)
+    for src in sources:
+        B.submit(_host(src), freq, True, src["prefactor"], k0=k0, prepare_only=True)
+    gi, jobs = B.flush()
+    cur = torch.cuda.current_stream()
+    cur.wait_stream(B.stream(gi))
+    ref = torch.empty(len(sources), dtype=torch.float64, device="cuda")
+    got = torch.empty_like(ref)
+    got2 = torch.empty_like(ref)
+    B.sum_loglike(gi, d, w, ref, cur.cuda_stream)
+    B.sum_loglike(gi, d, w, got, cur.cuda_stream, tile_const=tc)
+    sum_batch_loglike(jobs, d, w, got2, tile_const=tc)
+    torch.cuda.synchronize()
+    B.wait()
+    assert torch.all(torch.isfinite(ref)) and torch.all(ref < 0)
+    assert torch.equal(got, ref) and torch.equal(got2, ref)
+    # the constants alone sum to a zero template's sum |d - 0 w|^2 over every bin (to rounding:
+    # another summation order)
+    h0 = float((torch.abs(d) ** 2).sum())
+    assert abs(float(tc.sum()) - h0) <= 1e-12 * h0
+    with pytest.raises(ValueError):
+        sum_batch_loglike(jobs, d, w, got2, tile_const=tc[:-1])
