@@ -171,7 +171,8 @@ struct Header {
     int32_t bad_mn;             // set by k_group when |m| > 255 or |n| > 1023
     int32_t bad_tile;           // set by k_modesum when a dispatch-order entry is out of range
     int64_t magic;              // HDR_MAGIC once k_group has initialised the header
-    int64_t pad[3];             // 64 B
+    int32_t lane_lo, lane_hi;   // union [lo, hi) of the segments' lane ranges (k_segment_compact)
+    int64_t pad[2];             // 64 B
 };
 static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
@@ -565,11 +566,13 @@ __device__ __forceinline__ void group_body(const int32_t* __restrict__ marr,
         hdr->contributions = 0;
         hdr->evaluations = 0;
         hdr->groups = 0;
+        hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
+        hdr->lane_hi = INT32_MIN;
         if (!init) {
             hdr->runs_overflow = 0;
             hdr->bad_mn = 0;
             hdr->bad_tile = 0;
-            hdr->pad[0] = hdr->pad[1] = hdr->pad[2] = 0;
+            hdr->pad[0] = hdr->pad[1] = 0;
             hdr->magic = HDR_MAGIC;
         }
     }
@@ -1643,9 +1646,11 @@ __device__ __forceinline__ void segment_compact_body(const int2* __restrict__ sl
                                                          int2* __restrict__ seglh,
                                                          int4* __restrict__ seginfo,
                                                          int32_t* __restrict__ segbase,
-                                                         int32_t* __restrict__ nseg, int nblk) {
+                                                         int32_t* __restrict__ nseg, int nblk,
+                                                         Header* __restrict__ hdr) {
     __shared__ int wc[4];
     __shared__ int64_t wt[4];
+    __shared__ int2 wr[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int blk = blockIdx.x;
     int before = 0;
@@ -1687,6 +1692,22 @@ __device__ __forceinline__ void segment_compact_body(const int2* __restrict__ sl
                                                          : SEG_NO_STB;
     }
     if (blk == nblk - 1 && tid == 0) *nseg = base + wc[0] + wc[1] + wc[2] + wc[3];
+    // the union of the block's segment lane ranges into the header: k_modesum's tiles outside
+    // it skip the list build (one block-wide min / max, two global atomics per block)
+    int lo = valid ? lh.x : INT32_MAX, hi = valid ? lh.y : INT32_MIN;
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    if (lane == 0) wr[wave] = make_int2(lo, hi);
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w) { lo = min(lo, wr[w].x); hi = max(hi, wr[w].y); }
+        if (lo < hi) {
+            atomicMin(&hdr->lane_lo, lo);
+            atomicMax(&hdr->lane_hi, hi);
+        }
+    }
 }
 __global__ __launch_bounds__(256) void k_segment_compact(const PrepBatch B) {
     PREP_WALKER(B);
@@ -1696,7 +1717,7 @@ __global__ __launch_bounds__(256) void k_segment_compact(const PrepBatch B) {
                          ws_at<int32_t>(W, L.slotcnt), ws_at<int32_t>(W, L.slottiles),
                          2 * MAXRUNS * D.K, L.stbcap, ws_at<int2>(W, L.seglh),
                          ws_at<int4>(W, L.seginfo), ws_at<int32_t>(W, L.segbase),
-                         ws_at<int32_t>(W, L.nseg), nblk);
+                         ws_at<int32_t>(W, L.nseg), nblk, ws_at<Header>(W, L.header));
 }
 
 // One workgroup per segment (grid-stride): for every record p of the segment in lane order
@@ -2677,7 +2698,12 @@ __device__ __forceinline__ void modesum_tile(
     // keys[] until KEYCAP, then the chunked evaluation below drains them. The summation order
     // (segment, then lane order) is fixed, so the result is bitwise reproducible.
     const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
-    const int nseg = *nsegp;
+    // a tile outside the union of the segments' lane ranges has no record: no list to build
+#ifndef EFD_TILE_UNION
+#define EFD_TILE_UNION 1
+#endif
+    const int nseg = (EFD_TILE_UNION && pre < 0 && (hdr->lane_hi <= tlo || hdr->lane_lo >= thi))
+                         ? 0 : *nsegp;
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
     const int32_t w_hi = w_lo + 64 * BPL;
     double fk[BPL], tfk[BPL];
