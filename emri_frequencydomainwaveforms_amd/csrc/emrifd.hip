@@ -2604,7 +2604,8 @@ __device__ __forceinline__ void modesum_tile(
     // fused likelihood: the partial of a tile with no record (h = 0 on its bins), the same for
     // every walker (efd_loglike_tile_constants); NULL: such tiles compute it
     const double* __restrict__ llconst,
-    int64_t b) {   // b: this workgroup's place in the waveform's dispatch order
+    int64_t b,     // b: this workgroup's place in the waveform's dispatch order
+    bool direct = false) {   // b is the tile itself (k_modesum_batch's sparse form)
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -2624,7 +2625,9 @@ __device__ __forceinline__ void modesum_tile(
     // longest-first dispatch, so the launch does not end on expensive tiles started late;
     // consecutive blocks (similar cost) land on different XCDs.
     int64_t tile;
-    if (tperm != nullptr) {
+    if (direct) {
+        tile = b;
+    } else if (tperm != nullptr) {
         if (b >= ntiles) return;   // grid padding
         tile = tperm[b];
         if ((uint64_t)tile >= (uint64_t)ntiles) {
@@ -3222,11 +3225,17 @@ struct SumBatch {
     int32_t n;
 };
 static_assert(sizeof(SumBatch) <= 3584, "batch descriptors must fit the kernel arguments");
-template <bool PAIRED, int CAUSTIC, int BPL>
+// SPARSE (the fused likelihood with tile constants, no written outputs): only the tiles inside the
+// union of the waveform's segment lane ranges ([lane_lo, lane_hi) in its header, k_segment_compact)
+// are visited, by nper workgroups per waveform striding over them; k_ll_final takes the constant
+// of every tile outside. A sparse spectrum (config 4: 15 harmonics cover 576 of 6,164 tiles) then
+// launches a few hundred workgroups per walker instead of one per tile.
+template <bool PAIRED, int CAUSTIC, int BPL, bool SPARSE>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t ntiles,
                      int accumulate_out, const double* __restrict__ lld,
-                     const double* __restrict__ llw, const double* __restrict__ llconst) {
+                     const double* __restrict__ llw, const double* __restrict__ llconst,
+                     int64_t nper) {
     const int n = batch.n;
     int w;
     int64_t pos;
@@ -3244,6 +3253,20 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
         pos = (int64_t)(r / (unsigned)n) * 8 + (g & 7u);
     }
     const BatchDesc& d = batch.d[w];
+    if (SPARSE) {
+        const int32_t lo = d.hdr->lane_lo, hi = d.hdr->lane_hi;
+        if (lo >= hi) return;
+        const int64_t t1 = min((int64_t)(hi - 1) / TILE_LANES, ntiles - 1);
+        for (int64_t tile = lo / TILE_LANES + pos; tile <= t1; tile += nper) {
+            modesum_tile<PAIRED, CAUSTIC, BPL>(
+                d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt,
+                d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm,
+                d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld,
+                llw, d.llpart, llconst, tile, true);
+            __syncthreads();   // the next tile's LDS writes after every wave's last reads
+        }
+        return;
+    }
     modesum_tile<PAIRED, CAUSTIC, BPL>(
         d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt, d.K,
         d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm, d.segbase, d.stb0,
@@ -3322,6 +3345,7 @@ struct LlBatch {
     const double* part[EFD_BATCH_MAX];
     const Header* hdr[EFD_BATCH_MAX];
     double* out;
+    const double* llconst;   // sparse sum: the constants of the tiles outside each lane union
     int64_t ntiles;
     int32_t n;
 };
@@ -3347,8 +3371,27 @@ __global__ __launch_bounds__(64) void k_status_gather(const StatusBatch sb, int3
 __global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
     __shared__ double red[256];
     const double* p = lb.part[blockIdx.x];
+    const Header* h = lb.hdr[blockIdx.x];
+    // tiles [t0, t1] hold their own partials; with llconst (k_modesum_batch's sparse form) the
+    // others are empty and take their constants
+    int64_t t0 = 0, t1 = lb.ntiles - 1;
+    if (lb.llconst != nullptr) {
+        const int32_t lo = h->lane_lo, hi = h->lane_hi;
+        t0 = lo < hi ? lo / TILE_LANES : lb.ntiles;
+        t1 = lo < hi ? (int64_t)(hi - 1) / TILE_LANES : -1;
+    }
+    auto val = [&](int64_t i) { return (i < t0 || i > t1) ? lb.llconst[i] : p[i]; };
+    // each thread's tiles i, i + 256, ... added in that order; four loads in flight at a time
     double acc = 0.0;
-    for (int64_t i = threadIdx.x; i < lb.ntiles; i += 256) acc += p[i];
+    int64_t i = threadIdx.x;
+    for (; i + 3 * 256 < lb.ntiles; i += 4 * 256) {
+        const double v0 = val(i), v1 = val(i + 256), v2 = val(i + 512), v3 = val(i + 768);
+        acc += v0;
+        acc += v1;
+        acc += v2;
+        acc += v3;
+    }
+    for (; i < lb.ntiles; i += 256) acc += val(i);
     red[threadIdx.x] = acc;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -3359,7 +3402,6 @@ __global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
         // a walker whose workspace holds a device-side error flag gets a NaN log-likelihood
         // (the flags stay set: efd_modesum_status_batch reports and clears them), so a caller
         // that finds no NaN in the batch needs no status synchronisation
-        const Header* h = lb.hdr[blockIdx.x];
         const bool bad = h->runs_overflow | h->bad_mn | h->bad_tile;
         lb.out[blockIdx.x] = bad ? __longlong_as_double(0x7ff8000000000000LL) : -0.5 * 4.0 * red[0];
     }
@@ -4216,6 +4258,12 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
 
 // efd_modesum_sum_batch, and efd_modesum_sum_loglike when d != NULL (paired grids: the tiles
 // write their likelihood partials, k_ll_final turns each waveform's into out[i])
+#ifndef EFD_SPARSE_SUM
+#define EFD_SPARSE_SUM 1
+#endif
+#ifndef EFD_SPARSE_WG
+#define EFD_SPARSE_WG 4096   // workgroups of a sparse launch, all waveforms
+#endif
 int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const* workspace,
                    const size_t* workspace_bytes, int32_t count, const double* d, const double* w,
                    double* llout, void* stream, const double* llconst = nullptr) {
@@ -4277,15 +4325,35 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         d.K = ai->K;
     }
     hipStream_t st = (hipStream_t)stream;
+    // the sparse form (k_modesum_batch): the fused likelihood with tile constants, nothing
+    // written, and in-kernel lists (below 1,024 harmonics: the sparse spectra; denser ones keep
+    // the longest-first order over every tile)
+    bool sparse = EFD_SPARSE_SUM && d != nullptr && llconst != nullptr && a[0]->grid_symmetric;
+    for (int i = 0; i < count && sparse; ++i)
+        sparse = !a[i]->out && !a[i]->hp && !a[i]->hc && !use_prebuilt(a[i]->K) &&
+                 !use_cost_order(make_layout(a[i]->nt, a[i]->K, a[i]->nf, 1), a[i]->K);
     const int64_t gq = 8 * XCD_GROUP;
-    const int64_t nblk = (L0.ntiles + gq - 1) / gq * gq * count;
+    int64_t nper = 0;
+    if (sparse) {
+        // workgroups per waveform: a multiple of 8 (one XCD place each), ~EFD_SPARSE_WG in all
+        const int64_t cap = std::max<int64_t>(64, (EFD_SPARSE_WG / count + 7) / 8 * 8);
+        nper = std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
+    }
+    const int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;
     if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, F + ": grid too large");
     const dim3 grid((unsigned)nblk), block(TILE);
     const int acc = a[0]->accumulate ? 1 : 0;
     if (a[0]->prof_begin) HIP_TRY(hipEventRecord((hipEvent_t)a[0]->prof_begin, st));
 #define EFD_LAUNCH(P, C)                                                                      \
-    hipLaunchKernelGGL((k_modesum_batch<P, C, BPL>), grid, block, 0, st, batch, a[0]->nf,       \
-                       L0.nlanes, L0.ntiles, acc, d, w, d ? llconst : nullptr)
+    do {                                                                                      \
+        if (sparse)                                                                           \
+            hipLaunchKernelGGL((k_modesum_batch<P, C, BPL, true>), grid, block, 0, st, batch,  \
+                               a[0]->nf, L0.nlanes, L0.ntiles, acc, d, w, llconst, nper);     \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_modesum_batch<P, C, BPL, false>), grid, block, 0, st, batch, \
+                               a[0]->nf, L0.nlanes, L0.ntiles, acc, d, w,                     \
+                               d ? llconst : nullptr, (int64_t)0);                            \
+    } while (0)
     if (a[0]->grid_symmetric) {
         if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
         else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
@@ -4304,6 +4372,7 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
             lb.hdr[i] = (const Header*)workspace[i];
         }
         lb.out = llout;
+        lb.llconst = sparse ? llconst : nullptr;
         hipLaunchKernelGGL(k_ll_final, dim3((unsigned)count), dim3(256), 0, st, lb);
         HIP_TRY(hipGetLastError());
     }
