@@ -2707,6 +2707,8 @@ __device__ __forceinline__ void modesum_tile(
 #endif
     const int nseg = (EFD_TILE_UNION && pre < 0 && (hdr->lane_hi <= tlo || hdr->lane_lo >= thi))
                          ? 0 : *nsegp;
+    // a tile with no record at all never reads its frequencies (block-uniform)
+    const bool anyrec = pre > 0 || (pre < 0 && nseg > 0);
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
     const int32_t w_hi = w_lo + 64 * BPL;
     double fk[BPL], tfk[BPL];
@@ -2714,7 +2716,7 @@ __device__ __forceinline__ void modesum_tile(
 #pragma unroll
     for (int i = 0; i < BPL; ++i) {
         const int32_t k = w_lo + 64 * i + lane;
-        fk[i] = k < nlanes ? freq[k] : 0.0;
+        fk[i] = (anyrec && k < nlanes) ? freq[k] : 0.0;
         tfk[i] = TWO_PI * fk[i];
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
     }
