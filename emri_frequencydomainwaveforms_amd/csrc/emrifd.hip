@@ -2667,28 +2667,35 @@ __device__ __forceinline__ void modesum_tile(
     // table and the build below is skipped. Same keys in the same order as the build below, so
     // the sum is bitwise the in-kernel build's.
     const int pre = tcnt != nullptr ? tcnt[tile] : -1;
-    // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces). A
-    // prebuilt list brings it in with the keys; otherwise it comes in with the first stage of
-    // records, so a tile without records never loads it (tab = table issued: block-uniform)
+    const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
+    // a tile outside the union of the segments' lane ranges has no record: no list to build
+#ifndef EFD_TILE_UNION
+#define EFD_TILE_UNION 1
+#endif
+    const int nseg = (EFD_TILE_UNION && pre < 0 && (hdr->lane_hi <= tlo || hdr->lane_lo >= thi))
+                         ? 0 : *nsegp;
+    // a tile that can have records (a prebuilt list, or segments to search): block-uniform. Tiles
+    // without read neither their frequencies nor the sin/cos table
+    const bool anyrec = pre > 0 || (pre < 0 && nseg > 0);
+    bool seen = pre > 0;   // records evaluated (the fused likelihood's constant otherwise)
+    // the (sin, cos) table: k_group's copy, global -> LDS by LDS-DMA (lane-linear pieces), with
+    // a prebuilt list's keys
     static_assert(SCTAB % TILE == 0, "sin/cos table copy: whole rounds");
-#define EFD_TABLE_DMA()                                                                       \
-    do {                                                                                      \
-        _Pragma("unroll") for (int rd_ = 0; rd_ < SCTAB / TILE; ++rd_)                        \
-            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd_ * TILE + tid,                \
-                   reinterpret_cast<uint4*>(sctab) + rd_ * TILE + wave * 64);                 \
-    } while (0)
-    bool tab = false;
-    if (pre > 0) {
-        static_assert(KEYCAP % (4 * TILE) == 0, "key copy: whole rounds of 16-B pieces");
+    if (anyrec) {
+        if (pre > 0) {
+            static_assert(KEYCAP % (4 * TILE) == 0, "key copy: whole rounds of 16-B pieces");
 #pragma unroll
-        for (int rd = 0; rd < KEYCAP / (4 * TILE); ++rd) {
-            const int pc = rd * TILE + tid;                     // 16-B piece = 4 keys
-            if (4 * pc < pre)
-                glds16(reinterpret_cast<const uint4*>(tkeys + (size_t)tile * KEYCAP) + pc,
-                       reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
+            for (int rd = 0; rd < KEYCAP / (4 * TILE); ++rd) {
+                const int pc = rd * TILE + tid;                     // 16-B piece = 4 keys
+                if (4 * pc < pre)
+                    glds16(reinterpret_cast<const uint4*>(tkeys + (size_t)tile * KEYCAP) + pc,
+                           reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
+            }
         }
-        EFD_TABLE_DMA();
-        tab = true;
+#pragma unroll
+        for (int rd = 0; rd < SCTAB / TILE; ++rd)
+            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
+                   reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
         __syncthreads();
     }
@@ -2700,15 +2707,6 @@ __device__ __forceinline__ void modesum_tile(
     // sub-range [p0, p0 + n) reaching into the tile; (3) a block scan places the keys. Keys go to
     // keys[] until KEYCAP, then the chunked evaluation below drains them. The summation order
     // (segment, then lane order) is fixed, so the result is bitwise reproducible.
-    const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
-    // a tile outside the union of the segments' lane ranges has no record: no list to build
-#ifndef EFD_TILE_UNION
-#define EFD_TILE_UNION 1
-#endif
-    const int nseg = (EFD_TILE_UNION && pre < 0 && (hdr->lane_hi <= tlo || hdr->lane_lo >= thi))
-                         ? 0 : *nsegp;
-    // a tile with no record at all never reads its frequencies (block-uniform)
-    const bool anyrec = pre > 0 || (pre < 0 && nseg > 0);
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
     const int32_t w_hi = w_lo + 64 * BPL;
     double fk[BPL], tfk[BPL];
@@ -2885,10 +2883,7 @@ __device__ __forceinline__ void modesum_tile(
         // ---- evaluate the nkeys records in chunks of NC through the double-buffered stage
         const int cnt = nkeys;
         const int nchunk = (cnt + NC - 1) / NC;
-        if (!tab) {   // the first records of a built list: the table comes in with their stage
-            EFD_TABLE_DMA();
-            tab = true;
-        }
+        seen = true;
         EFD_GLDS(0, 0);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's LDS-DMA pieces landed
         __syncthreads();
@@ -3064,8 +3059,7 @@ __device__ __forceinline__ void modesum_tile(
         if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
-#undef EFD_TABLE_DMA
-    if (PAIRED && llconst != nullptr && !tab && out == nullptr && hp == nullptr) {
+    if (PAIRED && llconst != nullptr && !seen && out == nullptr && hp == nullptr) {
         // no record reached this tile: h = 0 on its bins, whose likelihood partial is the
         // walker-independent one k_ll_tile_const computed with this epilogue's arithmetic
         if (tid == 0) llpart[tile] = llconst[tile];

@@ -15,8 +15,11 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc", "emrifd.hip")
-KERNEL = "k_modesumILb1ELi1E"
+# ASM_SRC / ASM_KERNEL: another source file (e.g. an older revision) or kernel symbol prefix
+# (the batch sum of config 2: k_modesum_batchILb1ELi1ELi2ELb0E)
+SRC = os.environ.get("ASM_SRC") or os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc",
+                                                "emrifd.hip")
+KERNEL = os.environ.get("ASM_KERNEL", "k_modesumILb1ELi1E")
 
 
 def analyse(flags, show=False):
