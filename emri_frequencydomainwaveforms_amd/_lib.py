@@ -43,6 +43,8 @@ EXPORTED_SYMBOLS = (
     "efd_td_workspace_bytes",
     "efd_td_modesum",
     "efd_upload",
+    "efd_download",
+    "efd_stream_order",
     "efd_polarizations",
     "efd_loglike",
     "efd_inner_product",
@@ -205,6 +207,11 @@ def load(path=None):
     if hasattr(lib, "efd_upload"):   # absent only in older experiment builds
         lib.efd_upload.restype = ctypes.c_int
         lib.efd_upload.argtypes = [vp, vp, sz, vp]
+    if hasattr(lib, "efd_stream_order"):
+        lib.efd_download.restype = ctypes.c_int
+        lib.efd_download.argtypes = [vp, vp, sz, vp]
+        lib.efd_stream_order.restype = ctypes.c_int
+        lib.efd_stream_order.argtypes = [vp, ctypes.POINTER(vp), i32]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int

@@ -4591,6 +4591,31 @@ int efd_upload(void* dst, const void* src, size_t bytes, void* stream) {
     return EFD_OK;
 }
 
+int efd_download(void* dst, const void* src, size_t bytes, void* stream) {
+    if (bytes == 0) return EFD_OK;
+    if (!dst || !src) return fail(EFD_ERR_ARG, "efd_download: NULL pointer");
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return EFD_OK;
+}
+
+int efd_stream_order(void* src, void* const* dst, int32_t count) {
+    if (count < 0 || (count > 0 && !dst))
+        return fail(EFD_ERR_ARG, "efd_stream_order: need count >= 0 and a stream array");
+    if (count == 0) return EFD_OK;
+    // one event per thread and device, re-recorded each call: a wait already enqueued keeps the
+    // record it saw (stream-wait semantics), so reuse never loosens an earlier ordering
+    constexpr int MAX_DEV = 64;
+    thread_local hipEvent_t ev[MAX_DEV] = {};
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= MAX_DEV) return fail(EFD_ERR_ARG, "efd_stream_order: device index");
+    if (!ev[dev]) HIP_TRY(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ev[dev], (hipStream_t)src));
+    for (int32_t i = 0; i < count; ++i)
+        if (dst[i] != src) HIP_TRY(hipStreamWaitEvent((hipStream_t)dst[i], ev[dev], 0));
+    return EFD_OK;
+}
+
 int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, double* hc,
                       void* stream) {
     if (!S || !hp || !hc || nf <= 0 || k0 < 0 || k0 > nf)

@@ -25,8 +25,11 @@ Results are numpy float64 arrays ([B]), or device tensors with use_gpu=True, ret
 Time-domain templates (dt only) are not part of this path: get_ll raises NotImplementedError.
 """
 
+import ctypes
+
 import numpy as np
 
+from . import _lib
 from .summation import require_gpu
 
 
@@ -260,9 +263,24 @@ class Likelihood:
                                                       caustic=caustic, device=self.device),
                                    stream=torch.cuda.Stream(self.device))
         B, s_sum = F["prep"], F["stream"]
+        if "order" not in F:
+            # the stream handles the orderings below take (efd_stream_order: one event record
+            # and one stream wait each, in C), and one reused release event per group
+            vp = ctypes.c_void_p
+            F["order"] = (vp * (len(B.groups) + 1))(*[g["stream"].cuda_stream for g in B.groups],
+                                                     s_sum.cuda_stream)
+            F["gst"] = [g["stream"].cuda_stream for g in B.groups]
+            F["sum1"] = (vp * 1)(s_sum.cuda_stream)
+            F["ev"] = [torch.cuda.Event() for _ in B.groups]
+        lib = B.lib
         cur = torch.cuda.current_stream(self.device)
-        B.order_after_current()
-        s_sum.wait_stream(cur)
+        curh = cur.cuda_stream
+        # the groups' streams and the sum stream after the work queued so far on the current one
+        _lib.check(lib.efd_stream_order(curh, F["order"], len(F["order"])), "efd_stream_order",
+                   lib)
+        pin = F.get("pin")
+        if pin is None or pin.numel() < n:
+            pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
         try:
             batch = getattr(tm, "submit_batch", None)
             for g0 in range(0, n, G):
@@ -273,18 +291,16 @@ class Likelihood:
                         tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
                                   **kwargs)
                 gi, jobs = B.flush()
-                s_sum.wait_stream(B.stream(gi))
+                _lib.check(lib.efd_stream_order(F["gst"][gi], F["sum1"], 1), "efd_stream_order",
+                           lib)
                 tc = self._tile_constants(jobs[0][1], s_sum)
                 B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)],
                               s_sum.cuda_stream, tile_const=tc)
-                ev = torch.cuda.Event()
+                ev = F["ev"][gi]   # (flush waited on its previous record before this one)
                 ev.record(s_sum)
                 B.release(gi, ev)
-            pin = F.get("pin")
-            if pin is None or pin.numel() < n:
-                pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
-            with torch.cuda.stream(s_sum):
-                pin[:n].copy_(out[:n], non_blocking=True)
+            _lib.check(lib.efd_download(pin.data_ptr(), out.data_ptr(), 8 * n, s_sum.cuda_stream),
+                       "efd_download", lib)
         finally:
             B._pending = []
             # `out` belongs to the current stream: nothing may still write it when it is
@@ -293,7 +309,6 @@ class Likelihood:
         host = pin[:n].numpy().copy()
         if np.isnan(host).any():
             B.wait()   # device-side errors of the groups' workspaces (sticky across reuse)
-        cur.wait_stream(s_sum)
         return host
 
     # tiles no harmonic reaches take a precomputed partial instead of re-reading d and w

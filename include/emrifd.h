@@ -273,6 +273,15 @@ int efd_td_modesum(const efd_td_args* a, void* workspace, size_t workspace_bytes
  */
 int efd_upload(void* dst, const void* src, size_t bytes, void* stream);
 
+/* Host plumbing for batched callers: `bytes` from device memory into (pinned) host memory,
+ * asynchronous on `stream` (hipMemcpyAsync). */
+int efd_download(void* dst, const void* src, size_t bytes, void* stream);
+
+/* Host plumbing: the `count` streams dst[i] wait for the work queued so far on stream `src`
+ * (one event record, one stream wait each; nothing blocks the host). The library's event is
+ * per thread and device and re-recorded by each call; waits already enqueued are unaffected. */
+int efd_stream_order(void* src, void* const* dst, int32_t count);
+
 /*
  * h+ = (S(f) + conj(S_flip))/2, hx = i (S(f) - conj(S_flip))/2 with S_flip the array reversed
  * (FEW list output). Writes bins [k0, nf) of each (k0 = first bin to keep, e.g. the f >= 0

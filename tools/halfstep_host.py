@@ -7,7 +7,7 @@ timers between its phases (grid check and prefetch, stream setup, submit_batch, 
 sum_loglike and events, the final synchronisation, the status check) and prints microseconds
 per half-step. Keep the copy in step with likelihood.py when that changes.
 """
-import sys, time, json, collections
+import sys, time, json, collections, ctypes
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import numpy as np, torch
 import bench
@@ -34,9 +34,19 @@ def fused(self, tm, params, args, kwargs, out):
     if F is None:
         F = self._fused = dict(prep=BatchPreparer(max(G, self.FUSED_GROUP), self.FUSED_DEPTH, caustic=caustic, device=self.device), stream=torch.cuda.Stream(self.device))
     B, s_sum = F["prep"], F["stream"]
+    if "order" not in F:
+        vp = ctypes.c_void_p
+        F["order"] = (vp * (len(B.groups) + 1))(*[g["stream"].cuda_stream for g in B.groups],
+                                                 s_sum.cuda_stream)
+        F["gst"] = [g["stream"].cuda_stream for g in B.groups]
+        F["sum1"] = (vp * 1)(s_sum.cuda_stream)
+        F["ev"] = [torch.cuda.Event() for _ in B.groups]
+    lib = B.lib
     cur = torch.cuda.current_stream(self.device)
-    B.order_after_current()
-    s_sum.wait_stream(cur)
+    lib.efd_stream_order(cur.cuda_stream, F["order"], len(F["order"]))
+    pin = F.get("pin")
+    if pin is None or pin.numel() < n:
+        pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
     t2 = pc(); acc["setup"] += t2 - t1
     batch = tm.submit_batch
     for g0 in range(0, n, G):
@@ -45,15 +55,13 @@ def fused(self, tm, params, args, kwargs, out):
         tb = pc(); acc["submit_batch"] += tb - ta
         gi, jobs = B.flush()
         tc = pc(); acc["flush"] += tc - tb
-        s_sum.wait_stream(B.stream(gi))
-        B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)], s_sum.cuda_stream)
-        ev = torch.cuda.Event(); ev.record(s_sum); B.release(gi, ev)
+        lib.efd_stream_order(F["gst"][gi], F["sum1"], 1)
+        tcon = self._tile_constants(jobs[0][1], s_sum)
+        B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)], s_sum.cuda_stream,
+                      tile_const=tcon)
+        ev = F["ev"][gi]; ev.record(s_sum); B.release(gi, ev)
         td = pc(); acc["sum+events"] += td - tc
-    pin = F.get("pin")
-    if pin is None or pin.numel() < n:
-        pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
-    with torch.cuda.stream(s_sum):
-        pin[:n].copy_(out[:n], non_blocking=True)
+    lib.efd_download(pin.data_ptr(), out.data_ptr(), 8 * n, s_sum.cuda_stream)
     t3 = pc()
     B._pending = []
     s_sum.synchronize()
@@ -61,7 +69,6 @@ def fused(self, tm, params, args, kwargs, out):
     host = pin[:n].numpy().copy()
     if np.isnan(host).any():
         B.wait()
-    cur.wait_stream(s_sum)
     t5 = pc(); acc["status"] += t5 - t4
     return host
 L.Likelihood._get_ll_fused = fused
