@@ -146,3 +146,32 @@ def test_fused_loglike_argument_errors_are_host_side():
             setattr(a2, field, bad)
         rc, msg = call(a2, c)
         assert rc == -1 and b"fused likelihood needs" in msg, (field, msg)
+
+
+def test_tile_constants_and_ordering_argument_errors_are_host_side():
+    """efd_loglike_tile_count / _tile_constants, efd_modesum_sum_loglike_ex, efd_download and
+    efd_stream_order validate their arguments before any HIP call."""
+    lib = _lib.load()
+    fake = ctypes.c_void_p(16)
+    buf = ctypes.create_string_buffer(256)
+    assert lib.efd_loglike_tile_count(0) == 0
+    assert lib.efd_loglike_tile_count(6311631) == 6164   # config 4: 3,155,816 lane pairs / 512
+    assert lib.efd_loglike_tile_count(1001) >= 1
+    assert lib.efd_loglike_tile_constants(None, fake, 1001, 500, fake, None) == -1
+    lib.efd_last_error(buf, 256)
+    assert b"NULL d, w or tile_const" in buf.value
+    assert lib.efd_loglike_tile_constants(fake, fake, 1001, 1001, fake, None) == -1
+    lib.efd_last_error(buf, 256)
+    assert b"0 <= k0 < nf" in buf.value
+    pa = (ctypes.POINTER(_lib.ModesumArgs) * 1)()
+    ws = (ctypes.c_void_p * 1)(16)
+    nb = (ctypes.c_size_t * 1)(1 << 40)
+    assert lib.efd_modesum_sum_loglike_ex(pa, ws, nb, 1, fake, fake, fake, None, None) == -1
+    lib.efd_last_error(buf, 256)
+    assert b"NULL d, w or out" in buf.value
+    assert lib.efd_download(None, fake, 8, None) == -1
+    assert lib.efd_download(None, None, 0, None) == 0          # nothing to copy
+    assert lib.efd_stream_order(None, None, 0) == 0             # nothing to order
+    assert lib.efd_stream_order(None, None, 2) == -1
+    lib.efd_last_error(buf, 256)
+    assert b"efd_stream_order" in buf.value
