@@ -146,7 +146,7 @@ class ModeSumEngine:
         self.lib = _lib.load()
         self._ws = None
         self._ws_key = None
-        self._ws_cap, self._ws_dev = 0, None
+        self._ws_cap, self._ws_dev, self._ws_ptr = 0, None, 0
         self._last_args = None
         self.last_contributions = None
 
@@ -182,6 +182,7 @@ class ModeSumEngine:
                     ws[:64].zero_()
             self._ws = ws
         self._ws_cap, self._ws_dev = self._ws.numel(), self._ws.device
+        self._ws_ptr = self._ws.data_ptr()
         return self._ws
 
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
@@ -668,7 +669,8 @@ class BatchPreparer:
         keep = []    # arrays converted here stay alive until the staging copy below
         fast = [p[0].get("_src") for p in pend]
         scale = np.array([(p[3].real, p[3].imag) for p in pend], dtype=np.float64)
-        if all(f is not None for f in fast):
+        allfast = all(f is not None for f in fast)
+        if allfast:
             # the native upstream's walkers (prepare() records their arrays' addresses): one
             # conversion for the group instead of row by row
             src = np.array(fast, dtype=np.uint64)
@@ -676,7 +678,7 @@ class BatchPreparer:
         else:
             src = np.empty((n, 10), dtype=np.uint64)
             shape = np.empty((n, 2), dtype=np.int32)
-        for i, (host, _, _, sc, _, _) in enumerate(pend):
+        for i, (host, _, _, sc, _, _) in enumerate(() if allfast else pend):
             if fast[i] is not None:
                 src[i] = fast[i]
                 shape[i] = host["_shape"]
@@ -720,14 +722,19 @@ class BatchPreparer:
             G["pin_done"] = torch.cuda.Event()
         G["pin_done"].record(st)
         A, pw, pb = G["args"], G["pw"], G["pb"]
+        if "A_i" not in G:   # stable views of the group's argument structs, made once
+            G["A_i"] = [A[i] for i in range(self.group)]
+        A_i, engines = G["A_i"], G["engines"]
         jobs = []
         dev = freq.device
         for i, (nt_i, K_i) in enumerate(shape.tolist()):
-            eng = G["engines"][i]
-            ws = eng._workspace(nt_i, K_i, nf, dev, stream=st)
-            pw[i] = ws.data_ptr()
+            eng = engines[i]
+            nbytes = _WS_BYTES.get((nt_i, K_i, nf))
+            if nbytes is None or eng._ws is None or eng._ws_cap < nbytes or eng._ws_dev != dev:
+                eng._workspace(nt_i, K_i, nf, dev, stream=st)   # sized, or grown, here
+            pw[i] = eng._ws_ptr
             pb[i] = eng._ws_cap
-            a_i = A[i]
+            a_i = A_i[i]
             eng._last_args = a_i
             jobs.append((eng, {"freq": freq, "k0": k0, "grid_symmetric": sym, "_args": a_i}))
         _lib.check(self.lib.efd_modesum_prepare_batch(G["pa"], ctypes.cast(pw, ctypes.POINTER(
