@@ -27,6 +27,7 @@ import threading
 
 import numpy as np
 
+from . import _lib
 from .amplitude import ModeSelector, RomanAmplitude
 from .constants import Gpc, MRSUN_SI, MTSUN_SI
 from .frequencies import get_fundamental_frequencies
@@ -174,7 +175,19 @@ class FastSchwarzschildEccentricFlux:
         calls = [tuple(c) for c in calls]
         for c in calls:                       # Ylm per viewing angle before the threads start
             self._ylms(c[4], c[5])
-        res = list(_pool().map(lambda c: self.prepare(*c), calls))
+        pool = _pool()
+        # a batch smaller than the pool gives each walker's mode selection several OpenMP
+        # threads (efd_host_set_threads is per calling thread; bitwise the same result)
+        per = max(1, pool._max_workers // max(1, len(calls)))
+        if os.environ.get("EFD_PREFETCH_SPLIT", "1") == "0":
+            per = 1
+        lib = _lib.load()
+
+        def run(c):
+            lib.efd_host_set_threads(per)
+            return self.prepare(*c)
+
+        res = list(pool.map(run, calls))
         with self._lock:
             if len(self._prefetched) > 4096:   # results nobody took (e.g. after an exception)
                 self._prefetched.clear()
