@@ -57,51 +57,34 @@
 
 namespace {
 
-#ifndef EFD_TILE
-#define EFD_TILE 256
-#endif
-constexpr int TILE = EFD_TILE;      // threads per workgroup in k_modesum
+constexpr int TILE = 256;           // threads per workgroup in k_modesum (round 2: 512-thread
+                                    // tiles of 8 waves ran 0.974x)
 constexpr int NWAVE = TILE / 64;    // waves per workgroup
-#ifndef EFD_BPL
-#define EFD_BPL 2
-#endif
-constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum
+constexpr int BPL = 2;              // bins (lanes) per thread in k_modesum (3 or 4: +3-5%)
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
 constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
-#ifndef EFD_KEYCAP
-#define EFD_KEYCAP (EFD_TILE >= 512 ? 4096 : EFD_TILE >= 256 ? 2048 : 1024)
-#endif
-#ifndef EFD_SEGWIN_F
-#define EFD_SEGWIN_F 1   // 256 segments per window: 4 KB of LDS instead of 16 (4 workgroups/CU)
-#endif
-constexpr int KEYCAP = EFD_KEYCAP;  // record keys per tile pass held in LDS
-constexpr int SEGWIN = EFD_SEGWIN_F * TILE;  // segments examined per window (tile list build)
+constexpr int KEYCAP = 2048;        // record keys per tile pass held in LDS
+constexpr int SEGWIN = TILE;        // segments examined per window (tile list build): 4 KB of LDS
+                                    // instead of 16 at 4 x TILE, so 4 workgroups fit a CU
 constexpr int MAX_K = 8192;         // harmonics per call
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
 constexpr double INV_SQRT_3_2PI = 1.44720250911653531871; // sqrt(2 pi / 3)
-// EFD_VSCALE: the records' F'' coefficients also carry |KRH_1|^(1/4), so the fast path's square
+// The records' F'' coefficients carry sqrt(3/(2 pi)) |KRH_1|^(1/4), so the fast path's square
 // is v = sqrt|KRH_1| / |y| instead of 1/|y|: rho's leading correction 1 + KRH_1 / y^2 becomes
 // 1 - v^2, one FMA (the K_{1/3} series constants below are rescaled to v)
-#ifndef EFD_VSCALE
-#define EFD_VSCALE 1
-#endif
 constexpr double VS = 0.18633899812498247470;             // sqrt|KRH_1|
-constexpr double FDD_SCALE = EFD_VSCALE ? 0.29827892638794838654 : SQRT_3_2PI;
-constexpr double INV_FDD_SCALE = EFD_VSCALE ? 3.3525667136785156343 : INV_SQRT_3_2PI;
+constexpr double FDD_SCALE = 0.29827892638794838654;
+constexpr double INV_FDD_SCALE = 3.3525667136785156343;
 
 // Fast-path series length: FAST_J terms of each of R and I/w, exact (truncation < 1e-17) for
 // |y| >= FAST_Y (J = 3 -> 555, 4 -> 153, 5 -> 75, 6 -> 48); lanes below FAST_Y take the general
 // path, whose K_{1/3} factor comes from the piecewise-polynomial table of kfactor_table.inc.
-#ifndef EFD_FAST_J
-#define EFD_FAST_J 4
-#endif
-constexpr int FAST_J = EFD_FAST_J;
-constexpr double FAST_Y = FAST_J <= 3 ? 555.0 : FAST_J == 4 ? 153.0 : FAST_J == 5 ? 75.0 : 48.0;
-static_assert(FAST_J >= 3 && FAST_J <= 6, "fast-path series: 3..6 terms");
+constexpr int FAST_J = 4;
+constexpr double FAST_Y = 153.0;
 // Truncation after J terms is KB[J] w^(2J) < 1e-17 for |y| >= JSER_Y[J]; k_items picks the
 // smallest J whose bound holds on the whole interval (a lower bound of |y| there).
 #define EFD_TABLE __constant__
@@ -151,10 +134,7 @@ static_assert(sizeof(Item) == 288, "Item must be 288 B");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
 constexpr int B_PIECE = (int)offsetof(Item, b) / 16;   // first piece of b (b[0]: 4, b[1]: 4)
 static_assert(offsetof(Item, b) % 16 == 0 && sizeof(Item::b) == 8 * 16, "b: 8 whole pieces");
-#ifndef EFD_STAGE_ROUNDS
-#define EFD_STAGE_ROUNDS 2
-#endif
-constexpr int ROUNDS = EFD_STAGE_ROUNDS;         // 16-B pieces per thread per LDS stage
+constexpr int ROUNDS = 2;                        // 16-B pieces per thread per LDS stage
 constexpr int NC = (ROUNDS * TILE) / PIECES;     // records per LDS stage
 
 // The error flags (runs_overflow, bad_mn, bad_tile) are sticky: k_group clears only the counters
@@ -265,27 +245,18 @@ template <class T>
 __device__ __forceinline__ T* ws_at(char* ws, size_t off) { return reinterpret_cast<T*>(ws + off); }
 
 // rows of scratch / knot data fetched per block ahead of the serial spline recurrences
-#ifndef EFD_SPLINE_PF
-#define EFD_SPLINE_PF 8   // 16: same, 32: slower (k_prep 110 -> 177 us)
-#endif
+constexpr int SPLINE_PF = 8;   // 16: same, 32: slower (k_prep 110 -> 177 us)
 
 // 1/x for the spline solves: the hardware reciprocal estimate and two Newton steps (5 dependent
 // operations, within an ulp) instead of the IEEE division sequence (~10, with the scale and
 // fixup steps) on the serial Thomas chains, whose latency sets the preparation's length; the
 // coefficients stay within 1e-11 of scipy's (tests/test_gpu_modesum.py), their rounding level
-#ifndef EFD_SPLINE_RCP
-#define EFD_SPLINE_RCP 1
-#endif
 __device__ __forceinline__ double spl_rcp(double x) {
-#if EFD_SPLINE_RCP
     double y = __builtin_amdgcn_rcp(x);
     double e = fma(-x, y, 1.0);
     y = fma(y, e, y);
     e = fma(-x, y, 1.0);
     return fma(y, e, y);
-#else
-    return 1.0 / x;
-#endif
 }
 
 // ----------------------------------------------------------------------------------------
@@ -361,7 +332,7 @@ __device__ void spline_not_a_knot(int n, FX X, FY Y, FCP CP, FDP DP, FOUT OUT) {
     // back substitution, emitting interval coefficients from the right. CP/DP may live in
     // global memory: they are fetched PF rows at a time (independent loads, one wait per
     // block) so the serial chain does not pay a memory round trip per row.
-    constexpr int PF = EFD_SPLINE_PF;
+    constexpr int PF = SPLINE_PF;
     double xr = X(n - 1), yr = Y(n - 1);
     for (int i0 = n - 2; i0 >= 0; i0 -= PF) {
         double cpb[PF], dpb[PF];
@@ -398,7 +369,7 @@ __device__ __forceinline__ double dcubic(const double* c, double w) {
 }
 
 // ----------------------------------------------------------------------------------------
-// The same not-a-knot system solved by one wave with parallel cyclic reduction (EFD_PCR).
+// The same not-a-knot system solved by one wave with parallel cyclic reduction.
 // spline_not_a_knot's Thomas sweeps are serial chains of ~2n dependent steps per interpolant,
 // with CP/DP round trips through global memory: k_prep took 60-75 us at N_t ~ 100 (the longest
 // kernel of a walker's preparation, and the preparation is the latency of small waveforms).
@@ -414,9 +385,6 @@ __device__ __forceinline__ double dcubic(const double* c, double w) {
 // L: LDS scratch of 7 n doubles; at exit L[0, n) = x, L[n, 2n) = y, L[4n, 5n) = the knot
 // slopes s_i. Called by every lane of a one-wave (64-thread) workgroup, 4 <= n <= PCR_NMAX.
 // ----------------------------------------------------------------------------------------
-#ifndef EFD_PCR
-#define EFD_PCR 1
-#endif
 constexpr int PCR_RPL = 8;                 // rows per lane
 constexpr int PCR_NMAX = 64 * PCR_RPL;     // knots; longer trajectories take the Thomas kernel
 // Waveforms of PCR_MAX_K harmonics or more keep the Thomas kernel's amplitude role (one lane per
@@ -900,7 +868,7 @@ __device__ void spline_shared(const double* __restrict__ x, int n, YF yf, int co
     auto DPs = [&](int i) -> double& { return dpbase[(size_t)i * scratch_stride + q]; };
     // Global loads (y, and DP on the way back) are issued PF rows at a time, ahead of the
     // serial recurrence, so each block of rows waits for memory once.
-    constexpr int PF = EFD_SPLINE_PF;
+    constexpr int PF = SPLINE_PF;
     // forward sweep: dp_i = (r_i - a_i dp_{i-1}) / m_i, r_i from sl_{i-1}, sl_i
     const double y0 = Y(0), y1 = Y(1);
     double yprev = Y(2);
@@ -1066,12 +1034,6 @@ __device__ __forceinline__ void prep_body(
     Item* __restrict__ items, double* __restrict__ invcp, double* __restrict__ invdp,
     Header* __restrict__ hdr) {
     const int b = blockIdx.x;
-#ifdef EFD_EXP_PREP_ROLE
-    {
-        const int role = b == 0 ? 0 : (b < 1 + nb_amp ? 1 : 2);
-        if (role != EFD_EXP_PREP_ROLE) return;
-    }
-#endif
     if (b == 0) {
         traj_splines(t, phi_phi, phi_r, f_phi, f_r, nt, coefT, kslope, tscratch);
     } else if (b < 1 + nb_amp) {
@@ -1112,7 +1074,7 @@ __global__ __launch_bounds__(64) void k_prep_b(const PrepBatch B) {
               ws_at<double>(W, L.invcp), ws_at<double>(W, L.invdp), ws_at<Header>(W, L.header));
 }
 
-// K1-K3 with one wave per interpolant (EFD_PCR): blocks [0, 4) the trajectory splines (Phi_phi,
+// K1-K3 with one wave per interpolant (parallel cyclic reduction): blocks [0, 4) the trajectory splines (Phi_phi,
 // Phi_r, f_phi, f_r; the f_phi and f_r blocks go on to f_phi', f_r' from their own knot
 // slopes), [4, 4 + K) the inverse splines of group h = b - 4 < G, [4 + K, 4 + 5K) the group
 // amplitude splines (interpolant q = b - 4 - K < 4G; only when Item::pcr bit 1 is set, else the
@@ -1363,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
 }
 
 // One interval record of group h; `evals` = its (branch x bin) evaluation count.
-// EFD_SAFE_REC: a record whose every lane is known to pass the fast path's per-lane validity
+// Certified records: a record whose every lane is known to pass the fast path's per-lane validity
 // tests -- t(g) inside the record's knot interval and F' of the record's sign, nonzero -- skips
 // them (Item::fdneg bit 1, header bit 25): one 64-bit compare and one class test per bin, with
 // their ballots and mask arithmetic. Certified here on the device, with the kernel's own
@@ -1373,9 +1335,6 @@ __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
 // interior bins' rounding, and F' keeps the record's sign over the whole interval with a margin
 // of 1e-12 of its terms. Fold and edge records (overshooting t(g), turning points) keep the
 // tests; a safe record's lanes would all have passed them, so the spectrum is bitwise the same.
-#ifndef EFD_SAFE_REC
-#define EFD_SAFE_REC 1
-#endif
 __device__ bool record_safe(const Item& it, const double* __restrict__ freq, int64_t lo0,
                             int64_t hi0, int64_t lo1, int64_t hi1) {
     // the g range of the lanes: s = 0 lanes k in [lo0, hi0) at g = -freq[k], s = 1 at +freq[k]
@@ -1530,9 +1489,7 @@ __device__ void build_item(
     it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
     it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
     ranges[(size_t)h * ni + j] = make_int4((int)lo0, (int)hi0, (int)lo1, (int)hi1);
-#if EFD_SAFE_REC
     if (record_safe(it, freq, lo0, hi0, lo1, hi1)) it.fdneg |= 2;
-#endif
     // branch x bin evaluations (on a paired grid one lane serves both the branch and its partner)
     const int mult = paired ? 1 + partner : 1;
     evals = (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
@@ -1635,9 +1592,6 @@ __global__ __launch_bounds__(256) void k_segment_slots(const PrepBatch B) {
 // order, and segbase[s] = toff(s) - t0 (so the pair of tile t is stb[segbase[s] + t]), or
 // SEG_NO_STB when the pairs would pass the capacity (that segment keeps the bisection).
 constexpr int32_t SEG_NO_STB = INT32_MIN;
-#ifndef EFD_STB
-#define EFD_STB 1   // 0: every segment takes the bisection (reference for the bitwise check)
-#endif
 __device__ __forceinline__ void segment_compact_body(const int2* __restrict__ slot_lh,
                                                          const int4* __restrict__ slot_info,
                                                          const int32_t* __restrict__ blockcnt,
@@ -1688,7 +1642,7 @@ __device__ __forceinline__ void segment_compact_body(const int2* __restrict__ sl
     if (valid) {
         seglh[pos] = lh;
         seginfo[pos] = info;
-        segbase[pos] = (EFD_STB && toff + ntl <= stbcap) ? (int32_t)(toff - lh.x / TILE_LANES)
+        segbase[pos] = (toff + ntl <= stbcap) ? (int32_t)(toff - lh.x / TILE_LANES)
                                                          : SEG_NO_STB;
     }
     if (blk == nblk - 1 && tid == 0) *nseg = base + wc[0] + wc[1] + wc[2] + wc[3];
@@ -1815,19 +1769,16 @@ __device__ __forceinline__ void sincos_big(double x, double& s, double& c) {
 // The reduction is one FMA against the leading 53 bits of the step: the dropped q * STEP_2 is
 // < 3.9e-17 |x|, below half an ulp of x itself (the rounding every phase already carries), and
 // one FMA less on the longest dependency chain of an evaluation (k_modesum +1.2-1.6%, the
-// spectrum moves by 8e-12 of max|S| at config 2; -DEFD_CW_TWO_PART restores the second term).
+// spectrum moves by 8e-12 of max|S| at config 2).
 constexpr int SCTAB = 512;
-// EFD_COS_MM: the cosine on |r| <= pi/512 as COS_A - z/2 (z = r^2) with the constant chosen
+// The cosine on |r| <= pi/512 as COS_A - z/2 (z = r^2) with the constant chosen
 // minimax (max error 2.95e-11 = half the dropped z^2/24 at r = pi/512; mpmath), one FMA instead
 // of the r^4 Taylor form's two. 2.95e-11 of a term is far below the ~1e-9 rad rounding every
 // term's phase already carries (phases reach 1e7 rad). The slope stays -0.5 (an inline
 // constant: the free minimax slope, 7.4e-12, cost an SGPR pair and VGPR moves in the record
 // loop). COS_A is the constant callers pass as c0 (J <= 2 records fold rho - 1 into it:
 // fma(-v, v, COS_A) = COS_A rho to 2e-20).
-#ifndef EFD_COS_MM
-#define EFD_COS_MM 1
-#endif
-constexpr double COS_A = EFD_COS_MM ? 1.000000000029531 : 1.0;
+constexpr double COS_A = 1.000000000029531;
 constexpr double COS_B = -0.5;
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
                                            double& s, double& c, double extra = 0.0,
@@ -1835,18 +1786,12 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
                                            double c0 = COS_A) {
     constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
     constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
-    constexpr double STEP_2 = 4.7837765591693483e-19;    // pi/256 - STEP_1
     // q = nearest integer to x / step via the 1.5 * 2^52 shifter: its low word is q itself
     // (two's complement), so neither rint nor a float->int conversion is needed
     constexpr double SHIFTER = 6755399441055744.0;
     const double qs = fma(x, INV_STEP, SHIFTER);
     const double q = qs - SHIFTER;
     double r = fma(-q, STEP_1, x);
-#ifdef EFD_CW_TWO_PART
-    r = fma(-q, STEP_2, r);
-#else
-    (void)STEP_2;
-#endif
     // a small angle (|extra_scale * extra| < 1e-3) added after the reduction
     if (use_extra) r = fma(extra_scale, extra, r);
     const int qi = __double2loint(qs);
@@ -1854,48 +1799,27 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
     const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
     const double2 t = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
     const double z = r * r;
-#ifdef EFD_SIN_R5
-    const double sr = fma(r * z, fma(z, 8.333333333333333e-03, -1.6666666666666666e-01), r);
-#else
     const double sr = fma(r * z, -1.6666666666666666e-01, r);
-#endif
     // c0: the cosine polynomial's constant term (1, or a factor 1 + O(1e-9) folded in by the
-    // caller: rho (1 + d) E to within |d| |sr| < 3e-12, see EFD_EARLY_MASK)
-#if EFD_COS_MM
+    // caller: rho (1 + d) E to within |d| |sr| < 3e-12, see spa_fast_m)
     const double cr = fma(z, COS_B, c0);
-#else
-    const double cr = fma(z, fma(z, 4.1666666666666664e-02, -0.5), c0);
-#endif
     s = fma(t.x, cr, t.y * sr);
     c = fma(t.y, cr, -t.x * sr);
 }
 
-// 1/sqrt(x) for finite x > 0: the hardware estimate plus one Newton (second-order) correction,
-// relative error ~1e-15 (the OCML sequence's third-order step costs one more FP64 operation for
-// the last bits; the SPA amplitude needs no more). The callers mask x <= 0.
-__device__ __forceinline__ double rsqrt_pos(double x) {
-    const double y = __builtin_amdgcn_rsq(x);
-    const double e = fma(-x * y, y, 1.0);
-    return fma(y * e, 0.5, y);
-}
-
-// The same inside k_modesum with the halving on the FMA's output modifier (EFD_OMOD): e/2 comes
-// straight out of v_fma_f64 ... div:2, one FP64 operation fewer. The output modifiers apply only
-// with IEEE mode off and FP64 denormals flushed (tools/rsq_omod_check.hip: otherwise the
-// modifier is silently ignored), which modesum_tile sets in the MODE register; the compiler never
-// emits them itself in IEEE mode, hence the inline asm. Only for k_modesum's mode.
-#ifndef EFD_OMOD
-#define EFD_OMOD 1
-#endif
+// 1/sqrt(x) for finite x > 0 inside k_modesum: the hardware estimate plus one Newton
+// (second-order) correction, relative error ~1e-15 (the OCML sequence's third-order step costs
+// one more FP64 operation for the last bits; the SPA amplitude needs no more; callers mask
+// x <= 0), with the halving on the FMA's output modifier: e/2 comes straight out of
+// v_fma_f64 ... div:2, one FP64 operation fewer. The output modifiers apply only with IEEE mode
+// off and FP64 denormals flushed (tools/rsq_omod_check.hip: otherwise the modifier is silently
+// ignored), which modesum_tile sets in the MODE register; the compiler never emits them itself in
+// IEEE mode, hence the inline asm. Only for k_modesum's mode.
 __device__ __forceinline__ double rsqrt_pos_sum(double x) {
-#if EFD_OMOD
     const double y = __builtin_amdgcn_rsq(x);
     double h;
     asm("v_fma_f64 %0, -%1, %2, 1.0 div:2" : "=v"(h) : "v"(x * y), "v"(y));
     return fma(y, h, y);
-#else
-    return rsqrt_pos(x);
-#endif
 }
 
 // Q factor. The mirror-convention term of one branch is A Y Q e^{i(2 pi g t - Phi)} with
@@ -2057,178 +1981,31 @@ __device__ __forceinline__ double cubic(const double* __restrict__ c, double w) 
     return fma(fma(fma(c[0], w, c[1]), w, c[2]), w, c[3]);
 }
 
-// The same factor in polar form, G = rho e^{i theta} (fast path, EFD_POLAR): log G of the
-// Hankel series, re-expanded as rho = sum_j RH_j u^j and theta = w sum_j TH_j u^j (y > 0; theta
-// is odd in y), u = w^2, TH = {-0.069444444444444444444, 0.035525977366255144033,
-// -0.11095169967421124829, 0.85188445191064930488}. The first omitted terms fall below 1e-17 at
-// the same |y| bounds as KB / KC (JSER_Y), so a record's series length J serves both forms.
-// theta is added to the reduced sin/cos argument (|r| <= pi/512, where it costs no rounding) and
-// rho scales the amplitude: two FP64 operations fewer per evaluation than rotating by (R + iI).
-#ifndef EFD_POLAR
-#define EFD_POLAR 1
-#endif
-// Runtime series length J as increments on the 2-term form, which every record evaluates (81% of
-// records need J = 2; for J = 1 the second terms fall below the rounding of the first): a
-// switch over J-term Horner chains merged its results through 64-bit register copies (2 VALU
-// per evaluation, each as costly as an FMA), the increments accumulate in place. theta comes
-// out in units of its leading coefficient (thn = theta / TH_0), so both chains start from the
-// inline constant 1.0 and the caller's add of theta to the reduced angle becomes an FMA with
-// TH_0: one VALU operation fewer per evaluation than the TH-form chain.
+// The fast path's K_{1/3} factor in polar form, G = rho e^{i theta}: log G of the Hankel series,
+// re-expanded as rho = sum_j RH_j u^j and theta = w sum_j TH_j u^j (y > 0; theta is odd in y),
+// u = w^2, TH = {-0.069444444444444444444, 0.035525977366255144033, -0.11095169967421124829,
+// 0.85188445191064930488}. The first omitted terms fall below 1e-17 at the same |y| bounds as
+// KB / KC (JSER_Y), so a record's series length J serves both forms. theta is added to the
+// reduced sin/cos argument (|r| <= pi/512, where it costs no rounding) and rho scales the
+// amplitude: two FP64 operations fewer per evaluation than rotating by (R + iI). theta comes out
+// in units of its leading coefficient (thn = theta / TH_0), so the add of theta to the reduced
+// angle is one FMA with TH_0 (with the sign of F' and the v rescaling: RecSign::kth).
+//   - Records of series length 3 take the fourth terms too (below 1e-17 on their intervals, by the
+//     choice of J), so J = 3 and J = 4 share one real branch (the compiler otherwise if-converts
+//     the J >= 4 increments and merges the results with 4 v_cndmask per evaluation).
+//   - theta is an angle added to phases that reach 1e7 rad and carry ~1e-9 rad of rounding, so
+//     its series stops at terms below 1e-13 rad instead of the 1e-17 (relative) that picks J for
+//     rho, an amplitude factor: for J <= 2 records (|y| >= 8.7e3, 82% of records) the KTHN1 term
+//     is at most 0.0694 * 0.512 |w|^3 = 5.4e-14 rad and theta = TH_0 w; for J >= 3 the KTHN3
+//     term is at most 4.2e-16 rad (|y| >= 153).
 constexpr double KTH0 = -0.069444444444444444444;   // TH_0
-// EFD_J34: records of series length 3 take the fourth terms too (below 1e-17 on their
-// intervals, by the choice of J), so J = 3 and J = 4 share one branch: the compiler otherwise
-// if-converts the J >= 4 increments and merges the two results with 4 v_cndmask per evaluation.
-#ifndef EFD_J34
-#define EFD_J34 1
-#endif
-// EFD_THETA_TRUNC: theta is an angle added to phases that reach 1e7 rad and carry ~1e-9 rad of
-// rounding, so its series stops at terms below 1e-13 rad instead of the 1e-17 (relative) that
-// picks J for rho, an amplitude factor: for J <= 2 records (|y| >= 8.7e3, 82% of records) the
-// KTHN1 term is at most 0.0694 * 0.512 |w|^3 = 5.4e-14 rad and theta = TH_0 w; for J >= 3 the
-// KTHN3 term is at most 4.2e-16 rad (|y| >= 153). Two FP64 operations fewer per J <= 2
-// evaluation; rho keeps every term J asks for.
-#ifndef EFD_THETA_TRUNC
-#define EFD_THETA_TRUNC 1
-#endif
-__device__ __forceinline__ void kpolar_rt(int J, double ww, double& rho, double& thn) {
-    static_assert(FAST_J == 4, "kpolar_rt: increments up to 4 terms");
-    const double uu = ww * ww;
-    double r = fma(KRH[1], uu, 1.0);   // KRH[0] == 1
-#if EFD_THETA_TRUNC
-    static_assert(EFD_J34, "theta truncation assumes the shared J >= 3 branch");
-    thn = ww;
-    if (J >= 3) {   // wave-uniform; a real branch (see EFD_J34)
-        asm volatile("");
-        const double u2 = uu * uu;
-        r = fma(KRH[2], u2, r);
-        r = fma(KRH[3], u2 * uu, r);
-        const double t = fma(KTHN[2], u2, fma(KTHN[1], uu, 1.0));
-        thn = ww * t;
-    }
-    rho = r;
-#else
-    double t = fma(KTHN[1], uu, 1.0);
-    if (J >= 3) {   // wave-uniform
-#if EFD_J34
-        // a real branch: without it the compiler computes the 4-term form for every record and
-        // selects (6 FP64 operations + 4 v_cndmask per evaluation for the 82% of J <= 2)
-        asm volatile("");
-#endif
-        const double u2 = uu * uu;
-        r = fma(KRH[2], u2, r);
-        t = fma(KTHN[2], u2, t);
-        if (EFD_J34 || J >= 4) {
-            const double u3 = u2 * uu;
-            r = fma(KRH[3], u3, r);
-            t = fma(KTHN[3], u3, t);
-        }
-    }
-    rho = r;
-    thn = ww * t;
-#endif
-}
 
-// K_{1/3} series with a wave-uniform runtime length J (1..FAST_J): the branches are scalar, and
-// only R, I merge after them.
-__device__ __forceinline__ void kseries_rt(int J, double ww, double& R, double& I) {
-    switch (J) {
-        case 1: kseries<1>(ww, R, I); break;
-        case 2: kseries<2>(ww, R, I); break;
-        case 3: kseries<3>(ww, R, I); break;
-        default: kseries<FAST_J>(ww, R, I); break;
-    }
-}
-
-// Branch-free SPA evaluation of interval record `it` at the lane's bin: returns the
-// group-independent factor
-//   W = Q e^{i(2 pi g t - Phi)}   (Q-factor notes above; arg Q_spa folded into the phase)
-// and w = t - t_j for the amplitude cubics, for lanes with `act` set. need_general is set for
-// active lanes the general path must redo (t(g) overshot the record's knot interval, F' = 0, or
-// |y| < FAST_Y in the uniform mode); W is 0 for those and for inactive lanes. Everything is
-// computed unconditionally and masked once (selects, no divergent branches). The sub-branch
-// (g = -f or +f) and the series length are wave-uniform runtime values: sfk, stfk are g = +-fk,
-// 2 pi g (the tile keeps them signed for the current sub-branch), J the record's series length.
-// One body for every (sub-branch, J): round 1's 2 x 4 compiled copies merged the accumulators
-// through 8 v_mov_b64 per record and took 8x the code, for bitwise the same result.
-template <int CAUSTIC>
-__device__ __forceinline__ void spa_fast_rt(const Item* __restrict__ it, double sfk, double stfk,
-                                            int J, bool act, const double2* __restrict__ sct,
-                                            double& wr, double& wi, double& w, bool& need_general) {
-    const double u = sfk - it->gx;
-    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
-    w = tt - it->tj;
-    bool good = (unsigned long long)__double_as_longlong(w) <
-                (unsigned long long)__double_as_longlong(it->dtj);
-    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
-    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
-    const double afd = fabs(fd);
-    good = good & (afd > 0.0);
-#if EFD_POLAR
-    // F' = 0 gives amp = inf here; every quantity it reaches is selected away below (selects,
-    // not multiplications by a zero mask), so no NaN reaches the sums
-    const double amp = CAUSTIC == EFD_CAUSTIC_UNIFORM ? rsqrt_pos(afd)
-                                                      : (afd > 0.0 ? rsqrt_pos(afd) : 0.0);
-#else
-    const double amp = afd > 0.0 ? rsqrt_pos(afd) : 0.0;
-#endif
-    const double psi0 = fma(stfk, tt, -ph);
-    const int shift = fd > 0.0 ? 192 : -192;
-    double R = 1.0, I = 0.0;
-#if EFD_POLAR
-    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
-        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
-        const double a3 = amp * amp * amp;
-        const double t3 = fdds * a3;
-        const double ww = t3 * t3;   // 1/|y|
-        good = good & ((J < FAST_J) | (ww <= 1.0 / FAST_Y));
-        double rho, thn;
-        kpolar_rt(J, ww, rho, thn);
-        // theta is odd in y: the sign of F' (= sign of y) onto it by one XOR of the high word
-        const bool ok = act & good;
-        const double ths = ok ? __hiloint2double(__double2hiint(thn) ^ (__double2hiint(fd) & INT32_MIN),
-                                                 __double2loint(thn))
-                              : 0.0;
-        const double am = ok ? amp * rho : 0.0;
-        double sn, cs;
-        sincos_tab(psi0, shift, sct, sn, cs, ths, true, KTH0);   // theta = KTH0 * thn
-        wr = am * cs;
-        wi = am * sn;
-        need_general = act & !good;
-        return;
-    }
-#else
-    if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
-        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
-        const double a3 = amp * amp * amp;
-        const double t3 = fdds * a3;
-        // |w|; the sign of F' (w's sign) goes into I through the mask select below, where it
-        // costs one v_bfi instead of a copysign of its own (bitwise the same I: the rounding of
-        // a product is symmetric in sign)
-        const double ww = t3 * t3;
-        good = good & ((J < FAST_J) | (ww <= 1.0 / FAST_Y));
-        kseries_rt(J, ww, R, I);
-    }
-#endif
-    const double as = (act & good) ? copysign(amp, fd) : 0.0;
-    R *= fabs(as);
-    I *= CAUSTIC == EFD_CAUSTIC_UNIFORM ? as : fabs(as);
-    double sn, cs;
-    sincos_tab(psi0, shift, sct, sn, cs);
-    wr = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, cs, -I * sn) : R * cs;
-    wi = CAUSTIC == EFD_CAUSTIC_UNIFORM ? fma(R, sn, I * cs) : R * sn;
-    need_general = act & !good;
-}
-
-// Lane predicates as wave masks in scalar registers (EFD_SALU_MASKS): every VALU instruction
-// issues in 4 cycles per wave64, an FP64 FMA's cost, so the per-lane booleans of spa_fast_rt
-// (lane range: 2 integer compares per bin; the |y| test of a series-length-4 record, evaluated for
-// every record; the any-lane test of the general path: a select and a compare per record) are
-// replaced by masks: the lane range from the record's bounds in SALU (lane_range_mask), each
-// comparison's result taken by ballot (the compare itself writes the mask), the |y| test only
-// in a wave-uniform branch for records that need it, and the masks combined in SALU.
-#ifndef EFD_SALU_MASKS
-#define EFD_SALU_MASKS 1
-#endif
+// Lane predicates as wave masks in scalar registers: every VALU instruction issues in 4 cycles
+// per wave64, an FP64 FMA's cost, so the fast path's per-lane booleans (lane range: 2 integer
+// compares per bin; the |y| test of a series-length-4 record; the any-lane test of the general
+// path) are masks: the lane range from the record's bounds in SALU (lane_range_mask), each
+// comparison's result taken by ballot (the compare itself writes the mask), the |y| test only in
+// a wave-uniform branch for records that need it, and the masks combined in SALU.
 // lanes l of the wave with lo <= l < hi (wave-uniform bounds, any range). Selects, not a clamp:
 // min/max of a uniform value becomes v_med3 + v_readfirstlane (2 VALU), the selects stay SALU.
 __device__ __forceinline__ uint64_t lanes_below(int32_t x) {
@@ -2238,30 +2015,25 @@ __device__ __forceinline__ uint64_t lanes_below(int32_t x) {
 __device__ __forceinline__ uint64_t lane_range_mask(int32_t lo, int32_t hi) {
     return lanes_below(hi) & ~lanes_below(lo);
 }
-// spa_fast_rt with the active lanes given as a mask and the general-path lanes returned as one;
-// the same arithmetic (bitwise the same W and w). EFD_REC_SIGN: the sign of F' is the record's
-// (Item::fdneg, wave-uniform), so the table shift and the angle's sign are scalar values: one
-// v_cmp_class (F' of the record's sign, nonzero) replaces the |F'| > 0 compare, and the per-lane
-// sign compare, shift select and copysign go (lanes whose F' has the other sign, at turning
-// points, take the general path). The class test is inline asm: the builtin's boolean is turned
-// into a VGPR and compared back (2 VALU) before a ballot.
-#ifndef EFD_REC_SIGN
-#define EFD_REC_SIGN 1
-#endif
+// The sign of F' is the record's (Item::fdneg, wave-uniform), so the table shift and the angle's
+// sign are scalar values: one v_cmp_class (F' of the record's sign, nonzero) replaces an |F'| > 0
+// compare, a per-lane sign compare, a shift select and a copysign (lanes whose F' has the other
+// sign, at turning points, take the general path). The class test is inline asm: the builtin's
+// boolean is turned into a VGPR and compared back (2 VALU) before a ballot.
 struct RecSign {
     int32_t fdcls;   // v_cmp_class mask: F' normal or subnormal of the record's sign
     int32_t shift;   // sign(F') 3 pi / 4 in table steps
     double kth;      // theta = kth * min(|thn|, 1): KTH0 with the sign of F'
-    bool safe;       // every lane passes the interval and sign tests (EFD_SAFE_REC)
+    bool safe;       // every lane passes the interval and sign tests (record_safe)
 };
 // bits: Item::fdneg (bit 0: F' < 0, bit 1: safe record)
 __device__ __forceinline__ RecSign rec_sign(uint32_t bits) {
     const bool fdneg = bits & 1u;
     RecSign r;
-    r.safe = EFD_SAFE_REC && (bits & 2u);
+    r.safe = (bits & 2u) != 0;
     r.fdcls = fdneg ? 0x018 : 0x180;
     r.shift = fdneg ? -192 : 192;
-    r.kth = EFD_VSCALE ? (fdneg ? -KTH0 / VS : KTH0 / VS) : (fdneg ? -KTH0 : KTH0);
+    r.kth = fdneg ? -KTH0 / VS : KTH0 / VS;
     return r;
 }
 // lanes where v_cmp_class_f64(x, cls) holds, as a wave mask
@@ -2270,40 +2042,25 @@ __device__ __forceinline__ uint64_t class_mask(double x, int32_t cls) {
     asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(m) : "v"(x), "s"(cls));
     return m;
 }
-// Masking the fast path's amplitude (EFD_FTZ_SELECT): k_modesum runs with FP64 denormals
+// Masking the fast path's amplitude: k_modesum runs with FP64 denormals
 // flushed (modesum_tile sets the MODE register; no value of the sum comes near 1e-308), so
 // clearing the high word alone turns any amp -- inf and NaN included -- into a denormal that
 // every later FP64 operation reads as +0: one v_cndmask_b32 instead of two for the 64-bit
 // select, with bitwise the same W (+0 either way).
-#ifndef EFD_FTZ_SELECT
-#define EFD_FTZ_SELECT 1
-#endif
 __device__ __forceinline__ double ftz_select(bool ok, double v) {
-#if EFD_FTZ_SELECT
     return __hiloint2double(ok ? __double2hiint(v) : 0, __double2loint(v));
-#else
-    return ok ? v : 0.0;
-#endif
 }
-#ifndef EFD_EARLY_MASK
-#define EFD_EARLY_MASK 1
-#endif
-#if EFD_VSCALE && !(EFD_EARLY_MASK && EFD_SALU_MASKS && EFD_REC_SIGN)
-#error "EFD_VSCALE: the early-mask, SALU-mask, record-sign fast path only"
-#endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            int J, uint64_t actm, const double2* __restrict__ sct,
                                            const RecSign& rs, double& wr, double& wi, double& w,
                                            uint64_t& needm) {
-    static_assert(EFD_POLAR, "mask form of the polar fast path");
     const double u = sfk - it->gx;
     const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
     w = tt - it->tj;
     const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
-#if EFD_REC_SIGN
     uint64_t goodm = ~0ull;
     if (!rs.safe) {   // wave-uniform: a record k_items could not certify tests every lane
         asm volatile("");
@@ -2311,20 +2068,12 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
                                             (unsigned long long)__double_as_longlong(it->dtj)) &
                 class_mask(fd, rs.fdcls);
     }
-#else
-    uint64_t goodm = __builtin_amdgcn_ballot_w64((unsigned long long)__double_as_longlong(w) <
-                                                 (unsigned long long)__double_as_longlong(it->dtj));
-    goodm &= __builtin_amdgcn_ballot_w64(afd > 0.0);
-    const int shift = fd > 0.0 ? 192 : -192;
-#endif
     // F' = 0 gives amp = NaN here; every quantity it reaches is selected away below
     const double amp = rsqrt_pos_sum(afd);
     const double psi0 = fma(stfk, tt, -ph);
     double sn, cs;
     if (CAUSTIC == EFD_CAUSTIC_UNIFORM) {
-#if EFD_EARLY_MASK
-        static_assert(EFD_REC_SIGN && EFD_FTZ_SELECT && EFD_THETA_TRUNC && FAST_J == 4,
-                      "early mask: record sign, flushed denormals, truncated theta");
+        static_assert(FAST_J == 4, "early mask: the J >= 3 branch covers J = 3 and 4");
         // The amplitude is masked before it enters 1/|y|: masked lanes get amp = +0 (inf and
         // NaN included), so w = 0, theta = 0 and rho = 1 there and the angle stays finite with no
         // clamp; for J <= 3 records every in-interval lane is within the series' range, so
@@ -2339,14 +2088,13 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         const double t3 = fdds * a3;
         double ww = t3 * t3;   // 1/|y|
         double am, c0, thn;
-        if (J >= 3) {   // wave-uniform; a real branch (see EFD_J34)
+        if (J >= 3) {   // wave-uniform; a real branch (see KTH0's notes)
             asm volatile("");
             // the |y| >= FAST_Y test only matters for J = 4 (J = 3 lanes pass it by their
             // record's bound), but a nested J test's condition crossed the join as a per-lane
             // boolean (v_cndmask + v_cmp for every record)
             // |w| <= 1/153: rho's KRH_3 term (< 2.2e-14) and theta's KTHN_2 term (< 1.3e-12 rad)
             // are below the accuracy of the rest of the evaluation
-#if EFD_VSCALE
             // ww = v = VS w: rho = 1 - v^2 + (KRH_2 / KRH_1^2) v^4, theta / (TH_0 / VS) =
             // v (1 + (KTHN_1 / |KRH_1|) v^2)
             // lanes past the series' range get w = +0 (high word cleared, flushed): finite
@@ -2357,74 +2105,39 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
             const double uu = ww * ww;
             const double r = fma(45.7, uu * uu, 1.0 - uu);
             thn = ww * fma(-14.733333333333333333, uu, 1.0);
-#else
-            goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
-            ww = fmin(ww, 1.0);
-            const double uu = ww * ww;
-            const double r = fma(KRH[2], uu * uu, fma(KRH[1], uu, 1.0));
-            thn = ww * fma(KTHN[1], uu, 1.0);
-#endif
             am = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm & goodm), ampm * r);
             c0 = COS_A;
         } else {
-#if EFD_VSCALE
             c0 = fma(-ww, ww, COS_A);   // (1 + KRH_1 w^2) COS_A = (1 - v^2) COS_A
-#else
-            c0 = fma(KRH[1], ww * ww, 1.0);
-#endif
             thn = ww;
             am = ampm;
         }
         sincos_tab(psi0, rs.shift, sct, sn, cs, thn, true, rs.kth, c0);
         wr = am * cs;
         wi = am * sn;
-#else
-        const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
-        const double a3 = amp * amp * amp;
-        const double t3 = fdds * a3;
-        const double ww = t3 * t3;   // 1/|y|
-        // J < FAST_J: the record's |y| bound covers every in-interval lane
-        if (J >= FAST_J) goodm &= __builtin_amdgcn_ballot_w64(ww <= 1.0 / FAST_Y);
-        double rho, thn;
-        kpolar_rt(J, ww, rho, thn);
-        const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
-        // theta is odd in y and thn > 0 where ok: the sign of F' (= sign of y) by a copysign.
-        // Not masked: where ok, 0 < thn < 1/153; elsewhere min(|thn|, 1) keeps the angle finite
-        // (a NaN thn becomes 1; far outside the series' range thn is large of either sign), so
-        // sin/cos stay finite and the zero amplitude below zeroes W. |.| is a source modifier.
-#if EFD_REC_SIGN
-        const double am = ftz_select(ok, amp * rho);
-        sincos_tab(psi0, rs.shift, sct, sn, cs, fmin(fabs(thn), 1.0), true, rs.kth);
-#else
-        const double ths = copysign(fmin(fabs(thn), 1.0), fd);
-        const double am = ok ? amp * rho : 0.0;
-        sincos_tab(psi0, shift, sct, sn, cs, ths, true, KTH0);   // theta = KTH0 * thn
-#endif
-        wr = am * cs;
-        wi = am * sn;
-#endif
     } else {
         const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
         const double am = ftz_select(ok, amp);
-#if EFD_REC_SIGN
         sincos_tab(psi0, rs.shift, sct, sn, cs);
-#else
-        sincos_tab(psi0, shift, sct, sn, cs);
-#endif
         wr = am * cs;
         wi = am * sn;
     }
     needm = actm & ~goodm;
 }
 
-#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
+#ifdef EFD_EXP
 // record evals, cold-path evals, cold lanes, skips; cold lanes by cause: overshoot, 18.4 <= |y| <
 // FAST_Y, |y| < 18.4
-__device__ unsigned long long g_exp_count[32];  // [8..15]: |y| bands of kfactor_slow's J;
+// Experiment build (-DEFD_EXP, tools/exp_variants.py): counters and per-tile clocks. Never in the
+// product library (tests/test_abi.py checks that efd_exp_* is not exported).
+constexpr int EXP_NCOUNT = 40;
+__device__ unsigned long long g_exp_count[EXP_NCOUNT];  // [8..15]: |y| bands of kfactor_slow's J;
 // [16, 17]: cold wave evaluations / lanes (one-body kernel); [18..23]: overshoot bands of
 // max(-w, w - dtj) / dtj: < 1e-12, 1e-9, 1e-6, 1e-3, 1e-1, larger; [24, 25, 26]: chunk barrier
 // balance: sum over chunks of the busiest wave's record evaluations, of all waves' evaluations,
-// and the number of chunks
+// and the number of chunks; [27, 28]: segment table size, hits per tile summed (k_tile_keys);
+// [29]: wave-records of certified-safe records; [32..35]: wave-records by series length J = 1..4,
+// [36]: sub-branch flips
 __device__ unsigned int g_exp_tile[16384];       // record evaluations per tile (first 16384)
 __device__ unsigned long long g_exp_tclk[16384];  // wall clock (s_memrealtime) per tile
 #endif
@@ -2448,19 +2161,14 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
     double ph, fd, fdd;
     ColdEval c;
     const double wl = tt - it->tj;
-#ifdef EFD_EXP_COLD_NOFWD   // timing experiment: no generic forward evaluation
-    if (true) {
-        const double w = fmin(fmax(wl, 0.0), it->dtj);
-#else
     if (wl >= 0.0 && wl < it->dtj) {
         const double w = wl;
-#endif
         for (int q = 0; q < 4; ++q) c.b[q] = cubic(it->b[q >> 1][q & 1], w);
         ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
         fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
         fdd = INV_FDD_SCALE * fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
     } else {  // t(g) overshot the record's knot interval: evaluate like scipy
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
         atomicAdd(&g_exp_count[4], 1ull);
         {
             const double ov = fmax(-wl, wl - it->dtj) / it->dtj;
@@ -2483,7 +2191,7 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
         if (fabs(ww) * FAST_Y <= 1.0) {
             kseries_fast(ww, R, I);
         } else {
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
             atomicAdd(&g_exp_count[fabs(ww) * 18.4 <= 1.0 ? 5 : 6], 1ull);
             {
                 const double ay = 1.0 / fabs(ww);
@@ -2492,9 +2200,7 @@ __device__ __noinline__ ColdEval spa_general(const Item* __restrict__ it, double
                 atomicAdd(&g_exp_count[band], 1ull);
             }
 #endif
-#ifndef EFD_EXP_COLD_NOKF   // timing experiment: no slow K_{1/3} factor
             kfactor_slow(fd, fdd, R, I);
-#endif
         }
     }
     double sn, cs;
@@ -2525,7 +2231,7 @@ __device__ __forceinline__ void accumulate(double wr, double wi, double xr, doub
 }
 
 // One 16-B LDS-DMA piece per lane: global src (per lane) -> LDS dst (wave-uniform base + 16 B x
-// lane). Issued through inline asm (EFD_DMA_ASM): the compiler's waitcnt pass treats the
+// lane). Issued through inline asm: the compiler's waitcnt pass treats the
 // intrinsic's LDS write as possibly aliasing later ds_reads, so each wave waited for its prefetch
 // of the next stage at the first record of every chunk (s_waitcnt vmcnt at the loop head). Hidden
 // from that pass, the DMA is retired only by the explicit vmcnt(0) before each chunk barrier and
@@ -2534,23 +2240,15 @@ __device__ __forceinline__ void accumulate(double wr, double wi, double xr, doub
 // the same idea as neutral (1.148 vs 1.14 ms) while the cold block's reloads still kept a vmcnt
 // wait at the loop head. M0 (the DMA's LDS base) is set inside the asm: the k_modesum instances
 // have no other M0 user (checked in their ISA), hence the local -Winline-asm silence.
-#ifndef EFD_DMA_ASM
-#define EFD_DMA_ASM 1
-#endif
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void glds16(const uint4* src, uint4* dst) {
-#if EFD_DMA_ASM
     const uint32_t base = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(dst));
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :
                  : "v"(src), "s"(base)
                  : "memory", "m0");
-#else
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
-                                     (__attribute__((address_space(3))) void*)(dst), 16, 0, 0);
-#endif
 }
 #pragma clang diagnostic pop
 
@@ -2572,19 +2270,11 @@ template <bool PAIRED, int CAUSTIC, int BPL>
 // 37.6 KB of LDS per workgroup 4 workgroups fit a CU, and the fourth wave hides more FP64
 // latency than the spills cost (config 2: 1.00 ms against 1.09 ms at 3 waves / 147 VGPRs;
 // 5 waves with a one-round stage: 1.07 ms)
-#ifndef EFD_WAVES_PER_EU
 #define EFD_WAVES_PER_EU 4
-#endif
 // 1: the tiles' record lists are built by k_tile_keys in the preparation phase and DMA'd in by
 // the sum; tiles whose list needs more than one KEYCAP pass or has more than TK_HITS segments
 // (tcnt = -1) build it in the sum as before. 0: always in the sum.
-#ifndef EFD_PREBUILT_LISTS
-#define EFD_PREBUILT_LISTS 1
-#endif
 // sum dispatch order from k_tile_order: 0 = fixed (f = 0 outward), 1 = tiles longest first
-#ifndef EFD_COST_ORDER
-#define EFD_COST_ORDER 1
-#endif
 __device__ __forceinline__ void modesum_tile(
     const Item* __restrict__ items, const int4* __restrict__ ranges,
     const int2* __restrict__ seglh, const int4* __restrict__ seginfo,
@@ -2612,7 +2302,7 @@ __device__ __forceinline__ void modesum_tile(
     __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
     __shared__ int wcnt[(SEGWIN / TILE) * NWAVE];
     __shared__ double2 sctab[SCTAB];   // (sin, cos)(k pi/128) for sincos_tab
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
     __shared__ int wimb[2][NWAVE];     // records each wave evaluated in a chunk (barrier balance)
 #endif
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
@@ -2644,20 +2334,15 @@ __device__ __forceinline__ void modesum_tile(
         tile = ngrid - 1 - lin;
         if (tile >= ntiles) return;
     }
-#ifdef EFD_EXP_TCLK
+#ifdef EFD_EXP
     const unsigned long long t_start = wall_clock64();
 #endif
-#if EFD_FTZ_SELECT
     // MODE.FP_DENORM[3:2] (FP64/FP16) = 0: flush denormal inputs and outputs (ftz_select). The
     // mode is per wave and set from the kernel descriptor at every wave launch.
     __builtin_amdgcn_s_setreg(1 | (6 << 6) | (1 << 11), 0);   // hwreg(HW_REG_MODE, 6, 2)
-#endif
-#if EFD_OMOD
     // MODE.IEEE = 0 (rsqrt_pos_sum's output modifier). Nothing here depends on IEEE mode's NaN
     // rules: the one min (fmin(|thn|, 1)) sees quiet NaNs at most and returns 1 in either mode.
-    static_assert(EFD_FTZ_SELECT, "output modifiers need FP64 denormals flushed");
     __builtin_amdgcn_s_setreg(1 | (9 << 6), 0);               // hwreg(HW_REG_MODE, 9, 1)
-#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int ni = nt - 1;
@@ -2669,10 +2354,7 @@ __device__ __forceinline__ void modesum_tile(
     const int pre = tcnt != nullptr ? tcnt[tile] : -1;
     const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
     // a tile outside the union of the segments' lane ranges has no record: no list to build
-#ifndef EFD_TILE_UNION
-#define EFD_TILE_UNION 1
-#endif
-    const int nseg = (EFD_TILE_UNION && pre < 0 && (hdr->lane_hi <= tlo || hdr->lane_lo >= thi))
+    const int nseg = (pre < 0 && (hdr->lane_hi <= tlo || hdr->lane_lo >= thi))
                          ? 0 : *nsegp;
     // a tile that can have records (a prebuilt list, or segments to search): block-uniform. Tiles
     // without read neither their frequencies nor the sin/cos table
@@ -2876,9 +2558,6 @@ __device__ __forceinline__ void modesum_tile(
             __syncthreads();
         }
         if (nkeys == 0) break;
-#ifdef EFD_EXP_NOEVAL
-        if (nkeys < 0x7fffffff) { own_r[0] += nkeys; nkeys = 0; continue; }
-#endif
 
         // ---- evaluate the nkeys records in chunks of NC through the double-buffered stage
         const int cnt = nkeys;
@@ -2914,7 +2593,7 @@ __device__ __forceinline__ void modesum_tile(
                 hdr = lo | (hi << HB) | ((uint32_t)sl << (2 * HB)) |
                       ((uint32_t)il->jser << (2 * HB + 1)) | ((uint32_t)il->fdneg << (2 * HB + 4));
             }
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
             int nev = 0;
             if (c > 0 && tid == 0) {
                 int mx = 0, sm = 0;
@@ -2931,12 +2610,12 @@ __device__ __forceinline__ void modesum_tile(
                 const int32_t khi = tlo + (int32_t)((ha >> HB) & HM);
                 const Item* it = stg + ii;
                 if (khi <= w_lo || klo >= w_hi) {              // misses this wave's chunk
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
                     if (lane == 0) atomicAdd(&g_exp_count[3], 1ull);
 #endif
                     continue;
                 }
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
                 ++nev;
                 if (lane == 0) {
                     atomicAdd(&g_exp_count[0], 1ull);
@@ -2948,11 +2627,10 @@ __device__ __forceinline__ void modesum_tile(
                 {
                     // one body: sub-branch sign (the register state above) and series length as
                     // wave-uniform values
-#ifdef EFD_EXP_JDIST   // records by series length [0..3], sub-branch flips [4], records [5]
+#ifdef EFD_EXP   // records by series length [32..35], sub-branch flips [36]
                     if (lane == 0) {
-                        atomicAdd(&g_exp_count[min((int)((ha >> (2 * HB + 1)) & 7u), 4) - 1], 1ull);
-                        atomicAdd(&g_exp_count[5], 1ull);
-                        if (s != s_cur) atomicAdd(&g_exp_count[4], 1ull);
+                        atomicAdd(&g_exp_count[31 + min((int)((ha >> (2 * HB + 1)) & 7u), 4)], 1ull);
+                        if (s != s_cur) atomicAdd(&g_exp_count[36], 1ull);
                     }
 #endif
                     if (s != s_cur) {
@@ -2965,19 +2643,14 @@ __device__ __forceinline__ void modesum_tile(
                         }
                         s_cur = s;
                     }
-#ifdef EFD_EXP_JFIX   // experiment: every record takes the FAST_J-term series (no J dispatch)
-                    const int J = FAST_J;
-#else
                     const int J = CAUSTIC == EFD_CAUSTIC_UNIFORM ? (int)((ha >> (2 * HB + 1)) & 7u) : FAST_J;
-#endif
                     // the stage holds b[s] at b[0] (EFD_GLDS swaps the halves for s = 1)
                     const double* xo = &it->b[0][0][0];
                     const double* xm = &it->b[1][0][0];
                     double wr[BPL], wi[BPL], w[BPL];
-#if EFD_SALU_MASKS
                     uint64_t needm[BPL], needany = 0;
                     const RecSign rs = rec_sign((ha >> (2 * HB + 4)) & 3u);
-#ifdef EFD_EXP_COUNT   // [29]: wave-records of certified-safe records
+#ifdef EFD_EXP   // [29]: wave-records of certified-safe records
                     if (lane == 0 && rs.safe) atomicAdd(&g_exp_count[29], 1ull);
 #endif
 #pragma unroll
@@ -2990,16 +2663,6 @@ __device__ __forceinline__ void modesum_tile(
                         needany |= needm[i];
                     }
                     anyneed = needany != 0;
-#else
-#pragma unroll
-                    for (int i = 0; i < BPL; ++i) {
-                        const int32_t k = w_lo + 64 * i + lane;
-                        const bool act = (k >= klo) & (k < khi);
-                        spa_fast_rt<CAUSTIC>(it, fk[i], tfk[i], J, act, sctab, wr[i], wi[i], w[i],
-                                             need[i]);
-                        anyneed = anyneed | need[i];
-                    }
-#endif
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
@@ -3008,15 +2671,8 @@ __device__ __forceinline__ void modesum_tile(
                         accumulate<0, PAIRED>(wr[i], wi[i], xr, xi, zr, zi, own_r[i], own_i[i],
                                               mir_r[i], mir_i[i]);
                     }
-#ifdef EFD_EXP_NOSLOW
-                    anyneed = false;
-#endif
-#if EFD_SALU_MASKS
                     if (__builtin_expect(anyneed, 0)) {   // cold: general path, some lanes
-#else
-                    if (__builtin_expect(__any(anyneed), 0)) {   // cold: general path, some lanes
-#endif
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
                         {
                             unsigned long long nl_ = 0;
 #pragma unroll
@@ -3040,15 +2696,13 @@ __device__ __forceinline__ void modesum_tile(
                                                       mir_i[i]);
                             }
                         }
-#if EFD_DMA_ASM
                         // the cold block's reloads retired here, so the loop head needs no
                         // vmcnt wait (which would also wait for the hidden LDS-DMA)
                         __builtin_amdgcn_s_waitcnt(0x0f70);
-#endif
                     }
                 }
             }
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
             if (lane == 0) wimb[c & 1][wave] = nev;
 #endif
             // retire this wave's LDS-DMA pieces, then the barrier publishes chunk c+1's stage
@@ -3143,7 +2797,7 @@ __device__ __forceinline__ void modesum_tile(
             llpart[tile] = t;
         }
     }
-#ifdef EFD_EXP_TCLK
+#ifdef EFD_EXP
     if (threadIdx.x == 0 && tile < 16384)
         g_exp_tclk[tile] = ((t_start & 0xffffffffull) << 32) | ((wall_clock64() - t_start) & 0xffffffffull);
 #endif
@@ -3168,12 +2822,7 @@ __device__ __forceinline__ void modesum_tile(
 
 // K8: the mode sum (one workgroup per tile; prebuilt lists when tcnt is given)
 template <bool PAIRED, int CAUSTIC, int BPL>
-#ifdef EFD_MODESUM_VGPRS   // experiment: a VGPR cap below 128 leaves room for other waves
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
-__attribute__((amdgpu_num_vgpr(EFD_MODESUM_VGPRS)))
-#else
-__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
-#endif
 void k_modesum(EFD_MODESUM_PARAMS) {
     modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, nullptr, nullptr, nullptr, nullptr,
                                        (int64_t)blockIdx.x);
@@ -3280,12 +2929,8 @@ __global__ __launch_bounds__(TILE) void k_ll_tile_const(const double* __restrict
                                                         double* __restrict__ llconst) {
     const int64_t tile = blockIdx.x;
     // modesum_tile's FP modes, so the epilogue's arithmetic rounds the same
-#if EFD_FTZ_SELECT
     __builtin_amdgcn_s_setreg(1 | (6 << 6) | (1 << 11), 0);
-#endif
-#if EFD_OMOD
     __builtin_amdgcn_s_setreg(1 | (9 << 6), 0);
-#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -3434,7 +3079,7 @@ __device__ __forceinline__ void tile_keys_body(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int32_t tlo = (int32_t)(tile * TILE_LANES), thi = tlo + TILE_LANES;
     const int nseg = *nsegp;
-#ifdef EFD_EXP_COUNT   // segment table size [27], hits per tile summed [28]
+#ifdef EFD_EXP   // segment table size [27], hits per tile summed [28]
     if (tile == 0 && tid == 0) atomicAdd(&g_exp_count[27], (unsigned long long)nseg);
 #endif
     // (1) the segments overlapping the tile, in table order
@@ -3466,7 +3111,7 @@ __device__ __forceinline__ void tile_keys_body(
         }
         __syncthreads();
     }
-#ifdef EFD_EXP_COUNT
+#ifdef EFD_EXP
     if (tid == 0) atomicAdd(&g_exp_count[28], (unsigned long long)nhit);
 #endif
     if (nhit > TK_HITS) {
@@ -3918,10 +3563,10 @@ extern "C" {
 
 int efd_version(void) { return EFD_VERSION; }
 
-#if defined(EFD_EXP_COUNT) || defined(EFD_EXP_TCLK) || defined(EFD_EXP_JDIST)
+#ifdef EFD_EXP
 int efd_exp_counters(unsigned long long* out) {
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * 32));
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_count), sizeof(unsigned long long) * EXP_NCOUNT));
     return EFD_OK;
 }
 int efd_exp_tiles(unsigned int* out, unsigned long long* clk) {
@@ -3986,28 +3631,26 @@ static int64_t resident_tile_slots() {
 // while config 2 (3,020 harmonics) keeps +0.2% (paired A/B, ratio 1.002, CI 1.001-1.003).
 // prepare and sum see the same arguments, so they agree on whether tperm exists.
 constexpr int32_t ORDER_MIN_K = 1024;
-// Prebuilt tile lists (k_tile_keys) from EFD_LISTS_MIN_K harmonics up; below, the sum builds
+// Prebuilt tile lists (k_tile_keys) from LISTS_MIN_K harmonics up; below, the sum builds
 // them itself (short lists: one window pass per tile). With tens of harmonics (eps = 1e-2) the
 // in-sum build is cheaper than k_tile_keys' pass over every tile in the batched likelihood:
 // config 4's walker groups (bench.py --likelihood, 3 interleaved pairs) 11,253 -> 13,416 logL/s;
 // configs 1 / 3 (tools/configs.py, 2 interleaved pairs) 2,938 vs 2,897 and 8,166 vs 7,996
 // waveforms/s (neutral), config 5 40,729 vs 39,648 (neutral); config 2 (3,020 harmonics) keeps
 // the prebuilt lists.
-#ifndef EFD_LISTS_MIN_K
-#define EFD_LISTS_MIN_K 1024
-#endif
-// (the environment variable EFD_LISTS_MIN_K, read once per process, overrides the build's value:
+constexpr int32_t LISTS_MIN_K = 1024;
+// (the environment variable EFD_LISTS_MIN_K, read once per process, overrides it:
 // a tuning knob; prepare and sum read the same value, so they agree on whether lists exist)
 static int32_t lists_min_k() {
     static const int32_t v = [] {
         const char* e = std::getenv("EFD_LISTS_MIN_K");
-        return e ? (int32_t)std::atoi(e) : (int32_t)EFD_LISTS_MIN_K;
+        return e ? (int32_t)std::atoi(e) : LISTS_MIN_K;
     }();
     return v;
 }
-static bool use_prebuilt(int32_t K) { return EFD_PREBUILT_LISTS && K >= lists_min_k(); }
+static bool use_prebuilt(int32_t K) { return K >= lists_min_k(); }
 static bool use_cost_order(const Layout& L, int32_t K) {
-    return use_prebuilt(K) && EFD_COST_ORDER && K >= ORDER_MIN_K &&
+    return use_prebuilt(K) && K >= ORDER_MIN_K &&
            L.ntiles > resident_tile_slots();
 }
 
@@ -4071,7 +3714,7 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         d.lists = use_prebuilt(ai->K) ? (use_cost_order(L, ai->K) ? 3 : 1) : 0;
         any_lists |= d.lists != 0;
         any_order |= d.lists == 3;
-        const bool pcr = EFD_PCR && ai->nt >= 4 && ai->nt <= PCR_NMAX;
+        const bool pcr = ai->nt >= 4 && ai->nt <= PCR_NMAX;
         d.pcr = pcr ? (ai->K < PCR_MAX_K ? 3 : 1) : 0;
         if (pcr) {
             any_pcr = true;
@@ -4094,16 +3737,8 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
     (void)nimax;
     hipStream_t st = (hipStream_t)stream;
     const unsigned nz = (unsigned)count;
-#ifdef EFD_EXP_SKIP   // diagnostic: after the warm-up, skip preparation kernels (bit mask: 1 groups,
-    // 2 k_prep, 4 k_items, 8 segment table, 16 k_tile_keys, 32 k_tile_order); valid only when
-    // every call repeats the same inputs on workspaces that already hold their results
-    static int exp_calls = 0;
-    const int skip = ++exp_calls > 16 ? EFD_EXP_SKIP : 0;
-#else
-    constexpr int skip = 0;
-#endif
     // K0: (m, n) groups and their amplitudes at the knots
-    if (!(skip & 1)) {
+    {
         hipLaunchKernelGGL(k_group_b, dim3(1, 1, nz), dim3(256), 0, st, B);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax + 255) / 256, ntmax, nz), dim3(256), 0, st,
@@ -4112,7 +3747,7 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
     }
     // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
     // grids sized for G = K, blocks past the device-side G return at once)
-    if (!(skip & 2)) {
+    {
         if (any_pcr) {   // one wave per interpolant, parallel cyclic reduction (prep_pcr_body)
             hipLaunchKernelGGL(k_prep_pcr_b, dim3(pcr_blocks, 1, nz), dim3(64),
                                sizeof(double) * 9 * ntmax_pcr, st, B);
@@ -4124,18 +3759,15 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
                                st, B);
             HIP_TRY(hipGetLastError());
         }
-#ifdef EFD_EXP_PREP_ROLE
-        return EFD_OK;   // timing experiment: the later stages would read partial data
-#endif
     }
     // K4: interval records
-    if (!(skip & 4)) {
+    {
         const int64_t blocks = (items_max + 255) / 256;
         hipLaunchKernelGGL(k_items, dim3((unsigned)blocks, 1, nz), dim3(256), 0, st, B);
         HIP_TRY(hipGetLastError());
     }
     // K5: segment table
-    if (!(skip & 8)) {
+    {
         const int nslot = Kmax * MAXRUNS * 2;
         const int nblk = (nslot + 255) / 256;
         hipLaunchKernelGGL(k_segment_slots, dim3(nblk, 1, nz), dim3(256), 0, st, B);
@@ -4146,21 +3778,17 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
                            0, st, B);
         HIP_TRY(hipGetLastError());
     }
-#if EFD_PREBUILT_LISTS
     // K6: the tiles' record lists (k_tile_keys): moves the latency-bound build out of the mode
     // sum into the preparation phase, which overlaps the previous waveform's sum in a two-stream
     // pipeline
-    if (!(skip & 16) && any_lists) {
+    if (any_lists) {
         hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)ntiles, 1, nz), dim3(TILE), 0, st, B);
         HIP_TRY(hipGetLastError());
     }
-#if EFD_COST_ORDER
-    if (!(skip & 32) && any_order) {
+    if (any_order) {
         hipLaunchKernelGGL(k_tile_order, dim3(1, 1, nz), dim3(1024), 0, st, B);
         HIP_TRY(hipGetLastError());
     }
-#endif
-#endif
     return EFD_OK;
 }
 
@@ -4254,12 +3882,7 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
 
 // efd_modesum_sum_batch, and efd_modesum_sum_loglike when d != NULL (paired grids: the tiles
 // write their likelihood partials, k_ll_final turns each waveform's into out[i])
-#ifndef EFD_SPARSE_SUM
-#define EFD_SPARSE_SUM 1
-#endif
-#ifndef EFD_SPARSE_WG
-#define EFD_SPARSE_WG 4096   // workgroups of a sparse launch, all waveforms
-#endif
+constexpr int64_t SPARSE_WG = 4096;   // workgroups of a sparse launch, all waveforms
 int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const* workspace,
                    const size_t* workspace_bytes, int32_t count, const double* d, const double* w,
                    double* llout, void* stream, const double* llconst = nullptr) {
@@ -4324,15 +3947,15 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
     // the sparse form (k_modesum_batch): the fused likelihood with tile constants, nothing
     // written, and in-kernel lists (below 1,024 harmonics: the sparse spectra; denser ones keep
     // the longest-first order over every tile)
-    bool sparse = EFD_SPARSE_SUM && d != nullptr && llconst != nullptr && a[0]->grid_symmetric;
+    bool sparse = d != nullptr && llconst != nullptr && a[0]->grid_symmetric;
     for (int i = 0; i < count && sparse; ++i)
         sparse = !a[i]->out && !a[i]->hp && !a[i]->hc && !use_prebuilt(a[i]->K) &&
                  !use_cost_order(make_layout(a[i]->nt, a[i]->K, a[i]->nf, 1), a[i]->K);
     const int64_t gq = 8 * XCD_GROUP;
     int64_t nper = 0;
     if (sparse) {
-        // workgroups per waveform: a multiple of 8 (one XCD place each), ~EFD_SPARSE_WG in all
-        const int64_t cap = std::max<int64_t>(64, (EFD_SPARSE_WG / count + 7) / 8 * 8);
+        // workgroups per waveform: a multiple of 8 (one XCD place each), ~SPARSE_WG in all
+        const int64_t cap = std::max<int64_t>(64, (SPARSE_WG / count + 7) / 8 * 8);
         nper = std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
     }
     const int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;

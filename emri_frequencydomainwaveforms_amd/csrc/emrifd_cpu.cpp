@@ -55,11 +55,8 @@ constexpr double VS = 0.18633899812498247470;             // sqrt|KRH_1|
 constexpr double FDD_SCALE = 0.29827892638794838654;      // sqrt(3/(2 pi)) |KRH_1|^(1/4)
 constexpr double INV_FDD_SCALE = 3.3525667136785156343;
 constexpr double KTH0 = -0.069444444444444444444;
-// the kernel's cosine on |r| <= pi/512 (emrifd.hip, EFD_COS_MM): minimax line in r^2, 7.4e-12
-#ifndef EFD_COS_MM
-#define EFD_COS_MM 1
-#endif
-constexpr double COS_A = EFD_COS_MM ? 1.000000000029531 : 1.0;
+// the kernel's cosine on |r| <= pi/512 (emrifd.hip, sincos_tab): minimax line in r^2
+constexpr double COS_A = 1.000000000029531;
 constexpr double COS_B = -0.5;
 constexpr double KTAB_WMIN = 0x1p-8, KTAB_WMAX = 0x1p10;
 
@@ -577,11 +574,7 @@ void spa_fast(const Rec& it, int s, const double* fk, int n, double* wr, double*
         const double ts = T.s[off], tc = T.c[off];
         const double z = r * r;
         const double sr = std::fma(r * z, -1.6666666666666666e-01, r);
-#if EFD_COS_MM
         const double cr = std::fma(z, COS_B, c0);
-#else
-        const double cr = std::fma(z, std::fma(z, 4.1666666666666664e-02, -0.5), c0);
-#endif
         const double sn = std::fma(ts, cr, tc * sr);
         const double cs = std::fma(tc, cr, -ts * sr);
         wr[i] = am * cs;

@@ -36,7 +36,7 @@ def test_library_exports_every_symbol():
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", nm, flags=re.M), name
     # and nothing undeclared: the shipped build exports exactly the header's efd_* functions
-    # (efd_exp_* diagnostics exist only in -DEFD_EXP_* experiment builds)
+    # (efd_exp_* diagnostics exist only in -DEFD_EXP experiment builds)
     exported = sorted(set(re.findall(r"\bT (efd_\w+)$", nm, flags=re.M)))
     assert exported == declared_functions()
 

@@ -6,7 +6,7 @@
 `build` writes exp/libemrifd_<NAME>.so (git-ignored, travels with gpurun). `run` loads each
 variant in its own child process, runs config 2's full device pipeline, and prints one JSON line
 per variant: k_modesum ms (HIP events, mean of 5 launches), the spectrum's max deviation from
-the in-tree library's (relative to max|S|), and the EFD_EXP_COUNT counters when compiled in.
+the in-tree library's (relative to max|S|), and the -DEFD_EXP counters when compiled in.
 The variant named "base" is the in-tree library. EXP_T / EXP_EPS select the workload (default
 config 2: T = 2 yr, eps = 1e-5).
 """
@@ -90,7 +90,7 @@ def child(name, ref_path):
     elif name == "base" and ref_path:
         np.save(ref_path, Sh)
     if has_cnt and os.environ.get("EXP_TCLK") and "tclk" in name:
-        # per-tile wall clock of the last launch (-DEFD_EXP_TCLK; 100 MHz s_memrealtime ticks):
+        # per-tile wall clock of the last launch (-DEFD_EXP; 100 MHz s_memrealtime ticks):
         # how much of the launch runs below full tile concurrency (the tail)
         nt_ = min(int(os.environ["EXP_TCLK"]), 16384)
         ev = (ctypes.c_uint * 16384)()
@@ -123,7 +123,7 @@ def child(name, ref_path):
                         "us_below_half_concurrency": float(len(below) * (grid[1] - grid[0])) / 100.0,
                         "longest_tiles": [int(i) for i in np.argsort(dur)[-5:]]}
     if has_cnt:
-        cnt = (ctypes.c_ulonglong * 32)()
+        cnt = (ctypes.c_ulonglong * 40)()   # EXP_NCOUNT (emrifd.hip, -DEFD_EXP)
         lib.efd_exp_counters(cnt)
         runs = 1 + int(os.environ.get("EXP_REPS", "6"))  # counters accumulate over every launch
         out["counters_per_launch"] = {k: cnt[i] / runs for i, k in enumerate(
@@ -132,7 +132,8 @@ def child(name, ref_path):
              "y_ge29", "y_ge23", "y_ge20", "y_ge18", "y_lt18", "cold_wave_evals", "cold_wave_lanes",
              "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1",
              "chunk_max_wave_evals", "chunk_wave_evals", "chunks", "segments",
-             "tile_hits", "safe_wave_evals"))}
+             "tile_hits", "safe_wave_evals", "unused30", "unused31", "records_j1", "records_j2",
+             "records_j3", "records_j4", "subbranch_flips"))}
         c = out["counters_per_launch"]
         if c["chunk_wave_evals"] > 0:
             # wave-time lost at the chunk barriers if every record evaluation cost the same
