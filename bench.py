@@ -504,9 +504,15 @@ def bench_likelihood(args):
     import torch.distributed as dist
     from emri_frequencydomainwaveforms_amd import pe
     from emri_frequencydomainwaveforms_amd.parallel import ShardedLikelihood
+    from emri_frequencydomainwaveforms_amd import hostcpu
+    from emri_frequencydomainwaveforms_amd.parallel import shard_range
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # this rank's disjoint share of the node's host cores (LOCAL_WORLD_SIZE shares; the upstream
+    # pool and the native thread count follow it, not torchrun's OMP_NUM_THREADS=1)
+    share = hostcpu.pin()
+    host_threads = hostcpu.threads()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
@@ -546,7 +552,17 @@ def bench_likelihood(args):
         ll = sl(batches[i % len(batches)])
     barrier()
     elapsed = time.perf_counter() - t0
+    # per-rank API rate: this rank's walker shard over its own time with the upstream in the loop
+    lo, hi = shard_range(B, rank, world)
+    mine = dict(rank=rank, walkers_per_step=hi - lo, api_s=api,
+                api_loglikes_per_s=args.api_steps * (hi - lo) / api, host_threads=host_threads,
+                host_cores=len(share), host_core_range=[min(share), max(share)] if share else None)
+    per_rank = [mine]
+    rccl_world = 1
     if world > 1:
+        rccl_world = dist.get_world_size()
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         tt = torch.tensor([elapsed, api], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, api = float(tt[0]), float(tt[1])
@@ -567,6 +583,8 @@ def bench_likelihood(args):
                        "fused_likelihood": bool(s.like.fused_likelihood),
                        "tile_constants": bool(s.like.fused_tile_constants)},
             "api_loglikes_per_s": args.api_steps * B / api,
+            "api_per_rank": per_rank,
+            "world_size_rccl": rccl_world,
             "host_upstream_ms_per_walker": memo.host_s / max(1, len(memo.memo)) * 1e3,
             "ll_truth_walker_sample": float(np.asarray(ll)[0]),
             "note": "value: device path with each walker's host upstream memoised after the "

@@ -246,17 +246,30 @@ def load(path=None):
                                        ctypes.POINTER(i32), vp, i64]
         lib.efd_host_set_threads.restype = ctypes.c_int
         lib.efd_host_set_threads.argtypes = [i32]
-        # the loading (main) thread's one-at-a-time upstream calls spread their knots over the
-        # host cores; the prefetch pool's threads keep one each (the setting is per thread)
+        # the loading (main) thread's one-at-a-time upstream calls spread their knots over this
+        # rank's host cores (hostcpu: its disjoint share of the node, not OMP_NUM_THREADS). The
+        # setting is per thread: the prefetch pool's threads set their own per batch
+        # (waveform.FastSchwarzschildEccentricFlux.prefetch splits the pool's threads over the
+        # batch's walkers)
         import threading
         if threading.current_thread() is threading.main_thread():
-            n = len(os.sched_getaffinity(0))
-            n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16)
-            lib.efd_host_set_threads(max(1, n))
+            from . import hostcpu
+            global _host_threads
+            _host_threads = hostcpu.threads()
+            lib.efd_host_set_threads(_host_threads)
     _ = dbl
     if path is None:
         _lib = lib
     return lib
+
+
+_host_threads = 1
+
+
+def host_threads():
+    """The main thread's efd_host_set_threads value chosen by load() (hostcpu.threads())."""
+    load()
+    return _host_threads
 
 
 def last_error(lib=None):

@@ -4227,15 +4227,24 @@ int efd_stream_order(void* src, void* const* dst, int32_t count) {
     if (count == 0) return EFD_OK;
     // one event per thread and device, re-recorded each call: a wait already enqueued keeps the
     // record it saw (stream-wait semantics), so reuse never loosens an earlier ordering
+    // The event belongs to the source stream's device (not the caller's current device, which
+    // may have changed since the streams were made): created and recorded with that device
+    // current, the caller's device restored afterwards.
     constexpr int MAX_DEV = 64;
     thread_local hipEvent_t ev[MAX_DEV] = {};
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
+    int cur = 0, dev = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    dev = cur;
+    if (src) HIP_TRY(hipStreamGetDevice((hipStream_t)src, &dev));
     if (dev < 0 || dev >= MAX_DEV) return fail(EFD_ERR_ARG, "efd_stream_order: device index");
-    if (!ev[dev]) HIP_TRY(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(ev[dev], (hipStream_t)src));
-    for (int32_t i = 0; i < count; ++i)
-        if (dst[i] != src) HIP_TRY(hipStreamWaitEvent((hipStream_t)dst[i], ev[dev], 0));
+    if (dev != cur) HIP_TRY(hipSetDevice(dev));
+    hipError_t e = hipSuccess;
+    if (!ev[dev]) e = hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev[dev], (hipStream_t)src);
+    for (int32_t i = 0; e == hipSuccess && i < count; ++i)
+        if (dst[i] != src) e = hipStreamWaitEvent((hipStream_t)dst[i], ev[dev], 0);
+    if (dev != cur) HIP_TRY(hipSetDevice(cur));
+    HIP_TRY(e);
     return EFD_OK;
 }
 

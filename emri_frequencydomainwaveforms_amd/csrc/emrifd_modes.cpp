@@ -40,8 +40,8 @@ void magnitudes(double p, double e, int nm, const double* c1, const double* dn, 
     }
 }
 // threads for one efd_host_modes call, per calling thread (efd_host_set_threads): the API's
-// one-at-a-time calls split the knots over the host cores, while the prefetch pool's threads
-// (which never set it) run their walkers on one core each
+// one-at-a-time calls split the knots over the rank's host cores, and each prefetch pool thread
+// sets its share of the pool for the batch it works (pool size / walkers, at least 1)
 thread_local int t_threads = 1;
 }  // namespace
 

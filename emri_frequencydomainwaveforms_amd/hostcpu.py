@@ -1,0 +1,70 @@
+"""Host-core share of this process: one process per GPU, each with its own disjoint set of cores.
+
+The reference runs its upstream (trajectory, amplitudes, mode selection) on a process pool next
+to the sampler (`emri_pe.py:545`, `mp.Pool(4)`) and hands Eryn a vectorised likelihood
+(`ensemble.py:1283-1318`). Here each rank drives one GPU and runs the stand-in upstream of its
+walker shard on a thread pool (`waveform._pool`) whose native calls split their knots over
+`efd_host_set_threads` threads. Both counts come from this module, explicitly, so that neither
+the launcher's `OMP_NUM_THREADS=1` (torchrun sets it) nor a whole node's cores per rank decide
+them:
+
+  - the process's affinity set is split into `LOCAL_WORLD_SIZE` contiguous, disjoint shares and
+    rank `LOCAL_RANK` takes its own (a single process keeps the whole set);
+  - `pin()` restricts the process to that share (os.sched_setaffinity), so ranks on one node do
+    not oversubscribe each other's cores;
+  - `threads()` is the share's size, capped at `MAX_THREADS`; `EFD_HOST_THREADS` overrides it.
+"""
+
+import os
+
+MAX_THREADS = 16   # the GPU box's CPU share per GPU; more threads per walker batch stop paying
+
+
+def local_rank_world(env=None):
+    env = os.environ if env is None else env
+    return int(env.get("LOCAL_RANK", "0")), int(env.get("LOCAL_WORLD_SIZE", "1"))
+
+
+def rank_cores(affinity=None, local_rank=None, local_world=None):
+    """This rank's disjoint share of `affinity` (default: the process's affinity set), split
+    into `local_world` contiguous chunks of equal size (the remainder goes to the first ranks).
+    With fewer cores than ranks every rank keeps one core (round-robin)."""
+    cores = sorted(os.sched_getaffinity(0) if affinity is None else affinity)
+    lr, lw = local_rank_world()
+    lr = lr if local_rank is None else int(local_rank)
+    lw = lw if local_world is None else int(local_world)
+    if lw <= 1 or not cores:
+        return cores
+    if not 0 <= lr < lw:
+        raise ValueError(f"local rank {lr} outside a local world of {lw}")
+    if len(cores) < lw:
+        return [cores[lr % len(cores)]]
+    base, extra = divmod(len(cores), lw)
+    start = lr * base + min(lr, extra)
+    return cores[start:start + base + (1 if lr < extra else 0)]
+
+
+_PINNED = None
+
+
+def pin():
+    """Restrict this process to its rank's share (once; a no-op for a single local process).
+    Returns the share."""
+    global _PINNED
+    if _PINNED is None:
+        share = rank_cores()
+        _, lw = local_rank_world()
+        if lw > 1 and set(share) != os.sched_getaffinity(0):
+            os.sched_setaffinity(0, share)
+        _PINNED = share
+    return _PINNED
+
+
+def threads(share=None):
+    """Host threads for this rank's upstream: its share's size (at most MAX_THREADS), or
+    EFD_HOST_THREADS when set. OMP_NUM_THREADS is deliberately not consulted."""
+    env = os.environ.get("EFD_HOST_THREADS")
+    if env:
+        return max(1, int(env))
+    share = pin() if share is None else share
+    return max(1, min(len(share), MAX_THREADS))

@@ -253,6 +253,8 @@ class Likelihood:
         if hasattr(tm, "prefetch"):
             tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
         n = len(params)
+        if n == 0:
+            return np.empty(0, dtype=np.float64)
         ngroups = -(-n // self.FUSED_GROUP)
         G = -(-n // ngroups)                       # balanced groups of at most FUSED_GROUP
         caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),

@@ -75,6 +75,7 @@ class FastSchwarzschildEccentricFlux:
         self.last_modes = None
         self._ylm_cache = {}
         self._prefetched = {}
+        self._prefetched_bytes = 0
         self._lock = threading.Lock()
 
     # -- host-side upstream ------------------------------------------------------------------
@@ -108,6 +109,8 @@ class FastSchwarzschildEccentricFlux:
             if self._prefetched:
                 with self._lock:
                     hit = self._prefetched.pop(key, None)
+                    if hit is not None:
+                        self._prefetched_bytes -= _nbytes(hit)
                 if hit is not None:
                     return hit
         amp = self.amplitude_generator
@@ -189,12 +192,23 @@ class FastSchwarzschildEccentricFlux:
 
         res = list(pool.map(run, calls))
         with self._lock:
-            if len(self._prefetched) > 4096:   # results nobody took (e.g. after an exception)
+            # results nobody took (a batch interrupted by an exception, parameters the caller
+            # then changed) are dropped once they would hold more than PREFETCH_MAX_BYTES of
+            # host memory (each holds the walker's amplitudes, N_t x K complex, and trajectory)
+            add = sum(_nbytes(r) for r in res)
+            if self._prefetched_bytes + add > self.PREFETCH_MAX_BYTES:
                 self._prefetched.clear()
+                self._prefetched_bytes = 0
             for c, r in zip(calls, res):
                 key = tuple(float(v) for v in c[:11]) + (True,)
+                old = self._prefetched.pop(key, None)
+                if old is not None:
+                    self._prefetched_bytes -= _nbytes(old)
                 self._prefetched[key] = r
+                self._prefetched_bytes += _nbytes(r)
         return len(res)
+
+    PREFETCH_MAX_BYTES = 1 << 30
 
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
@@ -261,19 +275,26 @@ class FastSchwarzschildEccentricFlux:
         return out if self.use_gpu else out.cpu().numpy()
 
 
+def _nbytes(d):
+    """Host bytes held by one prepared upstream result (its numpy arrays)."""
+    return sum(v.nbytes for v in d.values() if isinstance(v, np.ndarray))
+
+
 _WAVEFORMS = {"FastSchwarzschildEccentricFlux": FastSchwarzschildEccentricFlux}
 _POOL = None
 
 
 def _pool():
-    """Threads for the host upstream of walker batches (its native parts release the GIL);
-    sized to this process's CPU share, at most 16."""
+    """Threads for the host upstream of walker batches (its native parts release the GIL):
+    one per core of this rank's disjoint host share (hostcpu.threads(): the node's cores split
+    over LOCAL_WORLD_SIZE ranks, at most 16; OMP_NUM_THREADS does not decide it)."""
     global _POOL
     if _POOL is None:
         from concurrent.futures import ThreadPoolExecutor
-        n = len(os.sched_getaffinity(0))
-        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16)
-        _POOL = ThreadPoolExecutor(max_workers=max(1, n), thread_name_prefix="efd-upstream")
+
+        from . import hostcpu
+        _POOL = ThreadPoolExecutor(max_workers=hostcpu.threads(),
+                                   thread_name_prefix="efd-upstream")
     return _POOL
 
 

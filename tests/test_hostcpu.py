@@ -1,0 +1,109 @@
+"""Per-rank host-core shares (emri_frequencydomainwaveforms_amd/hostcpu.py).
+
+One process per GPU: each rank's upstream thread pool and native thread count come from its own
+disjoint share of the node's cores, not from OMP_NUM_THREADS (torchrun sets it to 1) and not from
+the whole node per rank. The gloo test launches 2 ranks as torchrun would (LOCAL_RANK,
+LOCAL_WORLD_SIZE, OMP_NUM_THREADS=1) and checks the shares they pin are disjoint and sized as
+the pool uses them. Reference shape: emri_pe.py:514-575 (mp.Pool next to the sampler),
+ensemble.py:1283-1318 (vectorised likelihood call).
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from emri_frequencydomainwaveforms_amd import hostcpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.mark.parametrize("ncores,world", [(128, 8), (16, 1), (16, 2), (10, 4), (3, 8), (8, 3)])
+def test_rank_cores_disjoint_and_covering(ncores, world):
+    aff = set(range(100, 100 + ncores))   # a faked affinity set (core ids need not start at 0)
+    shares = [hostcpu.rank_cores(aff, r, world) for r in range(world)]
+    assert all(len(s) >= 1 for s in shares)
+    if ncores >= world:
+        flat = [c for s in shares for c in s]
+        assert len(flat) == len(set(flat)) == ncores          # disjoint, every core used
+        sizes = [len(s) for s in shares]
+        assert max(sizes) - min(sizes) <= 1
+        for s in shares:                                      # contiguous runs
+            assert s == list(range(s[0], s[0] + len(s)))
+    else:
+        assert all(len(s) == 1 for s in shares)
+
+
+def test_threads_ignores_omp_and_caps(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    monkeypatch.delenv("EFD_HOST_THREADS", raising=False)
+    assert hostcpu.threads(list(range(12))) == 12
+    assert hostcpu.threads(list(range(64))) == hostcpu.MAX_THREADS
+    monkeypatch.setenv("EFD_HOST_THREADS", "3")
+    assert hostcpu.threads(list(range(64))) == 3
+
+
+def test_rank_cores_bad_rank():
+    with pytest.raises(ValueError):
+        hostcpu.rank_cores({0, 1, 2, 3}, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    # the environment torchrun gives each rank of one node
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      OMP_NUM_THREADS="1")
+    os.environ.pop("EFD_HOST_THREADS", None)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from emri_frequencydomainwaveforms_amd import hostcpu as hc
+        from emri_frequencydomainwaveforms_amd import waveform
+        share = hc.pin()
+        n = hc.threads()
+        pool = waveform._pool()._max_workers
+        # a faked 128-core node split the same way (the 8-GPU box's shape)
+        fake = hc.rank_cores(set(range(128)), rank, world)
+        got = [None] * world
+        dist.all_gather_object(got, dict(share=sorted(share),
+                                         affinity=sorted(os.sched_getaffinity(0)),
+                                         threads=n, pool=pool, fake=fake))
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_pin_disjoint_shares():
+    ncpu = len(os.sched_getaffinity(0))
+    if ncpu < 2:
+        pytest.skip("needs 2 host cores")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = res[0]
+    a, b = got[0], got[1]
+    assert set(a["share"]).isdisjoint(b["share"])
+    assert a["affinity"] == a["share"] and b["affinity"] == b["share"]   # pinned
+    assert len(a["share"]) + len(b["share"]) == ncpu
+    for g in (a, b):
+        # OMP_NUM_THREADS=1 from the launcher does not decide the pool or the native threads
+        assert g["threads"] == g["pool"] == min(len(g["share"]), hostcpu.MAX_THREADS)
+    assert set(a["fake"]).isdisjoint(b["fake"]) and len(a["fake"]) == len(b["fake"]) == 64
+    assert np.array_equal(res[1][0]["share"], a["share"])   # both ranks saw the same gather

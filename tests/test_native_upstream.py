@@ -78,6 +78,11 @@ def test_modes_match_numpy(trajs, theta, eps):
         np.testing.assert_array_equal(kp, ModeSelector(amp.m0mask)(amp(p, e), ylms, None, eps=eps))
 
 
+def waveform_nbytes(d):
+    from emri_frequencydomainwaveforms_amd.waveform import _nbytes
+    return _nbytes(d)
+
+
 def _bare_generator(backend):
     """The FD generator's host half only (no GPU needed)."""
     from emri_frequencydomainwaveforms_amd.waveform import FastSchwarzschildEccentricFlux
@@ -88,6 +93,7 @@ def _bare_generator(backend):
     wg.mode_selector = ModeSelector(wg.amplitude_generator.m0mask)
     wg.output_type, wg.last_modes = "fd", None
     wg._ylm_cache, wg._prefetched, wg._lock = {}, {}, threading.Lock()
+    wg._prefetched_bytes = 0
     return wg
 
 
@@ -108,7 +114,12 @@ def test_prepare_native_vs_numpy_and_prefetch():
         got = wn.prepare(*c)                       # taken from the prefetched results
         for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
             np.testing.assert_array_equal(got[k], ref[k])
-    assert not wn._prefetched
+    assert not wn._prefetched and wn._prefetched_bytes == 0
+    # results nobody takes are dropped once they pass the byte bound
+    wn.PREFETCH_MAX_BYTES = 3 * waveform_nbytes(serial[0])
+    wn.prefetch(calls[:2])
+    wn.prefetch(calls[2:4])                        # 4 results would pass 3: the first 2 go
+    assert len(wn._prefetched) == 2 and wn._prefetched_bytes <= wn.PREFETCH_MAX_BYTES
 
 
 def test_host_modes_threads_bitwise():
@@ -132,7 +143,7 @@ def test_host_modes_threads_bitwise():
             keep, teuk = amp.select(p, e, y, 1e-4, lib=lib)
             res.append((keep.copy(), teuk.copy()))
     finally:
-        lib.efd_host_set_threads(1)
+        lib.efd_host_set_threads(_lib.host_threads())   # the value load() chose
     for keep, teuk in res[1:]:
         np.testing.assert_array_equal(keep, res[0][0])
         np.testing.assert_array_equal(teuk, res[0][1])
