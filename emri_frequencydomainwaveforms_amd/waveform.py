@@ -393,6 +393,67 @@ class GenerateEMRIWaveform:
                         f_phi=d["f_phi"], f_r=d["f_r"], m=d["m"], n=d["n"], ylm_p=y[:K],
                         ylm_m=y[K:], _keep=d), freq, True, scale, k0=kc, prepare_only=True)
 
+    # waveforms per device group of generate_batch: one packed upload, one
+    # efd_modesum_prepare_batch and one efd_modesum_sum_batch each (EFD_BATCH_MAX at most)
+    BATCH_GROUP = 16
+
+    def generate_batch(self, params, out, T=1.0, dt=10.0, eps=1e-5, f_arr=None, **kwargs):
+        """[h+, hx] over f >= 0 of every row of params (B x 14, FEW's order) into out
+        (complex128 [B][2][N_pos] on the device): the vectorised form of B calls
+        `self(*row, T=T, dt=dt, eps=eps, mask_positive=True)` with return_list=True (bitwise
+        the same values), for scans like check_mode_by_mode.py:183-229 and batches of walkers.
+
+        The host upstream of all rows runs at once on the thread pool (prefetch: trajectory,
+        amplitudes, selection; this rank's host-core share), then the device work goes in
+        groups of BATCH_GROUP: one packed upload and one efd_modesum_prepare_batch per group on
+        that group's stream, one efd_modesum_sum_batch writing the group's h+/hx, two groups in
+        flight. Returns out, ordered after the work on the current stream."""
+        torch = require_gpu()
+        from .summation import BatchPreparer, sum_batch
+        gen = self.waveform_generator
+        if gen.output_type != "fd":
+            raise ValueError("generate_batch is the FD path")
+        params = np.asarray(params, dtype=np.float64).reshape(-1, 14)
+        B = len(params)
+        cw = gen.create_waveform
+        freq, sym = cw._grid(T, dt, f_arr)
+        if not sym:
+            raise ValueError("generate_batch needs a symmetric grid")
+        npos = int(freq.numel()) - cw._k0
+        if tuple(out.shape) != (B, 2, npos) or out.dtype != torch.complex128:
+            raise ValueError(f"out must be complex128 [{B}][2][{npos}]")
+        if B == 0:
+            return out
+        self.prefetch(params, T=T, dt=dt, eps=eps, **kwargs)
+        G = min(self.BATCH_GROUP, _lib.EFD_BATCH_MAX)
+        st = getattr(self, "_gen_batch", None)
+        if st is None or st["prep"].caustic != cw.caustic or st["device"] != out.device:
+            st = self._gen_batch = dict(
+                prep=BatchPreparer(group=G, depth=2, caustic=cw.caustic, device=out.device),
+                stream=torch.cuda.Stream(out.device), device=out.device,
+                ev=[torch.cuda.Event(), torch.cuda.Event()])
+        prep, s_sum = st["prep"], st["stream"]
+        cur = torch.cuda.current_stream(out.device)
+        prep.order_after_current()
+        s_sum.wait_stream(cur)
+        try:
+            for g0 in range(0, B, G):
+                rows = params[g0:g0 + G]
+                self.submit_batch(prep, rows, T=T, dt=dt, eps=eps, f_arr=f_arr, **kwargs)
+                gi, jobs = prep.flush()
+                s_sum.wait_stream(prep.stream(gi))
+                sum_batch([(eng, dict(kw, hp=torch.view_as_real(out[g0 + i, 0]),
+                                      hc=torch.view_as_real(out[g0 + i, 1])))
+                           for i, (eng, kw) in enumerate(jobs)], stream=s_sum.cuda_stream)
+                ev = st["ev"][gi]
+                ev.record(s_sum)
+                prep.release(gi, ev)
+        finally:
+            prep._pending = []
+            cur.wait_stream(s_sum)
+        prep.wait()   # device-side errors of the groups' workspaces raise here
+        return out
+
     def prefetch(self, params, T=1.0, dt=10.0, eps=1e-5, mode_selection=None,
                  include_minus_m=True, **kwargs):
         """The host upstream of a batch of 14-parameter sets at once (thread pool; see

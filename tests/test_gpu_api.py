@@ -220,3 +220,30 @@ def test_pipelined_likelihood_asymmetric_grid(setup):
     like_g.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2, noise_kwargs=[{}, {}])
     np.testing.assert_array_equal(like_g.get_ll(walkers, **kw2), ll)
     assert ll[0] == 0.0 and np.all(ll[1:] < 0.0)
+
+
+def test_generate_batch_matches_calls(setup):
+    """GenerateEMRIWaveform.generate_batch (the vectorised scan: pooled host upstream, groups of
+    BATCH_GROUP on the device) writes, bitwise, each row's [h+, hx] over f >= 0 as the
+    one-at-a-time list call with mask_positive=True; a ragged last group and a second call on
+    the reused groups included."""
+    params, kw, gen, gen_list = setup
+    rng = np.random.default_rng(11)
+    rows = np.repeat(params[None, :], 5, axis=0)
+    rows[:, 0] *= 1.0 + 1e-3 * rng.normal(size=5)          # distinct M
+    rows[:, 4] = E0 + 0.01 * rng.normal(size=5)            # distinct e0
+    rows[:, 11] = rng.uniform(0, 2 * np.pi, size=5)         # distinct Phi_phi0
+    gen_list.BATCH_GROUP = 2                                # groups of 2, 2, 1
+    try:
+        ref = [torch.stack(gen_list(*r, mask_positive=True, **kw)) for r in rows]
+        out = torch.empty((5,) + tuple(ref[0].shape), dtype=torch.complex128, device="cuda")
+        for _ in range(2):
+            out.zero_()
+            gen_list.generate_batch(rows, out, **kw)
+            torch.cuda.synchronize()
+            for b in range(5):
+                assert torch.equal(out[b], ref[b]), b
+    finally:
+        del gen_list.BATCH_GROUP
+    with pytest.raises(ValueError):
+        gen_list.generate_batch(rows, out[:4], **kw)
