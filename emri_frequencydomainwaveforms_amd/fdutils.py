@@ -76,6 +76,37 @@ def get_convolution(a, b):
     return full[nb - 1:nx] / nb
 
 
+def window_multiplier(window, window_in_fd=False):
+    """The window convolution of get_fd_windowed as a multiplier in the DFT's other domain.
+
+    get_convolution(conj(fft(w)), b) is the circular convolution (a (*) b) / N with
+    a = conj(fft(w)); by the convolution theorem it equals ifft(fft(a) fft(b)) / N, and
+    fft(conj(fft(w))) = N conj(w). So the windowed spectrum is ifft(m * fft(b)) with m = conj(w)
+    (= w for the reference's real window: exact, no transform of the window); for a window given
+    in FD (window_in_fd), m = fft(conj(window)) / N."""
+    torch = require_gpu()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    w = torch.as_tensor(window, device=dev)
+    if window_in_fd:
+        n = int(w.numel())
+        return torch.fft.fft(torch.conj(w.to(torch.complex128))) / n
+    return torch.conj(w) if torch.is_complex(w) else w.to(torch.float64)
+
+
+def windowed_spectrum(S, mult):
+    """The two-sided spectrum S = h+ - i hx (rows: one waveform each) convolved with the
+    window: ifft(mult * fft(S)) along the last axis (rocFFT, batched over rows).
+
+    The reference convolves h+ and hx separately (FDutils.py:95-96). The window kernel
+    a = conj(fft(w)) of a real window is Hermitian (a[-m] = conj(a[m])), so the convolution
+    commutes with the mirror-conjugation b[k] -> conj(b[N-1-k]) of the odd two-sided grid; h+ and
+    hx are linear in S and its mirror-conjugate (h+ = (S + M S) / 2, hx = i (S - M S) / 2), so
+    the windowed h+ and hx are those of the windowed S: one transform pair per waveform instead
+    of one per channel."""
+    torch = require_gpu()
+    return torch.fft.ifft(torch.fft.fft(S.to(torch.complex128), dim=-1) * mult, dim=-1)
+
+
 def get_fd_windowed(signal, window, window_in_fd=False):
     """[h+, hx] convolved with the window's spectrum (FDutils.py:66-101)."""
     if window is None:
@@ -102,16 +133,35 @@ class get_fd_waveform_fromFD:
         self.window = window
         self.window_in_fd = window_in_fd
         self.dt = dt
+        self._mult = None if window is None else window_multiplier(window, window_in_fd)
         # contiguous-suffix mask (f >= 0 of a sorted grid): the fused fill path applies
         pm = self.positive_frequency_mask
         k0 = int(torch.argmax(pm.to(torch.int8)).item()) if bool(pm.any()) else int(pm.numel())
         self._suffix_k0 = k0 if bool(pm[k0:].all()) and not bool(pm[:k0].any()) else None
         self.num_bins = int(pm.sum().item())
 
+    def _windowed_s_path(self):
+        """Windowed templates through the two-sided spectrum (windowed_spectrum): a generator
+        with the spectrum entry (GenerateEMRIWaveform) on a symmetric grid whose f >= 0 part is
+        the positive mask's suffix."""
+        gen = self.waveform_generator
+        return (self.window is not None and self._suffix_k0 is not None
+                and hasattr(gen, "_spectrum") and hasattr(gen, "waveform_generator")
+                and getattr(gen.waveform_generator, "output_type", None) == "fd"
+                and self._mult is not None
+                and int(self._mult.numel()) == int(self.positive_frequency_mask.numel()))
+
     def __call__(self, *args, **kwargs):
+        torch = require_gpu()
+        if self._windowed_s_path():
+            out = torch.empty((2, self.num_bins), dtype=torch.complex128,
+                              device=self.positive_frequency_mask.device)
+            self.fill(out, *args, **kwargs)
+            if self.non_zero_mask is not None:
+                out[:, ~self.non_zero_mask] = 0.0
+            return [out[0], out[1]]
         chans = self.waveform_generator(*args, **kwargs)
         p, c = get_fd_windowed(chans, self.window, window_in_fd=self.window_in_fd)
-        torch = require_gpu()
         p = torch.as_tensor(p)
         c = torch.as_tensor(c)
         ch1 = p[self.positive_frequency_mask]
@@ -124,12 +174,14 @@ class get_fd_waveform_fromFD:
     @property
     def can_fill(self):
         gen = self.waveform_generator
-        return (self.window is None and self._suffix_k0 is not None
-                and hasattr(gen, "fill_channels"))
+        if self.window is not None:
+            return self._windowed_s_path()
+        return self._suffix_k0 is not None and hasattr(gen, "fill_channels")
 
     @property
     def can_pipeline(self):
-        return self.can_fill and hasattr(self.waveform_generator, "submit_channels")
+        return (self.window is None and self.can_fill
+                and hasattr(self.waveform_generator, "submit_channels"))
 
     def submit(self, pipeline, out, *args, **kwargs):
         """fill, queued on a WaveformPipeline slot (returns the slot; see
@@ -158,7 +210,17 @@ class get_fd_waveform_fromFD:
         Bins outside non_zero_mask are NOT zeroed here; the Likelihood folds that mask into
         the template's noise weight instead (same result: h * 0).
         """
-        self.waveform_generator.fill_channels(out, *args, k0=self._suffix_k0, **kwargs)
+        if self.window is None:
+            self.waveform_generator.fill_channels(out, *args, k0=self._suffix_k0, **kwargs)
+            return out
+        if not self._windowed_s_path():
+            raise ValueError("fill: a windowed template needs the spectrum path")
+        gen = self.waveform_generator
+        S = gen._spectrum(*args, **kwargs)
+        cw = gen.waveform_generator.create_waveform
+        if self._suffix_k0 != cw.positive_start():
+            raise ValueError("positive_frequency_mask does not match the generator's grid")
+        cw.polarizations(windowed_spectrum(S, self._mult), True, out=(out[0], out[1]))
         return out
 
 

@@ -213,6 +213,8 @@ class Likelihood:
         elif getattr(tm, "can_fill", False):
             if self._buf is None or tuple(self._buf.shape) != (nch, nb):
                 self._buf = torch.empty((nch, nb), dtype=torch.complex128, device=self.device)
+            if hasattr(tm, "prefetch"):
+                tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
             for i, params_i in enumerate(params):
                 tm.fill(self._buf, *params_i, *args, **kwargs)
                 self._red.loglike(self._buf, self._d, self._w_templ, out=out[i:i + 1])

@@ -47,7 +47,10 @@ class PESetup:
 
 
 def setup(Tobs=2.0, dt=10.0, eps=1e-2, M=1e6, mu=10.0, e0=0.35, downsample=None, nwalkers=16,
-          ntemps=1, seed=SEED, caustic="uniform", subset=24):
+          ntemps=1, seed=SEED, caustic="uniform", subset=24, window_flag=False):
+    """window_flag: the templates and the injection convolved with a Hann window of the grid's
+    length (emri_pe.py:259-263, -window_flag 1 in test.sh: scipy.signal.windows.hann(N), N the
+    TD/FD length, odd_len); not with downsampling (emri_pe.py:330-331)."""
     from .fdutils import get_fd_waveform_fromFD, get_sensitivity
     from .likelihood import Likelihood
     from .trajectory import EMRIInspiral, get_p_at_t
@@ -78,6 +81,13 @@ def setup(Tobs=2.0, dt=10.0, eps=1e-2, M=1e6, mu=10.0, e0=0.35, downsample=None,
     pos = frequency >= 0.0
     info = {"p0": p0, "N_f": int(len(frequency))}
     like_subset = subset
+    window = None
+    if window_flag:
+        if downsample:
+            raise ValueError("Cannot run downsampling with windowing")   # emri_pe.py:331
+        from scipy.signal.windows import hann
+        window = hann(len(frequency))
+        info["window"] = "hann"
     if downsample:
         fixed = frequency[pos]
         nz = np.abs(sig[0].cpu().numpy()) > 1e-50                    # emri_pe.py:245
@@ -91,7 +101,7 @@ def setup(Tobs=2.0, dt=10.0, eps=1e-2, M=1e6, mu=10.0, e0=0.35, downsample=None,
         info.update(downsample=downsample, N_f_downsampled=int(len(newfreq)))
     else:
         f_like = frequency[pos]
-    gen = get_fd_waveform_fromFD(few, pos, dt)
+    gen = get_fd_waveform_fromFD(few, pos, dt, window=window)
     like = Likelihood(gen, 2, parameter_transforms={"emri": tc}, vectorized=False,
                       transpose_params=False, subset=like_subset, f_arr=f_like, use_gpu=True)
     data = gen(*injection, **kw)

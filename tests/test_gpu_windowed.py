@@ -1,0 +1,102 @@
+"""GPU parity of the windowed FD likelihood at the reference's own smoke shape (test.sh:3).
+
+    emri_pe.py -Tobs 4.0 -M 3670041.7362535275 -mu 292.0583167470244 -e0 0.5794130830706371
+               -eps 1e-2 -dt 10.0 -template fd -nwalkers 16 -ntemps 1 -window_flag 1
+
+The templates and the injection are the FD mode sum convolved with a Hann window of the grid's
+length (emri_pe.py:259-263; FDutils.py:66-101 get_fd_windowed, :105-139 get_fd_waveform_fromFD),
+on the full 12,623,261-bin grid. The injection is the FD template of the truth (injectFD 1), so
+the truth's logL is exactly 0. One red-blue half-step of 8 walkers from the reference's start
+distribution goes through Likelihood.__call__ (GPU: mode sum -> windowed_spectrum, one rocFFT
+transform pair per walker -> h+/hx -> efd_loglike).
+
+Checker, per walker (all 8):
+  - the GPU spectrum S against the oracle's C-restatement spectrum R of the same walker, bin by
+    bin (tests/helpers.split_check: 1e-9 max|R| off the folds, 2 D_k at the folds);
+  - the oracle's logL: R windowed on the CPU by likelihood_oracle.windowed_polarizations (the
+    reference's per-channel get_convolution, through S; pinned to the direct convolution in
+    tests/test_oracle_likelihood.py), positive mask, likelihood_oracle.loglike with the oracle's
+    own windowed injection as data;
+  - tolerance, written out: with r = d - h w and e = ||(d_gpu - d_R)|| + ||(h_gpu - h_R) w|| the
+    measured distance between the GPU's and the oracle's windowed channels (h_gpu: the GPU's S
+    windowed on the CPU the same way), |ll_gpu - ll_oracle| <= 4 ||r|| e + 2 e^2
+    (Cauchy-Schwarz on -2 sum |r|^2); and the GPU's logL equals the CPU loglike of its own
+    windowed spectrum to 1e-10 relative (rocFFT vs pocketfft rounding and reduction order).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from emri_frequencydomainwaveforms_amd import pe  # noqa: E402
+from emri_frequencydomainwaveforms_amd.fdutils import get_sensitivity  # noqa: E402
+from oracle import likelihood_oracle as lo  # noqa: E402
+from tests.helpers import oracle_spectra, record_parity, split_check  # noqa: E402
+
+TEST_SH = dict(Tobs=4.0, dt=10.0, eps=1e-2, M=3670041.7362535275, mu=292.0583167470244,
+               e0=0.5794130830706371)
+
+
+def _workers():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _windowed_channels(S, window, grid):
+    hp, hc = lo.windowed_polarizations(S, window, workers=_workers())
+    keep = np.asarray(grid) >= 0.0
+    return np.stack([hp[keep], hc[keep]])
+
+
+def test_windowed_likelihood_test_sh_full_grid():
+    s = pe.setup(nwalkers=16, ntemps=1, window_flag=True, **TEST_SH)
+    assert s.info["N_f"] == 12623261 and s.half_step == 8 and s.info.get("window") == "hann"
+    gen = s.gen
+    assert gen.can_fill and not gen.can_pipeline      # the windowed spectrum path
+    like = s.like
+    batch = s.half_steps()[0]
+    ll = like(batch, **s.kwargs)
+    assert np.array_equal(like(batch, **s.kwargs), ll)                 # repeatable
+    assert like(s.truth6[None, :], **s.kwargs)[0] == 0.0              # injectFD: exact zero
+    assert np.all(ll < 0.0)
+
+    f = s.f_like
+    w = lo.noise_factor(f, [get_sensitivity(f)] * 2)
+    window = gen.window
+    # the oracle's injection, windowed on the CPU
+    R0, _, grid, _ = oracle_spectra(s.few, s.truth14, s.kwargs)
+    d_R = _windowed_channels(R0, window, grid) * w
+    S0 = s.few._spectrum(*s.truth14, **s.kwargs).cpu().numpy()
+    d_gpu = _windowed_channels(S0, window, grid) * w
+    e_d = np.sqrt(np.sum(np.abs(d_gpu - d_R) ** 2))
+    params14 = s.transform.both_transforms(batch)
+    rows, ok_all = [], True
+    for i, p in enumerate(params14):
+        R, Rps, _, E = oracle_spectra(s.few, p, s.kwargs, perturb_seeds=(20 + i, 2000 + i))
+        S = s.few._spectrum(*p, **s.kwargs).cpu().numpy()
+        ok, st, _ = split_check(S, R, Rps, E=E)
+        np.testing.assert_array_equal(S != 0, R != 0)
+        h_R = _windowed_channels(R, window, grid)
+        h_gpu = _windowed_channels(S, window, grid)
+        ll_R = lo.loglike(h_R, d_R, w)
+        ll_self = lo.loglike(h_gpu, d_gpu, w)      # the GPU's own spectrum, windowed on the CPU
+        e = e_d + np.sqrt(np.sum(np.abs((h_gpu - h_R) * w) ** 2))
+        rn = np.sqrt(np.sum(np.abs(d_R - h_R * w) ** 2))
+        bound = 4.0 * rn * e + 2.0 * e * e
+        err = abs(ll[i] - ll_R)
+        self_rel = abs(ll[i] - ll_self) / abs(ll_self)
+        rows.append(dict(walker=i, ll_gpu=float(ll[i]), ll_oracle=float(ll_R),
+                         abs_err=float(err), bound=float(bound),
+                         err_over_bound=float(err / bound) if bound > 0 else 0.0,
+                         ll_self_rel=float(self_rel), spectrum=st))
+        ok_all &= ok and err <= bound and self_rel <= 1e-10
+    rec = {"config": "test_sh_windowed", "walkers": len(rows), "N_f": s.info["N_f"],
+           "p0": s.info["p0"], "rows": rows,
+           "max_err_over_bound": max(r["err_over_bound"] for r in rows),
+           "max_bound": max(r["bound"] for r in rows),
+           "max_ll_self_rel": max(r["ll_self_rel"] for r in rows)}
+    record_parity("test_sh_windowed", rec)
+    assert ok_all, rec

@@ -80,3 +80,26 @@ def test_convolution_and_window(g):
     circ = np.fft.ifft(np.fft.fft(fw) * np.fft.fft(sig[0])) / len(win)
     assert _close(circ, g["win_conv"])
     np.testing.assert_allclose(g["win_fd_infd"], g["win_fd"], rtol=0, atol=1e-12)
+
+
+def test_windowed_convolution_forms(g):
+    """The FFT forms the full-size GPU test checks against (get_convolution_fft per channel,
+    windowed_polarizations through S) equal the direct get_convolution of the reference's form
+    (pinned to its scipy output by the golden fixture above) on the reference's own windowing
+    inputs and on a random odd-grid spectrum with a Hann window (scipy.signal.windows.hann, as
+    emri_pe.py:261)."""
+    from scipy.signal.windows import hann
+    sig, win = g["win_sig"], g["win_window"]
+    a = np.conj(np.fft.fft(win))
+    for ch in range(2):
+        assert _close(lo.get_convolution_fft(a, sig[ch]), lo.get_convolution(a, sig[ch]), 1e-12)
+    rng = np.random.default_rng(3)
+    for N in (101, 1001):
+        S = rng.normal(size=N) + 1j * rng.normal(size=N)
+        w = hann(N)
+        hp, hc = lo.polarizations(S)
+        np.testing.assert_allclose(hp - 1j * hc, S, rtol=0, atol=1e-14)   # S = h+ - i hx
+        aw = np.conj(np.fft.fft(w))
+        ref_p, ref_c = lo.get_convolution(aw, hp), lo.get_convolution(aw, hc)
+        wp, wc = lo.windowed_polarizations(S, w)
+        assert _close(wp, ref_p, 1e-12) and _close(wc, ref_c, 1e-12)

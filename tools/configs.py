@@ -230,20 +230,23 @@ def config3(reps, slots=4):
                            "host stand-in upstream incl. the p0 root solve per point"}
 
 
-def _likelihood_setup(T, eps, downsample, nwalkers, seed=2601996):
+def _likelihood_setup(T, eps, downsample, nwalkers, seed=2601996, **extra):
     """emri_pe.py's setup (emri_frequencydomainwaveforms_amd.pe: its angles, distance, phases,
     p0 for 0.99 Tobs, downsampled grid, Likelihood, walker start); the batch is the first
     red-blue half-step of the start, mapped to FEW's 14 parameters by the TransformContainer,
     with walker 0 on the injection (logL = 0 exactly)."""
     from emri_frequencydomainwaveforms_amd import pe
-    st = pe.setup(Tobs=T, eps=eps, downsample=downsample, nwalkers=nwalkers, seed=seed)
+    st = pe.setup(Tobs=T, eps=eps, downsample=downsample, nwalkers=nwalkers, seed=seed,
+                  **extra)
     walkers = st.transform.both_transforms(st.half_steps()[0])
     walkers[0] = st.truth14
     return st.few, st.like, walkers, st.kwargs, len(st.f_like)
 
 
-def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, group=None):
-    few, like, walkers, kw, nbins = _likelihood_setup(T, eps, downsample, nwalkers)
+def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, group=None,
+                **extra):
+    few, like, walkers, kw, nbins = _likelihood_setup(T, eps, downsample, nwalkers, **extra)
+    windowed = like.template_model.window is not None
     like.num_streams = slots
     like.fused_likelihood = fused
     if group:
@@ -272,9 +275,13 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
             "host_upstream_ms_per_walker": cache.host_s / B * 1e3,
             "ll_truth": float(ll[0]), "ll_min": float(np.min(ll)),
             "ll_bitwise_repeatable": bool(np.array_equal(ll, ll2)), "streams": slots,
-            "fused_likelihood": fused,
+            "fused_likelihood": fused and not windowed,
             "device_note": "Likelihood.get_ll over the half-step batch with the host upstream "
                            "memoised: " + (
+                               "per walker the FD spectrum S (mode sum), the Hann window "
+                               "convolution as one rocFFT transform pair on S "
+                               "(fdutils.windowed_spectrum), h+/hx over f >= 0 and efd_loglike"
+                               if windowed else 
                                "per balanced group of up to 16 walkers one packed input "
                                "upload (efd_stage_batch), one efd_modesum_prepare_batch and "
                                "one mode-sum launch with the likelihood fused in (no "
@@ -309,6 +316,14 @@ def main():
         out.append(config_like("config4: emri_pe nwalkers=16 ntemps=1 injectFD=1 template=fd "
                                "Tobs=2yr eps=1e-2 full grid", 2.0, 1e-2, None, 16, args.reps,
                                args.slots, not args.unfused, args.fused_group))
+        print(json.dumps(out[-1]), flush=True)
+    if "w" in which:
+        # test.sh:3: -Tobs 4 -M 3.67e6 -mu 292 -e0 0.579 -eps 1e-2 -template fd -window_flag 1
+        out.append(config_like("test.sh windowed: emri_pe Tobs=4yr M=3.67e6 mu=292 e0=0.579 "
+                               "eps=1e-2 nwalkers=16 window_flag=1 full grid", 4.0, 1e-2, None,
+                               16, args.reps, args.slots, not args.unfused, args.fused_group,
+                               M=3670041.7362535275, mu=292.0583167470244,
+                               e0=0.5794130830706371, window_flag=True))
         print(json.dumps(out[-1]), flush=True)
     if "5" in which:
         out.append(config_like("config5: emri_pe downsample=100 Tobs=4yr eps=1e-2 "
