@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "efd_download",
     "efd_stream_order",
     "efd_polarizations",
+    "efd_hann_polarizations",
     "efd_loglike",
     "efd_inner_product",
     "efd_modesum_cpu",
@@ -214,6 +215,8 @@ def load(path=None):
         lib.efd_stream_order.argtypes = [vp, ctypes.POINTER(vp), i32]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
+    lib.efd_hann_polarizations.restype = ctypes.c_int
+    lib.efd_hann_polarizations.argtypes = [vp, vp, vp, i64, i64, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int
     lib.efd_loglike.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
     lib.efd_inner_product.restype = ctypes.c_int

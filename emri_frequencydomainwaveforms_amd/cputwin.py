@@ -78,3 +78,20 @@ def stats():
     c, e, g = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
     _lib_cpu().efd_modesum_cpu_stats(ctypes.byref(c), ctypes.byref(e), ctypes.byref(g))
     return int(c.value), int(e.value), int(g.value)
+
+
+def loglike(h, d, w):
+    """efd_loglike_cpu: -1/2 * 4 * sum |d - h w|^2 over [nchan][nbin] host arrays (the host
+    twin of efd_loglike, same partition and reduction order)."""
+    lib = _lib_cpu()
+    h = np.ascontiguousarray(h, dtype=np.complex128)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    if h.shape != d.shape or w.shape != d.shape or d.ndim != 2:
+        raise ValueError("loglike: h, d, w must share one [nchan][nbin] shape")
+    out = np.zeros(1)
+    rc = lib.efd_loglike_cpu(h.ctypes.data, d.ctypes.data, w.ctypes.data, d.shape[0],
+                             d.shape[1], out.ctypes.data, None, None)
+    if rc != _lib.EFD_OK:
+        raise _lib.EFDError(f"efd_loglike_cpu failed ({rc}): {last_error()}")
+    return float(out[0])

@@ -3463,6 +3463,29 @@ __global__ void k_polarizations(const double2* __restrict__ S, int64_t nf, int64
     hc[i] = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
 }
 
+// h+/hx of the Hann-windowed spectrum (efd_hann_polarizations): S_w at k and at its mirror
+// nf - 1 - k from S and the complex64 correction C (neighbours mod nf), then the split
+__device__ __forceinline__ double2 hann_sw(const double2* __restrict__ S,
+                                           const float2* __restrict__ C, int64_t nf, int64_t k,
+                                           double c) {
+    const int64_t kp = k + 1 < nf ? k + 1 : 0, km = k > 0 ? k - 1 : nf - 1;
+    const double2 s = S[k], sp = S[kp], sm = S[km];
+    const float2 cp = C[kp], cm = C[km];
+    return make_double2(0.5 * s.x - 0.25 * (sp.x + sm.x) - c * ((double)cp.x - (double)cm.x),
+                        0.5 * s.y - 0.25 * (sp.y + sm.y) - c * ((double)cp.y - (double)cm.y));
+}
+__global__ void k_hann_polarizations(const double2* __restrict__ S, const float2* __restrict__ C,
+                                     const double* __restrict__ cscale, int64_t nf, int64_t k0,
+                                     double2* __restrict__ hp, double2* __restrict__ hc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = k0 + i;
+    if (k >= nf) return;
+    const double c = *cscale / (4.0 * (double)(nf - 1));
+    const double2 a = hann_sw(S, C, nf, k, c), b = hann_sw(S, C, nf, nf - 1 - k, c);
+    hp[i] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+    hc[i] = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+}
+
 // fused log-likelihood partials: one workgroup per chunk, then a second pass
 __global__ void k_loglike_partial(const double2* __restrict__ h, const double2* __restrict__ d,
                                   const double* __restrict__ w, int64_t total,
@@ -4258,6 +4281,21 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
     const int64_t blocks = (cnt + threads - 1) / threads;
     hipLaunchKernelGGL(k_polarizations, dim3((unsigned)blocks), dim3(threads), 0,
                        (hipStream_t)stream, (const double2*)S, nf, k0, (double2*)hp, (double2*)hc);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
+int efd_hann_polarizations(const double* S, const float* C, const double* cscale, int64_t nf,
+                           int64_t k0, double* hp, double* hc, void* stream) {
+    if (!S || !C || !cscale || !hp || !hc || nf < 3 || k0 < 0 || k0 > nf)
+        return fail(EFD_ERR_ARG, "efd_hann_polarizations: bad arguments");
+    const int64_t cnt = nf - k0;
+    if (cnt == 0) return EFD_OK;
+    const int threads = 256;
+    const int64_t blocks = (cnt + threads - 1) / threads;
+    hipLaunchKernelGGL(k_hann_polarizations, dim3((unsigned)blocks), dim3(threads), 0,
+                       (hipStream_t)stream, (const double2*)S, (const float2*)C, cscale, nf, k0,
+                       (double2*)hp, (double2*)hc);
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }

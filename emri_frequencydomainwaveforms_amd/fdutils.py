@@ -93,6 +93,91 @@ def window_multiplier(window, window_in_fd=False):
     return torch.conj(w) if torch.is_complex(w) else w.to(torch.float64)
 
 
+class HannConvolution:
+    """The reference's window convolution for its own window, scipy.signal.windows.hann(N)
+    (emri_pe.py:261, sym=True: w[n] = 1/2 - 1/2 cos(2 pi n / (N - 1))), without size-N DFTs.
+
+    windowed_spectrum's S_w = ifft(w fft(S)) splits, with theta = 2 pi / (N - 1) = (2 pi / N)
+    (1 + e), e = 1 / (N - 1), into 1/2 S minus 1/4 of the trigonometric interpolant
+    S~(k) = sum_j S[j] G(k - j), G(u) = (1/N) sum_n exp(2 pi i n u / N), at k +- (1 + e):
+      S_w[k] = 1/2 S[k] - 1/4 (S[k+1] + S[k-1]) - 1/4 e (C[k+1] - C[k-1]) + O(e^2),
+      C = K (*) S (circular),  K[m] = G'(m) = -i pi / N + (pi / N) cot(pi m / N),
+                               K[0] = i pi (N - 1) / N,
+    indices mod N. The dropped second-order term is below 1e-13 max|S| at N = 12.6 M (numpy
+    check: the first-order form is within 3e-12 of the exact DFT form at N = 1e6, falling as
+    1/N^2). The correction term is itself ~1e-6 of max|S|, so C needs ~3 significant digits: it
+    is a zero-padded linear convolution on power-of-two FFTs of M >= 2N - 1 points in complex64
+    (S scaled by 1/max|S|), i.e. two rocFFT transforms of 2^25 points per waveform at N = 12.6 M
+    instead of the two Bluestein transforms of 2^25 points *each* that the size-N DFTs take."""
+
+    def __init__(self, n, device):
+        torch = require_gpu()
+        self.n = n = int(n)
+        self.m = 1 << (2 * n - 2).bit_length()          # power of two >= 2 n - 1
+        self.eps = 1.0 / (n - 1)
+        lag = torch.arange(-(n - 1), n, device=device, dtype=torch.int64)
+        mm = torch.remainder(lag, n).to(torch.float64)
+        zero = mm == 0
+        re = torch.where(zero, torch.zeros_like(mm), (np.pi / n) / torch.tan(np.pi * mm / n))
+        im = torch.where(zero, torch.full_like(mm, np.pi * (n - 1) / n),
+                         torch.full_like(mm, -np.pi / n))
+        k = torch.complex(re, im)
+        kp = torch.zeros(self.m, dtype=torch.complex128, device=device)
+        kp[:2 * n - 1] = k
+        self.kf = torch.fft.fft(kp).to(torch.complex64)   # lag t sits at t + n - 1
+        self.device = device
+
+    @staticmethod
+    def matches(window):
+        """Whether window is scipy.signal.windows.hann(len(window)) (the reference's)."""
+        from scipy.signal.windows import hann
+        w = np.asarray(window.cpu().numpy() if hasattr(window, "detach") else window)
+        return w.ndim == 1 and len(w) >= 3 and np.array_equal(w, hann(len(w)))
+
+    def _scaled_correction(self, S):
+        """(c, scale): c = (K (*) S) / scale in complex64, rows along the last axis, with C[k] at
+        c[..., n - 1 + k]; scale = max|S| per row (device tensor [..., 1]). The padded input
+        buffer is kept per row count (its tail stays zero)."""
+        torch = require_gpu()
+        n, m = self.n, self.m
+        shape = S.shape[:-1] + (m,)
+        y = getattr(self, "_y", None)
+        if y is None or tuple(y.shape) != tuple(shape) or y.device != S.device:
+            y = self._y = torch.zeros(shape, dtype=torch.complex64, device=S.device)
+        scale = S.abs().amax(dim=-1, keepdim=True).clamp_min(1e-300)
+        y[..., :n].copy_(S)                       # complex128 -> complex64 (spectra ~1e-20)
+        y[..., :n].mul_((1.0 / scale).to(torch.float32))
+        Y = torch.fft.fft(y, dim=-1)
+        Y.mul_(self.kf)
+        return torch.fft.ifft(Y, dim=-1), scale
+
+    def correction(self, S):
+        """C = K (*) S (complex128, rows of S along the last axis)."""
+        torch = require_gpu()
+        c, scale = self._scaled_correction(S)
+        return c[..., self.n - 1:2 * self.n - 1].to(torch.complex128) * scale
+
+    def polarizations(self, S, hp, hc, k0, lib):
+        """h+/hx over bins [k0, n) of the windowed S (one row) into hp, hc
+        (efd_hann_polarizations: the stencil and the split in one pass)."""
+        from . import _lib
+        torch = require_gpu()
+        c, scale = self._scaled_correction(S)
+        st = torch.cuda.current_stream(S.device).cuda_stream
+        _lib.check(lib.efd_hann_polarizations(
+            torch.view_as_real(S).data_ptr(), torch.view_as_real(c[self.n - 1:]).data_ptr(),
+            scale.data_ptr(), self.n, k0, torch.view_as_real(hp).data_ptr(),
+            torch.view_as_real(hc).data_ptr(), st), "efd_hann_polarizations", lib)
+        return hp, hc
+
+    def __call__(self, S):
+        torch = require_gpu()
+        C = self.correction(S)
+        Sp, Sm = torch.roll(S, -1, dims=-1), torch.roll(S, 1, dims=-1)
+        Cd = torch.roll(C, -1, dims=-1) - torch.roll(C, 1, dims=-1)
+        return 0.5 * S - 0.25 * (Sp + Sm) - (0.25 * self.eps) * Cd
+
+
 def windowed_spectrum(S, mult):
     """The two-sided spectrum S = h+ - i hx (rows: one waveform each) convolved with the
     window: ifft(mult * fft(S)) along the last axis (rocFFT, batched over rows).
@@ -134,6 +219,10 @@ class get_fd_waveform_fromFD:
         self.window_in_fd = window_in_fd
         self.dt = dt
         self._mult = None if window is None else window_multiplier(window, window_in_fd)
+        # the reference's own window (hann(N), emri_pe.py:261) takes HannConvolution
+        self._hann = (HannConvolution(len(window), dev)
+                      if window is not None and not window_in_fd and HannConvolution.matches(window)
+                      else None)
         # contiguous-suffix mask (f >= 0 of a sorted grid): the fused fill path applies
         pm = self.positive_frequency_mask
         k0 = int(torch.argmax(pm.to(torch.int8)).item()) if bool(pm.any()) else int(pm.numel())
@@ -220,6 +309,10 @@ class get_fd_waveform_fromFD:
         cw = gen.waveform_generator.create_waveform
         if self._suffix_k0 != cw.positive_start():
             raise ValueError("positive_frequency_mask does not match the generator's grid")
+        if self._hann is not None:
+            self._hann.polarizations(S.contiguous(), out[0], out[1], self._suffix_k0,
+                                     cw.engine.lib)
+            return out
         cw.polarizations(windowed_spectrum(S, self._mult), True, out=(out[0], out[1]))
         return out
 

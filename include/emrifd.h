@@ -291,6 +291,21 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
                       void* stream);
 
 /*
+ * The h+/hx of efd_polarizations for the spectrum convolved with the reference's Hann window
+ * (FDutils.py:66-101 get_fd_windowed with emri_pe.py:261's scipy hann(nf), sym=True), without
+ * size-nf DFTs: the windowed spectrum is
+ *   S_w[k] = S[k]/2 - (S[k+1] + S[k-1])/4 - c (C[k+1] - C[k-1]),   indices mod nf,
+ * C = K (*) S the circular convolution with K[m] = -i pi/nf + (pi/nf) cot(pi m/nf),
+ * K[0] = i pi (nf-1)/nf (the derivative of the DFT's trigonometric interpolant), c =
+ * (*cscale) / (4 (nf - 1)); the caller computes C (rocFFT, zero-padded power-of-two linear
+ * convolution; fdutils.HannConvolution). S complex128 [nf]; C complex64 [nf] (the caller's C
+ * divided by *cscale); cscale one device double. Writes bins [k0, nf) into hp, hc.
+ * Replaces: no reference function (the reference convolves each channel with scipy/cupy).
+ */
+int efd_hann_polarizations(const double* S, const float* C, const double* cscale, int64_t nf,
+                           int64_t k0, double* hp, double* hc, void* stream);
+
+/*
  * Fused Gaussian log-likelihood over nchan channels of nbin bins each:
  *   out = -1/2 * 4 * sum_c sum_k | d[c][k] - h[c][k] * w[c][k] |^2
  * (likelihood.py:257-274 with noise factor w = sqrt(df/S) built at likelihood.py:213-220).
