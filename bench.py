@@ -59,7 +59,7 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector FP64 peak (AMD spec: 256 CUs x 12
 
 
 def build_workload(T=2.0, dt=10.0, eps=1e-5, M=1e6, mu=10.0, e0=0.35, theta=np.pi / 3,
-                   phi=-np.pi / 2, dist=1.0):
+                   phi=-np.pi / 2, dist=1.0, p0=None, Phi_phi0=0.0, Phi_r0=0.0):
     from emri_frequencydomainwaveforms_amd.amplitude import ModeSelector, SyntheticTeukolskyAmplitude
     from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI, MTSUN_SI
     from emri_frequencydomainwaveforms_amd.frequencies import get_fundamental_frequencies
@@ -68,8 +68,9 @@ def build_workload(T=2.0, dt=10.0, eps=1e-5, M=1e6, mu=10.0, e0=0.35, theta=np.p
     from emri_frequencydomainwaveforms_amd.ylm import GetYlms
 
     traj = EMRIInspiral()
-    p0 = get_p_at_t(traj, 0.99 * T, [M, mu, 0.0, e0, 1.0])
-    t, p, e, x, pp, pt, pr = traj(M, mu, 0.0, p0, e0, 1.0, T=T)
+    if p0 is None:
+        p0 = get_p_at_t(traj, 0.99 * T, [M, mu, 0.0, e0, 1.0])
+    t, p, e, x, pp, pt, pr = traj(M, mu, 0.0, p0, e0, 1.0, Phi_phi0=Phi_phi0, Phi_r0=Phi_r0, T=T)
     amp = SyntheticTeukolskyAmplitude()
     A = amp(p, e)
     ylms = GetYlms(assume_positive_m=True)(amp.l_arr, amp.m_arr, theta, phi)
@@ -81,10 +82,35 @@ def build_workload(T=2.0, dt=10.0, eps=1e-5, M=1e6, mu=10.0, e0=0.35, theta=np.p
                 m=amp.m_arr[keep].astype(np.int32), n=amp.n_arr[keep].astype(np.int32),
                 ylm_p=ylms[:Kall][keep], ylm_m=ylms[Kall:][keep],
                 prefactor=mu * MRSUN_SI / (dist * Gpc), freq=fd_grid(T, dt),
-                params=dict(M=M, mu=mu, p0=float(p0), e0=e0, T=T, dt=dt, eps=eps))
+                params=dict(M=M, mu=mu, p0=float(p0), e0=e0, T=T, dt=dt, eps=eps,
+                            Phi_phi0=Phi_phi0, Phi_r0=Phi_r0))
 
 
-def fp64_roofline(B, n_eval, kern_ms, caustic):
+def build_workloads(B, T=2.0, dt=10.0, eps=1e-5, sources="walkers", seed=2601996):
+    """B config-2 sources: the source itself, then (sources="walkers") B - 1 draws of emri_pe.py's
+    walker start around it, multivariate_normal(truth, cov(covariance.npy) / (2.4 * 6)) in
+    (ln M, ln(mu/M), p0, e0, Phi_phi0, Phi_r0) (emri_pe.py:437-444; the covariance is the
+    package's data/walker_cov.npy, numpy's Generator with the reference's seed): distinct
+    waveforms, each with its own trajectory, harmonic selection and records, as a walker batch
+    of the sampler is. sources="same": B copies of the source (rounds 1-3's headline)."""
+    w0 = build_workload(T=T, dt=dt, eps=eps)
+    if sources == "same" or B == 1:
+        return [w0] * B
+    from emri_frequencydomainwaveforms_amd import pe
+    P = w0["params"]
+    truth6 = np.array([np.log(P["M"]), np.log(P["mu"] / P["M"]), P["p0"], P["e0"], 0.0, 0.0])
+    cov = np.load(pe._COV, allow_pickle=False) / (2.4 * 6)
+    draws = np.random.default_rng(seed).multivariate_normal(truth6, cov, size=B - 1)
+    out = [w0]
+    for lnM, lnq, p0, e0, pp0, pr0 in draws:
+        M = float(np.exp(lnM))
+        out.append(build_workload(T=T, dt=dt, eps=eps, M=M, mu=float(M * np.exp(lnq)),
+                                  e0=float(e0), p0=float(p0), Phi_phi0=float(pp0),
+                                  Phi_r0=float(pr0)))
+    return out
+
+
+def fp64_roofline(B, n_eval, kern_ms, caustic, sources="walkers"):
     """FP64 VALU roofline of the mode-sum kernel: FLOP per launch from the committed rocprofv3
     PMC pass (profiles/pmc_traffic.json, written by tools/summarize_profiles.py: FP64 FMA counts
     2, MUL/ADD/TRANS 1, times 64 lanes x measured lane utilisation), taken per SPA evaluation and
@@ -107,13 +133,14 @@ def fp64_roofline(B, n_eval, kern_ms, caustic):
             return out
         src = os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc", "emrifd.hip")
         sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
-        flops = fpe * n_eval * B
+        flops = fpe * n_eval   # n_eval: the launch's SPA evaluations (all B waveforms)
         tf = flops / (kern_ms * 1e-3) / 1e12
         out.update(achieved=tf, frac=tf / FP64_VALU_PEAK_TFLOPS,
                    flops_per_launch=flops, flops_per_evaluation=fpe,
                    valu_busy=f.get("valu_busy"),
                    pmc_source=pj.get("source"), pmc_matches_build=pj.get("src_sha16") == sha)
-        if int(pj.get("batch", 1)) == B and pj.get("workload") == "config2":
+        if (int(pj.get("batch", 1)) == B and pj.get("workload") == "config2"
+                and pj.get("sources", "same") == sources):
             out["traffic"] = pj.get("hbm_bytes_per_launch")
     except (ValueError, OSError, KeyError, TypeError):
         pass
@@ -248,6 +275,9 @@ def main():
     ap.add_argument("--caustic", default="uniform", choices=["uniform", "spa"])
     ap.add_argument("--T", type=float, default=2.0)
     ap.add_argument("--eps", type=float, default=1e-5)
+    ap.add_argument("--sources", default="walkers", choices=["walkers", "same"],
+                    help="the B waveforms of a step: distinct sources from emri_pe.py's walker "
+                         "start around config 2's (default), or B copies of config 2's source")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pipeline", default="overlap", choices=["overlap", "serial"],
@@ -304,16 +334,24 @@ def main():
     from emri_frequencydomainwaveforms_amd.summation import (DeviceInputs, ModeSumEngine,
                                                              prepare_batch, sum_batch)
 
-    w = build_workload(T=args.T, eps=args.eps)
-    inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"],
-                                 w["f_r"], w["m"], w["n"], w["ylm_p"], w["ylm_m"], device=dev)
-    freq = torch.as_tensor(w["freq"], device=dev)
-    nf = int(freq.numel())
-    k0 = int(np.searchsorted(w["freq"], 0.0))
     overlap = args.pipeline == "overlap"
     B = args.batch if overlap else 1
     if not 1 <= B <= _lib.EFD_BATCH_MAX:
         raise SystemExit(f"--batch must be in [1, {_lib.EFD_BATCH_MAX}]")
+    ws = build_workloads(B, T=args.T, eps=args.eps, sources=args.sources)
+    w = ws[0]
+    inps = []
+    for wj in ws:
+        if inps and wj is ws[0]:
+            inps.append(inps[0])
+            continue
+        inps.append(DeviceInputs.from_host(wj["t"], wj["amp"], wj["phi_phi"], wj["phi_r"],
+                                           wj["f_phi"], wj["f_r"], wj["m"], wj["n"], wj["ylm_p"],
+                                           wj["ylm_m"], device=dev))
+    inp = inps[0]
+    freq = torch.as_tensor(w["freq"], device=dev)
+    nf = int(freq.numel())
+    k0 = int(np.searchsorted(w["freq"], 0.0))
     # Slots of B waveforms (a workspace + h+/hx outputs each). "overlap": batch i+1's
     # preparation (grouping, splines, records: latency-bound kernels on few CUs) runs on the prep
     # stream while batch i's mode sums run on the sum stream, all B in one launch
@@ -345,12 +383,13 @@ def main():
                 if sl["sum_done"] is not None:    # the slot's previous sums have read it
                     s_prep.wait_event(sl["sum_done"])
                 if args.prep == "batch":
-                    prepare_batch([(x["eng"], dict(inp=inp, freq=freq, out=None,
-                                                   grid_symmetric=True, scale=w["prefactor"]))
-                                   for x in sl["wf"]], stream=s_prep.cuda_stream)
+                    prepare_batch([(x["eng"], dict(inp=inps[j], freq=freq, out=None,
+                                                   grid_symmetric=True,
+                                                   scale=ws[j]["prefactor"]))
+                                   for j, x in enumerate(sl["wf"])], stream=s_prep.cuda_stream)
                 else:
-                    for x in sl["wf"]:
-                        x["eng"].launch(inp, freq, None, True, w["prefactor"],
+                    for j, x in enumerate(sl["wf"]):
+                        x["eng"].launch(inps[j], freq, None, True, ws[j]["prefactor"],
                                         stream=s_prep.cuda_stream, phase="prepare")
                 sl["prep_done"].record(s_prep)
                 ss.wait_event(sl["prep_done"])
@@ -359,9 +398,9 @@ def main():
                 x["eng"].launch(inp, freq, None, True, w["prefactor"], stream=ss.cuda_stream,
                                 prof_events=pe, hp=x["fhp"], hc=x["fhc"], k0=k0, phase="sum")
             else:
-                sum_batch([(x["eng"], dict(inp=inp, freq=freq, out=None, grid_symmetric=True,
-                                           scale=w["prefactor"], hp=x["fhp"], hc=x["fhc"],
-                                           k0=k0)) for x in sl["wf"]],
+                sum_batch([(x["eng"], dict(inp=inps[j], freq=freq, out=None, grid_symmetric=True,
+                                           scale=ws[j]["prefactor"], hp=x["fhp"], hc=x["fhc"],
+                                           k0=k0)) for j, x in enumerate(sl["wf"])],
                           stream=ss.cuda_stream, prof_events=pe)
             done = torch.cuda.Event()
             done.record(ss)
@@ -403,7 +442,11 @@ def main():
     # its preparation and for the launch): what the pipeline loses beside the kernel itself
     gaps = [evs[i][1].elapsed_time(evs[i + 1][0]) for i in range(len(evs) - 1)]
     gap_ms = float(np.mean(gaps)) if gaps else 0.0
-    C, n_eval, n_groups = slots[0]["wf"][0]["eng"].stats(s_sum.cuda_stream)
+    # contributions, SPA evaluations and (m, n) groups of one launch (the B waveforms of a slot)
+    st_all = [x["eng"].stats(s_sum.cuda_stream) for x in slots[0]["wf"]]
+    C = sum(s_[0] for s_ in st_all)
+    n_eval = sum(s_[1] for s_ in st_all)
+    n_groups = [s_[2] for s_ in st_all]
 
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -411,15 +454,16 @@ def main():
         elapsed, kern_ms = float(tt[0]), float(tt[1])
 
     if rank == 0:
-        K = int(len(w["m"]))
-        nt = int(len(w["t"]))
-        n_interp = 2 * K + 4
-        b_alg = 32.0 * C + 32.0 * n_interp * nt + 16.0 * nf
+        Ks = [int(len(wj["m"])) for wj in ws]
+        nts = [int(len(wj["t"])) for wj in ws]
+        # SURVEY 8(d)'s algorithmic bytes of the launch's B waveforms (C summed over them)
+        b_alg = 32.0 * C + sum(32.0 * (2 * K_ + 4) * nt_ for K_, nt_ in zip(Ks, nts)) \
+            + 16.0 * nf * B
         wf_ms = kern_ms / B   # one launch sums B waveforms
         # SURVEY 8(d)'s scatter-formulation bytes: a secondary figure, never the roofline (the
         # output-stationary kernel never makes those accesses, so it exceeds HBM "peak")
-        scatter_gbs = B * b_alg / (kern_ms * 1e-3) / 1e9
-        roof = fp64_roofline(B, n_eval, kern_ms, args.caustic)
+        scatter_gbs = b_alg / (kern_ms * 1e-3) / 1e9
+        roof = fp64_roofline(B, n_eval, kern_ms, args.caustic, args.sources)
         cpu = cpu_ref = api = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -451,8 +495,11 @@ def main():
             "data": "synthetic (stand-in trajectory/amplitudes; FEW data absent offline)",
             "config": {"workload": "config2: M=1e6 mu=10 e0=0.35 Tobs=2yr dt=10s eps=1e-5 "
                                    f"caustic={args.caustic}",
-                       "harmonics": K, "mn_groups": n_groups, "N_t": nt, "N_f": nf,
-                       "contributions": C, "spa_evaluations": n_eval,
+                       "sources": ("config 2's source + emri_pe walker-start draws "
+                                   "(emri_pe.py:437-444)" if args.sources == "walkers"
+                                   else "B copies of config 2's source"),
+                       "harmonics": Ks, "mn_groups": n_groups, "N_t": nts, "N_f": nf,
+                       "contributions_per_launch": C, "spa_evaluations_per_launch": n_eval,
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
                        "pipeline": args.pipeline + (" (diagnostic: sum only)"
                                                     if args.diag_sum_only else ""),
@@ -464,8 +511,8 @@ def main():
                 "waveforms_per_launch": B,
                 "kernel_timing": "HIP events around each k_modesum launch in the timed region "
                                  "(sum stream), mean",
-                "spa_evaluations_per_s": n_eval / (wf_ms * 1e-3),
-                "contributions_per_s": C / (wf_ms * 1e-3),
+                "spa_evaluations_per_s": n_eval / (kern_ms * 1e-3),
+                "contributions_per_s": C / (kern_ms * 1e-3),
                 "scatter_equiv_gbs": scatter_gbs,
                 "scatter_equiv_note": "SURVEY 8(d) B_alg = 32 C + 32 n_interp N_t + 16 N_f per "
                                       "waveform / kernel time: the reference scatter "

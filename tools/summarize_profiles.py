@@ -86,13 +86,19 @@ def main(tag):
                "bench_event_ms": bench["roofline"]["kernel_ms"]}
     json.dump(summary, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     # FP64 FLOP per SPA evaluation (bench.py scales it to its own run's evaluation count)
-    evals = float(bench["config"].get("spa_evaluations", 0)) * batch
+    cfg = bench["config"]
+    evals = (float(cfg["spa_evaluations_per_launch"]) if "spa_evaluations_per_launch" in cfg
+             else float(cfg.get("spa_evaluations", 0)) * batch)
+    sources = "walkers" if "walker" in str(cfg.get("sources", "")) else "same"
+    summary["sources"] = sources
+    json.dump(summary, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     if fp64 and evals > 0:
         fp64["flops_per_evaluation"] = fp64["flops_per_launch"] / evals
     import hashlib
     src_sha = hashlib.sha256(open(os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc",
                                                "emrifd.hip"), "rb").read()).hexdigest()[:16]
     json.dump({"workload": "config2", "caustic": "uniform", "kernel": kernel, "batch": batch,
+               "sources": sources,
                "hbm_bytes_per_launch": hbm, "fp64": fp64, "evaluations_per_launch": evals,
                "src_sha16": src_sha, "source": f"profiles/{tag}_pmc.json"},
               open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
