@@ -60,7 +60,13 @@ namespace {
 constexpr int TILE = 256;           // threads per workgroup in k_modesum (round 2: 512-thread
                                     // tiles of 8 waves ran 0.974x)
 constexpr int NWAVE = TILE / 64;    // waves per workgroup
-constexpr int BPL = 2;              // bins (lanes) per thread in k_modesum (3 or 4: +3-5%)
+#ifndef EFD_BPL
+#define EFD_BPL 2
+#endif
+#ifndef EFD_SPLIT_B
+#define EFD_SPLIT_B 0
+#endif
+constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum (3 or 4: +3-5%)
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
@@ -2663,6 +2669,29 @@ __device__ __forceinline__ void modesum_tile(
                         needany |= needm[i];
                     }
                     anyneed = needany != 0;
+#if EFD_SPLIT_B
+                    // the own bins' amplitude cubics (b[0], 16 VGPRs) first, then the mirrors'
+                    // (b[1], read after a compiler fence so they can reuse the registers)
+#pragma unroll
+                    for (int i = 0; i < BPL; ++i) {
+                        const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
+                        own_r[i] = fma(xr, wr[i], own_r[i]);
+                        own_r[i] = fma(-xi, wi[i], own_r[i]);
+                        own_i[i] = fma(xr, wi[i], own_i[i]);
+                        own_i[i] = fma(xi, wr[i], own_i[i]);
+                    }
+                    if (PAIRED) {
+                        asm volatile("" ::: "memory");
+#pragma unroll
+                        for (int i = 0; i < BPL; ++i) {
+                            const double zr = cubic(xm, w[i]), zi = cubic(xm + 4, w[i]);
+                            mir_r[i] = fma(zr, wr[i], mir_r[i]);
+                            mir_r[i] = fma(-zi, wi[i], mir_r[i]);
+                            mir_i[i] = fma(-zr, wi[i], mir_i[i]);
+                            mir_i[i] = fma(-zi, wr[i], mir_i[i]);
+                        }
+                    }
+#else
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
@@ -2671,6 +2700,7 @@ __device__ __forceinline__ void modesum_tile(
                         accumulate<0, PAIRED>(wr[i], wi[i], xr, xi, zr, zi, own_r[i], own_i[i],
                                               mir_r[i], mir_i[i]);
                     }
+#endif
                     if (__builtin_expect(anyneed, 0)) {   // cold: general path, some lanes
 #ifdef EFD_EXP
                         {

@@ -157,6 +157,21 @@ class HannConvolution:
         c, scale = self._scaled_correction(S)
         return c[..., self.n - 1:2 * self.n - 1].to(torch.complex128) * scale
 
+    def polarizations_batch(self, S, outs, k0, lib):
+        """polarizations for every row of S ([B][n], contiguous): one batched transform pair
+        (rocFFT over the rows) and one efd_hann_polarizations per row into outs[i] = (hp, hc)."""
+        from . import _lib
+        torch = require_gpu()
+        c, scale = self._scaled_correction(S)
+        st = torch.cuda.current_stream(S.device).cuda_stream
+        for i, (hp, hc) in enumerate(outs):
+            _lib.check(lib.efd_hann_polarizations(
+                torch.view_as_real(S[i]).data_ptr(),
+                torch.view_as_real(c[i, self.n - 1:]).data_ptr(), scale[i].data_ptr(), self.n,
+                k0, torch.view_as_real(hp).data_ptr(), torch.view_as_real(hc).data_ptr(), st),
+                "efd_hann_polarizations", lib)
+        return outs
+
     def polarizations(self, S, hp, hc, k0, lib):
         """h+/hx over bins [k0, n) of the windowed S (one row) into hp, hc
         (efd_hann_polarizations: the stencil and the split in one pass)."""
@@ -292,6 +307,44 @@ class get_fd_waveform_fromFD:
         ahead of the per-walker submit/fill calls; a no-op for other generators."""
         fn = getattr(self.waveform_generator, "prefetch", None)
         return fn(params, **kwargs) if fn is not None and not args else 0
+
+    # walkers per windowed group (fill_batch): their spectra share one batched transform pair
+    WINDOW_GROUP = 8
+
+    @property
+    def can_fill_batch(self):
+        return self._hann is not None and self._windowed_s_path()
+
+    def fill_batch(self, outs, params, **kwargs):
+        """fill for a batch of walkers (rows of params, FEW's 14) into outs[i] (complex128
+        [2][num_bins] each): every walker's spectrum queued into one [B][N] buffer without a
+        synchronisation, then the Hann window for all of them (one batched transform pair,
+        HannConvolution.polarizations_batch). Same values as B fill calls up to the batched
+        transform's rounding (the correction term carries ~1e-6 of max|S|; it enters at
+        <= 1e-12). The engine's device-side status is checked once, at the end."""
+        torch = require_gpu()
+        if not self.can_fill_batch:
+            raise ValueError("fill_batch: the Hann-window spectrum path only")
+        gen = self.waveform_generator
+        B = len(params)
+        if B == 0:
+            return outs
+        n = int(self.positive_frequency_mask.numel())
+        dev = self.positive_frequency_mask.device
+        buf = getattr(self, "_sbuf", None)
+        if buf is None or buf.shape[0] < B or buf.shape[1] != n:
+            buf = self._sbuf = torch.empty((B, n), dtype=torch.complex128, device=dev)
+        for i, p in enumerate(params):
+            gen._spectrum(*p, out=buf[i], check=False, **kwargs)
+        cw = gen.waveform_generator.create_waveform
+        if self._suffix_k0 != cw.positive_start():
+            raise ValueError("positive_frequency_mask does not match the generator's grid")
+        self._hann.polarizations_batch(buf[:B], [(o[0], o[1]) for o in outs], self._suffix_k0,
+                                       cw.engine.lib)
+        if not cw.engine.status():
+            from . import _lib
+            raise _lib.EFDError(f"efd_modesum: {_lib.last_error(cw.engine.lib)}")
+        return outs
 
     def fill(self, out, *args, **kwargs):
         """Write [ch1, ch2] into out (complex128 [2][num_bins], device) without copies.

@@ -991,8 +991,10 @@ class FDInterpolatedModeSum:
         return slot
 
     def spectrum(self, t, teuk_modes, ylm_p, ylm_m, Phi_phi, Phi_r, m_arr, n_arr, M, p, e,
-                 dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j, f_phi=None, f_r=None):
-        """S(f) = h+ - i hx on the grid (torch complex128 on the GPU). f_phi, f_r: the orbital
+                 dt=10.0, T=1.0, f_arr=None, scale=1.0 + 0.0j, f_phi=None, f_r=None, out=None,
+                 check=True):
+        """S(f) = h+ - i hx on the grid (torch complex128 on the GPU; into out when given;
+        check=False: no status synchronisation, see ModeSumEngine.run). f_phi, f_r: the orbital
         frequencies at the knots when the upstream already has them (the native trajectory),
         else FEW's get_fundamental_frequencies(p, e) (the same values submit_channels uses, so
         an injection and a walker on the same parameters give bitwise the same template)."""
@@ -1003,7 +1005,7 @@ class FDInterpolatedModeSum:
         inp = DeviceInputs.from_host(t, teuk_modes, Phi_phi, Phi_r, f_phi, f_r, m_arr, n_arr,
                                      ylm_p, ylm_m)
         freq, sym = self._grid(T, dt, f_arr)
-        return self.engine.run(inp, freq, grid_symmetric=sym, scale=scale)
+        return self.engine.run(inp, freq, out=out, grid_symmetric=sym, scale=scale, check=check)
 
     def positive_start(self):
         """Index of the first f >= 0 bin of the last grid (emri_pe.py:239 mask, sorted grid);

@@ -212,9 +212,11 @@ class FastSchwarzschildEccentricFlux:
 
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
-                 extra_scale=1.0 + 0.0j, **kwargs):
+                 extra_scale=1.0 + 0.0j, out=None, check=True, **kwargs):
         """Complex FD spectrum S = h+ - i hx (torch, on the GPU), distance-scaled; for
-        output_type "td" the complex time series h = h+ - i hx instead."""
+        output_type "td" the complex time series h = h+ - i hx instead. FD: out (complex128
+        [N_f] on the device) receives S; check=False queues without the status
+        synchronisation (the caller reads the engine's status later)."""
         require_gpu()
         if self.output_type == "td":
             return self.time_series(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, dt, T,
@@ -226,7 +228,8 @@ class FastSchwarzschildEccentricFlux:
         return self.create_waveform.spectrum(d["t"], d["teuk"], d["ylms"][:K], d["ylms"][K:],
                                              d["Phi_phi"], d["Phi_r"], d["m"], d["n"], M, d["p"],
                                              d["e"], dt=dt, T=T, f_arr=f_arr, scale=scale,
-                                             f_phi=d["f_phi"], f_r=d["f_r"])
+                                             f_phi=d["f_phi"], f_r=d["f_r"], out=out,
+                                             check=check)
 
     def submit_channels(self, pipeline, out, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0,
                         Phi_r0=0.0, dt=10.0, T=1.0, eps=1e-5, mode_selection=None,

@@ -62,6 +62,14 @@ def test_windowed_likelihood_test_sh_full_grid():
     assert np.array_equal(like(batch, **s.kwargs), ll)                 # repeatable
     assert like(s.truth6[None, :], **s.kwargs)[0] == 0.0              # injectFD: exact zero
     assert np.all(ll < 0.0)
+    # the batched window (groups of WINDOW_GROUP spectra, one transform pair) against one
+    # walker at a time: the batched transform's rounding only
+    gen.WINDOW_GROUP = 1
+    try:
+        ll1 = like(batch, **s.kwargs)
+    finally:
+        del gen.WINDOW_GROUP
+    np.testing.assert_allclose(ll1, ll, rtol=1e-12, atol=0.0)
 
     f = s.f_like
     w = lo.noise_factor(f, [get_sensitivity(f)] * 2)
