@@ -46,7 +46,10 @@ EXPORTED_SYMBOLS = (
     "efd_download",
     "efd_stream_order",
     "efd_polarizations",
+    "efd_hann_extent",
+    "efd_hann_stage",
     "efd_hann_polarizations",
+    "efd_hann_loglike",
     "efd_loglike",
     "efd_inner_product",
     "efd_modesum_cpu",
@@ -215,8 +218,14 @@ def load(path=None):
         lib.efd_stream_order.argtypes = [vp, ctypes.POINTER(vp), i32]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
+    lib.efd_hann_extent.restype = ctypes.c_int
+    lib.efd_hann_extent.argtypes = [vp, i64, i64, i32, vp, vp]
+    lib.efd_hann_stage.restype = ctypes.c_int
+    lib.efd_hann_stage.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp]
     lib.efd_hann_polarizations.restype = ctypes.c_int
-    lib.efd_hann_polarizations.argtypes = [vp, vp, vp, i64, i64, vp, vp, vp]
+    lib.efd_hann_polarizations.argtypes = [vp, vp, vp, i64, i64, i64, vp, vp, vp]
+    lib.efd_hann_loglike.restype = ctypes.c_int
+    lib.efd_hann_loglike.argtypes = [vp, i64, vp, vp, i64, i32, i64, i64, vp, vp, vp, vp, vp]
     lib.efd_loglike.restype = ctypes.c_int
     lib.efd_loglike.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
     lib.efd_inner_product.restype = ctypes.c_int

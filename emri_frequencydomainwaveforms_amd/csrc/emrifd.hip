@@ -542,6 +542,9 @@ __device__ __forceinline__ void group_body(const int32_t* __restrict__ marr,
         hdr->groups = 0;
         hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
         hdr->lane_hi = INT32_MIN;
+#ifdef EFD_PERSIST
+        hdr->pad[0] = 0;            // k_modesum_batch's persistent tile counter (two int32)
+#endif
         if (!init) {
             hdr->runs_overflow = 0;
             hdr->bad_mn = 0;
@@ -2301,7 +2304,8 @@ __device__ __forceinline__ void modesum_tile(
     // every walker (efd_loglike_tile_constants); NULL: such tiles compute it
     const double* __restrict__ llconst,
     int64_t b,     // b: this workgroup's place in the waveform's dispatch order
-    bool direct = false) {   // b is the tile itself (k_modesum_batch's sparse form)
+    bool direct = false,     // b is the tile itself (k_modesum_batch's sparse form)
+    bool* tab_loaded = nullptr) {   // persistent workgroups: the sin/cos table is in LDS already
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -2380,10 +2384,13 @@ __device__ __forceinline__ void modesum_tile(
                            reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
             }
         }
+        if (tab_loaded == nullptr || !*tab_loaded) {
 #pragma unroll
-        for (int rd = 0; rd < SCTAB / TILE; ++rd)
-            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
-                   reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
+            for (int rd = 0; rd < SCTAB / TILE; ++rd)
+                glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
+                       reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
+            if (tab_loaded != nullptr) *tab_loaded = true;
+        }
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
         __syncthreads();
     }
@@ -2948,6 +2955,45 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
         d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld, llw, d.llpart, llconst, pos);
 }
 
+#ifdef EFD_PERSIST
+// The dense batch in persistent form: one workgroup per resident slot takes (waveform, place)
+// items in dispatch order from a counter in waveform 0's header (k_group zeroes it, the last
+// workgroup to finish resets it); the sin/cos table (the same bits in every waveform's workspace)
+// comes into LDS once per workgroup instead of once per tile.
+template <bool PAIRED, int CAUSTIC, int BPL>
+__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
+void k_modesum_persist(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t ntiles,
+                       int accumulate_out) {
+    const int n = batch.n;
+    int32_t* ctr = reinterpret_cast<int32_t*>(&batch.d[0].hdr->pad[0]);
+    const int64_t gq = 8 * XCD_GROUP, ngrid = (ntiles + gq - 1) / gq * gq;
+    const int64_t total = ngrid * n;
+    __shared__ int32_t s_item;
+    bool tl = false;
+    while (true) {
+        if (threadIdx.x == 0) s_item = atomicAdd(ctr, 1);
+        __syncthreads();
+        const int64_t item = s_item;
+        if (item >= total) break;
+        const int wv = (int)(item % n);
+        const BatchDesc& e = batch.d[wv];
+        modesum_tile<PAIRED, CAUSTIC, BPL>(
+            e.items, e.ranges, e.seglh, e.seginfo, e.nseg, e.freq, nf, nlanes, ntiles, e.nt,
+            e.K, e.gm, e.gn, e.t, e.coefA, e.coefT, e.sctab, e.tkeys, e.tcnt, e.tperm,
+            e.segbase, e.stb0, e.stb1, e.hdr, accumulate_out, e.out, e.hp, e.hc, e.k0,
+            nullptr, nullptr, nullptr, nullptr, item / n, false, &tl);
+        __syncthreads();   // s_item and the LDS stages reused by the next item
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(ctr + 1, 1) == (int)gridDim.x - 1) {
+            atomicExch(ctr, 0);
+            atomicExch(ctr + 1, 0);
+        }
+    }
+}
+#endif
+
 // The fused likelihood's partial of a tile whose waveform has no record on it (every bin's
 // h = 0): modesum_tile's epilogue with zero accumulators, the same operations in the same order,
 // so a tile that takes it (llconst) gives bitwise what computing it would. Depends on the grid
@@ -3493,27 +3539,155 @@ __global__ void k_polarizations(const double2* __restrict__ S, int64_t nf, int64
     hc[i] = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
 }
 
-// h+/hx of the Hann-windowed spectrum (efd_hann_polarizations): S_w at k and at its mirror
-// nf - 1 - k from S and the complex64 correction C (neighbours mod nf), then the split
+// ---- The Hann window's convolution (fdutils.HannConvolution; efd_hann_*). A row's correction
+// C = K (*) S (circular, mod nf) is the linear convolution of the row's support [first, last) with
+// the lag kernel, on m-point transforms (m >= nf + (last - first) - 1): the caller's Y[s] holds
+// S[first + s] / scale for s < last - first, zero up to m (efd_hann_stage), and after its
+// transforms (the kernel's spectrum includes 1/m) C[k] = scale Y[((k - first) mod nf) + m - nf].
+// info[r] = {bits of scale = max(|Re|, |Im|), first nonzero bin, last nonzero bin + 1, 0}; a
+// NaN anywhere in the row makes the scale NaN (the bit pattern orders above every finite
+// value), so the row's outputs are NaN.
+__global__ void k_hann_info_init(uint64_t* __restrict__ info, int32_t rows) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    info[4 * r + 0] = 0;
+    info[4 * r + 1] = ~0ull;
+    info[4 * r + 2] = 0;
+    info[4 * r + 3] = 0;
+}
+__global__ __launch_bounds__(256) void k_hann_extent(const double2* __restrict__ S, int64_t stride,
+                                                     int64_t nf, uint64_t* __restrict__ info) {
+    const double2* row = S + (int64_t)blockIdx.y * stride;
+    uint64_t mx = 0, lo = ~0ull, hi = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nf;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const double2 v = row[k];
+        const uint64_t bx = (uint64_t)__double_as_longlong(fabs(v.x));
+        const uint64_t by = (uint64_t)__double_as_longlong(fabs(v.y));
+        mx = max(mx, max(bx, by));
+        if ((bx | by) != 0) {          // nonzero (or NaN)
+            lo = min(lo, (uint64_t)k);
+            hi = (uint64_t)k + 1;      // k grows along the thread's stride
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = max(mx, (uint64_t)__shfl_xor((unsigned long long)mx, o, 64));
+        lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, o, 64));
+        hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        uint64_t* in = info + 4 * blockIdx.y;
+        if (mx) atomicMax((unsigned long long*)&in[0], (unsigned long long)mx);
+        if (hi) {
+            atomicMin((unsigned long long*)&in[1], (unsigned long long)lo);
+            atomicMax((unsigned long long*)&in[2], (unsigned long long)hi);
+        }
+    }
+}
+struct HannRow {
+    int64_t first, len;
+    double scale;   // 0 for an all-zero row (its Y is zero)
+};
+__device__ __forceinline__ HannRow hann_row(const uint64_t* __restrict__ info, int r) {
+    HannRow h;
+    const uint64_t lo = info[4 * r + 1], hi = info[4 * r + 2];
+    h.first = hi ? (int64_t)lo : 0;
+    h.len = hi ? (int64_t)(hi - lo) : 0;
+    h.scale = __longlong_as_double((long long)info[4 * r + 0]);
+    return h;
+}
+__global__ __launch_bounds__(256) void k_hann_stage(const double2* __restrict__ S, int64_t stride,
+                                                    const uint64_t* __restrict__ info, int64_t m,
+                                                    float2* __restrict__ Y) {
+    const int r = blockIdx.y;
+    const HannRow h = hann_row(info, r);
+    const double2* row = S + (int64_t)r * stride + h.first;
+    float2* y = Y + (int64_t)r * m;
+    const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;   // NaN scale: NaN row
+    const bool bad = h.len > m;     // the host sized m from info: never, but never write past Y
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < m;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        float2 v = make_float2(0.f, 0.f);
+        if (bad) {
+            v = make_float2(__int_as_float(0x7fc00000), 0.f);
+        } else if (s < h.len) {
+            const double2 x = row[s];
+            v = make_float2((float)(x.x * inv), (float)(x.y * inv));
+        }
+        y[s] = v;
+    }
+}
+// S_w at bin k: the 3-point stencil on S and the correction's difference (neighbours mod nf)
 __device__ __forceinline__ double2 hann_sw(const double2* __restrict__ S,
-                                           const float2* __restrict__ C, int64_t nf, int64_t k,
-                                           double c) {
+                                           const float2* __restrict__ Y, int64_t nf, int64_t k,
+                                           double c, int64_t first, int64_t off) {
     const int64_t kp = k + 1 < nf ? k + 1 : 0, km = k > 0 ? k - 1 : nf - 1;
+    int64_t qp = kp - first, qm = km - first;
+    qp += qp < 0 ? nf : 0;
+    qm += qm < 0 ? nf : 0;
     const double2 s = S[k], sp = S[kp], sm = S[km];
-    const float2 cp = C[kp], cm = C[km];
+    const float2 cp = Y[qp + off], cm = Y[qm + off];
     return make_double2(0.5 * s.x - 0.25 * (sp.x + sm.x) - c * ((double)cp.x - (double)cm.x),
                         0.5 * s.y - 0.25 * (sp.y + sm.y) - c * ((double)cp.y - (double)cm.y));
 }
-__global__ void k_hann_polarizations(const double2* __restrict__ S, const float2* __restrict__ C,
-                                     const double* __restrict__ cscale, int64_t nf, int64_t k0,
-                                     double2* __restrict__ hp, double2* __restrict__ hc) {
+// h+ = (a + conj b)/2, hx = i (a - conj b)/2 of the windowed spectrum at k (a) and nf-1-k (b)
+__device__ __forceinline__ void hann_pol(const double2* __restrict__ S,
+                                         const float2* __restrict__ Y, int64_t nf, int64_t k,
+                                         double c, int64_t first, int64_t off, double2& vp,
+                                         double2& vc) {
+    const double2 a = hann_sw(S, Y, nf, k, c, first, off);
+    const double2 b = hann_sw(S, Y, nf, nf - 1 - k, c, first, off);
+    vp = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+    vc = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+}
+__global__ void k_hann_polarizations(const double2* __restrict__ S, const float2* __restrict__ Y,
+                                     const uint64_t* __restrict__ info, int64_t m, int64_t nf,
+                                     int64_t k0, double2* __restrict__ hp,
+                                     double2* __restrict__ hc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t k = k0 + i;
     if (k >= nf) return;
-    const double c = *cscale / (4.0 * (double)(nf - 1));
-    const double2 a = hann_sw(S, C, nf, k, c), b = hann_sw(S, C, nf, nf - 1 - k, c);
-    hp[i] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
-    hc[i] = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
+    const HannRow h = hann_row(info, 0);
+    const double c = h.scale / (4.0 * (double)(nf - 1));
+    double2 vp, vc;
+    hann_pol(S, Y, nf, k, c, h.first, m - nf, vp, vc);
+    hp[i] = vp;
+    hc[i] = vc;
+}
+// the windowed templates' log-likelihood partials, row blockIdx.y: efd_loglike's terms
+// (d - h w, product rounded then difference) for both channels of every bin [k0, nf)
+__global__ __launch_bounds__(256) void k_hann_loglike_partial(
+    const double2* __restrict__ S, int64_t stride, const float2* __restrict__ Y,
+    const uint64_t* __restrict__ info, int64_t m, int64_t nf, int64_t k0,
+    const double2* __restrict__ d, const double* __restrict__ w, double* __restrict__ part) {
+#pragma clang fp contract(off)
+    const int r = blockIdx.y;
+    const HannRow h = hann_row(info, r);
+    const double c = h.scale / (4.0 * (double)(nf - 1));
+    const double2* row = S + (int64_t)r * stride;
+    const float2* y = Y + (int64_t)r * m;
+    const int64_t nb = nf - k0;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double2 vp, vc;
+        hann_pol(row, y, nf, k0 + i, c, h.first, m - nf, vp, vc);
+        const double2 d0 = d[i], d1 = d[nb + i];
+        const double w0 = w[i], w1 = w[nb + i];
+        const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
+        const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
+        acc = fma(r0, r0, fma(i0, i0, acc));
+        acc = fma(r1, r1, fma(i1, i1, acc));
+    }
+    __shared__ double red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(int64_t)r * gridDim.x + blockIdx.x] = red[0];
 }
 
 // fused log-likelihood partials: one workgroup per chunk, then a second pass
@@ -3546,7 +3720,10 @@ __global__ void k_loglike_partial(const double2* __restrict__ h, const double2* 
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
+// (one row per workgroup: partials part[row * np ...], out[row])
 __global__ void k_loglike_final(const double* __restrict__ part, int np, double* __restrict__ out) {
+    part += (int64_t)blockIdx.x * np;
+    out += blockIdx.x;
     __shared__ double red[256];
     double acc = 0.0;
     for (int i = threadIdx.x; i < np; i += blockDim.x) acc += part[i];
@@ -4011,7 +4188,13 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         const int64_t cap = std::max<int64_t>(64, (SPARSE_WG / count + 7) / 8 * 8);
         nper = std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
     }
-    const int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;
+    int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;
+#ifdef EFD_PERSIST
+    const bool persist = !d;   // the persistent dense form: resident slots only
+    if (persist) nblk = std::min<int64_t>(resident_tile_slots(), nblk);
+#else
+    constexpr bool persist = false;
+#endif
     if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, F + ": grid too large");
     const dim3 grid((unsigned)nblk), block(TILE);
     const int acc = a[0]->accumulate ? 1 : 0;
@@ -4024,15 +4207,28 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         else                                                                                  \
             hipLaunchKernelGGL((k_modesum_batch<P, C, BPL, false>), grid, block, 0, st, batch, \
                                a[0]->nf, L0.nlanes, L0.ntiles, acc, d, w,                     \
-                               d ? llconst : nullptr, (int64_t)0);                            \
+                               d ? llconst : nullptr, nper);                                  \
     } while (0)
+#ifdef EFD_PERSIST
+#define EFD_LAUNCH_P(P, C)                                                                    \
+    do {                                                                                      \
+        if (persist)                                                                          \
+            hipLaunchKernelGGL((k_modesum_persist<P, C, BPL>), grid, block, 0, st, batch,      \
+                               a[0]->nf, L0.nlanes, L0.ntiles, acc);                          \
+        else                                                                                  \
+            EFD_LAUNCH(P, C);                                                                 \
+    } while (0)
+#else
+#define EFD_LAUNCH_P(P, C) EFD_LAUNCH(P, C)
+#endif
     if (a[0]->grid_symmetric) {
-        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
-        else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
+        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH_P(true, EFD_CAUSTIC_UNIFORM);
+        else EFD_LAUNCH_P(true, EFD_CAUSTIC_SPA);
     } else {
-        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(false, EFD_CAUSTIC_UNIFORM);
-        else EFD_LAUNCH(false, EFD_CAUSTIC_SPA);
+        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH_P(false, EFD_CAUSTIC_UNIFORM);
+        else EFD_LAUNCH_P(false, EFD_CAUSTIC_SPA);
     }
+#undef EFD_LAUNCH_P
 #undef EFD_LAUNCH
     HIP_TRY(hipGetLastError());
     if (d) {
@@ -4315,17 +4511,67 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
     return EFD_OK;
 }
 
-int efd_hann_polarizations(const double* S, const float* C, const double* cscale, int64_t nf,
-                           int64_t k0, double* hp, double* hc, void* stream) {
-    if (!S || !C || !cscale || !hp || !hc || nf < 3 || k0 < 0 || k0 > nf)
+static bool hann_rows_ok(const char* fn, const void* S, int64_t stride, int64_t nf,
+                         int32_t rows) {
+    if (!S || nf < 3 || rows < 1 || rows > 65535 || stride < nf) {
+        fail(EFD_ERR_ARG, std::string(fn) + ": bad arguments");
+        return false;
+    }
+    return true;
+}
+int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows, uint64_t* info,
+                    void* stream) {
+    if (!hann_rows_ok("efd_hann_extent", S, stride, nf, rows) || !info)
+        return fail(EFD_ERR_ARG, "efd_hann_extent: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_hann_info_init, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, info,
+                       rows);
+    HIP_TRY(hipGetLastError());
+    const int64_t blocks = std::min<int64_t>(2048, (nf + 255) / 256);
+    hipLaunchKernelGGL(k_hann_extent, dim3((unsigned)blocks, (unsigned)rows), dim3(256), 0, st,
+                       (const double2*)S, stride, nf, info);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                   const uint64_t* info, int64_t m, float* Y, void* stream) {
+    if (!hann_rows_ok("efd_hann_stage", S, stride, nf, rows) || !info || !Y || m < nf)
+        return fail(EFD_ERR_ARG, "efd_hann_stage: bad arguments");
+    const int64_t blocks = std::min<int64_t>(4096, (m + 255) / 256);
+    hipLaunchKernelGGL(k_hann_stage, dim3((unsigned)blocks, (unsigned)rows), dim3(256), 0,
+                       (hipStream_t)stream, (const double2*)S, stride, info, m, (float2*)Y);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
+                           int64_t nf, int64_t k0, double* hp, double* hc, void* stream) {
+    if (!S || !Y || !info || !hp || !hc || nf < 3 || m < nf || k0 < 0 || k0 > nf)
         return fail(EFD_ERR_ARG, "efd_hann_polarizations: bad arguments");
     const int64_t cnt = nf - k0;
     if (cnt == 0) return EFD_OK;
     const int threads = 256;
     const int64_t blocks = (cnt + threads - 1) / threads;
     hipLaunchKernelGGL(k_hann_polarizations, dim3((unsigned)blocks), dim3(threads), 0,
-                       (hipStream_t)stream, (const double2*)S, (const float2*)C, cscale, nf, k0,
+                       (hipStream_t)stream, (const double2*)S, (const float2*)Y, info, m, nf, k0,
                        (double2*)hp, (double2*)hc);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint64_t* info,
+                     int64_t m, int32_t rows, int64_t nf, int64_t k0, const double* d,
+                     const double* w, double* out, double* scratch, void* stream) {
+    if (!hann_rows_ok("efd_hann_loglike", S, stride, nf, rows) || !Y || !info || !d || !w ||
+        !out || !scratch || m < nf || k0 < 0 || k0 >= nf)
+        return fail(EFD_ERR_ARG, "efd_hann_loglike: bad arguments");
+    const int64_t nb = nf - k0;
+    const int threads = 256;
+    const int np = (int)std::min<int64_t>(EFD_LOGLIKE_SCRATCH, (nb + threads - 1) / threads);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)np, (unsigned)rows), dim3(threads),
+                       0, st, (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
+                       (const double2*)d, w, scratch);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_loglike_final, dim3((unsigned)rows), dim3(256), 0, st, scratch, np, out);
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }

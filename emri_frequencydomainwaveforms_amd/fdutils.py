@@ -106,26 +106,28 @@ class HannConvolution:
     indices mod N. The dropped second-order term is below 1e-13 max|S| at N = 12.6 M (numpy
     check: the first-order form is within 3e-12 of the exact DFT form at N = 1e6, falling as
     1/N^2). The correction term is itself ~1e-6 of max|S|, so C needs ~3 significant digits: it
-    is a zero-padded linear convolution on power-of-two FFTs of M >= 2N - 1 points in complex64
-    (S scaled by 1/max|S|), i.e. two rocFFT transforms of 2^25 points per waveform at N = 12.6 M
-    instead of the two Bluestein transforms of 2^25 points *each* that the size-N DFTs take."""
+    is computed in complex64 (rows scaled by their max component) as a linear convolution of
+    each row's SUPPORT [first, last) (its nonzero bins: the harmonics reach |f| <= F_max only)
+    with the lag kernel, on m-point transforms, m the smallest 2^a or 3 2^a >= N + (last -
+    first) - 1 (include/emrifd.h, efd_hann_extent). test.sh's 12.6 M-bin grid with its
+    harmonics below ~15% of Nyquist takes m = 2^24, where the full-support form needs 2^25 and
+    the size-N DFT form two Bluestein transforms of 2^25 each. The transforms are in place
+    (hipFFT plans per (m, rows), _hipfft); efd_hann_loglike then reduces the windowed templates'
+    logL without writing them."""
+
+    KEEP_KERNELS = 2   # lag-kernel spectra kept (one per m)
 
     def __init__(self, n, device):
-        torch = require_gpu()
+        require_gpu()
         self.n = n = int(n)
-        self.m = 1 << (2 * n - 2).bit_length()          # power of two >= 2 n - 1
+        if n < 3:
+            raise ValueError("HannConvolution: n >= 3")
         self.eps = 1.0 / (n - 1)
-        lag = torch.arange(-(n - 1), n, device=device, dtype=torch.int64)
-        mm = torch.remainder(lag, n).to(torch.float64)
-        zero = mm == 0
-        re = torch.where(zero, torch.zeros_like(mm), (np.pi / n) / torch.tan(np.pi * mm / n))
-        im = torch.where(zero, torch.full_like(mm, np.pi * (n - 1) / n),
-                         torch.full_like(mm, -np.pi / n))
-        k = torch.complex(re, im)
-        kp = torch.zeros(self.m, dtype=torch.complex128, device=device)
-        kp[:2 * n - 1] = k
-        self.kf = torch.fft.fft(kp).to(torch.complex64)   # lag t sits at t + n - 1
         self.device = device
+        self._kf = {}
+        self._plans = {}
+        self._ybuf = None
+        self._info = None
 
     @staticmethod
     def matches(window):
@@ -134,56 +136,132 @@ class HannConvolution:
         w = np.asarray(window.cpu().numpy() if hasattr(window, "detach") else window)
         return w.ndim == 1 and len(w) >= 3 and np.array_equal(w, hann(len(w)))
 
-    def _scaled_correction(self, S):
-        """(c, scale): c = (K (*) S) / scale in complex64, rows along the last axis, with C[k] at
-        c[..., n - 1 + k]; scale = max|S| per row (device tensor [..., 1]). The padded input
-        buffer is kept per row count (its tail stays zero)."""
-        torch = require_gpu()
-        n, m = self.n, self.m
-        shape = S.shape[:-1] + (m,)
-        y = getattr(self, "_y", None)
-        if y is None or tuple(y.shape) != tuple(shape) or y.device != S.device:
-            y = self._y = torch.zeros(shape, dtype=torch.complex64, device=S.device)
-        scale = S.abs().amax(dim=-1, keepdim=True).clamp_min(1e-300)
-        y[..., :n].copy_(S)                       # complex128 -> complex64 (spectra ~1e-20)
-        y[..., :n].mul_((1.0 / scale).to(torch.float32))
-        Y = torch.fft.fft(y, dim=-1)
-        Y.mul_(self.kf)
-        return torch.fft.ifft(Y, dim=-1), scale
+    @staticmethod
+    def size_for(n, support):
+        """The transform length for a support of `support` bins: the smallest 2^a or 3 2^a
+        that is >= n + support - 1."""
+        need = int(n) + max(int(support), 1) - 1
+        best = None
+        for base in (1, 3):
+            m = base
+            while m < need:
+                m *= 2
+            best = m if best is None else min(best, m)
+        return best
 
-    def correction(self, S):
+    def kernel_spectrum(self, m):
+        """fft(z) / m in complex64, z[t] = K[(t - (m - n)) mod n] (computed in complex128)."""
+        kf = self._kf.get(m)
+        if kf is None:
+            torch = require_gpu()
+            n = self.n
+            t = torch.arange(m, device=self.device, dtype=torch.int64)
+            mm = torch.remainder(t - (m - n), n).to(torch.float64)
+            zero = mm == 0
+            re = torch.where(zero, torch.zeros_like(mm), (np.pi / n) / torch.tan(np.pi * mm / n))
+            im = torch.where(zero, torch.full_like(mm, np.pi * (n - 1) / n),
+                             torch.full_like(mm, -np.pi / n))
+            kf = (torch.fft.fft(torch.complex(re, im)) / m).to(torch.complex64)
+            while len(self._kf) >= self.KEEP_KERNELS:
+                self._kf.pop(next(iter(self._kf)))
+            self._kf[m] = kf
+        return kf
+
+    def _rows(self, S):
+        torch = require_gpu()
+        if S.dim() == 1:
+            S = S[None]
+        if (S.dtype != torch.complex128 or S.shape[-1] != self.n or not S.is_contiguous()
+                or S.device != torch.device(self.device)):
+            raise ValueError(f"HannConvolution: contiguous complex128 rows of {self.n} bins on "
+                             f"{self.device}")
+        return S
+
+    def transform(self, S, lib):
+        """(Y, info, m) for the rows of S ([rows][n], complex128, contiguous): Y complex64
+        [rows][m] holds each row's C / scale at ((k - first) mod n) + m - n (efd_hann_stage's
+        layout after the transform pair); info int64 [rows][4] (efd_hann_extent). One host
+        synchronisation: the rows' supports choose m."""
+        from . import _hipfft, _lib
+        torch = require_gpu()
+        S = self._rows(S)
+        rows, n = int(S.shape[0]), self.n
+        st = torch.cuda.current_stream(S.device).cuda_stream
+        if self._info is None or self._info.shape[0] < rows:
+            self._info = torch.empty((rows, 4), dtype=torch.int64, device=S.device)
+        info = self._info[:rows]
+        sp = torch.view_as_real(S).data_ptr()
+        _lib.check(lib.efd_hann_extent(sp, n, n, rows, info.data_ptr(), st), "efd_hann_extent",
+                   lib)
+        ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
+        live = ext[:, 1] > 0
+        support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
+        m = self.size_for(n, support)
+        need = rows * m
+        if self._ybuf is None or self._ybuf.numel() < need:
+            self._ybuf = None
+            self._ybuf = torch.empty(need, dtype=torch.complex64, device=S.device)
+        Y = self._ybuf[:need].view(rows, m)
+        yp = torch.view_as_real(Y).data_ptr()
+        _lib.check(lib.efd_hann_stage(sp, n, n, rows, info.data_ptr(), m, yp, st),
+                   "efd_hann_stage", lib)
+        plan = self._plans.get((m, rows))
+        if plan is None:
+            plan = self._plans[(m, rows)] = _hipfft.C2CPlan(m, rows)
+        plan(yp, _hipfft.FORWARD, st)
+        Y.mul_(self.kernel_spectrum(m))
+        plan(yp, _hipfft.BACKWARD, st)
+        return Y, info, m
+
+    def correction(self, S, lib=None):
         """C = K (*) S (complex128, rows of S along the last axis)."""
-        torch = require_gpu()
-        c, scale = self._scaled_correction(S)
-        return c[..., self.n - 1:2 * self.n - 1].to(torch.complex128) * scale
-
-    def polarizations_batch(self, S, outs, k0, lib):
-        """polarizations for every row of S ([B][n], contiguous): one batched transform pair
-        (rocFFT over the rows) and one efd_hann_polarizations per row into outs[i] = (hp, hc)."""
         from . import _lib
         torch = require_gpu()
-        c, scale = self._scaled_correction(S)
+        one = S.dim() == 1
+        Y, info, m = self.transform(S, lib or _lib.load())
+        n = self.n
+        first = info[:, 1].clamp_min(0)
+        scale = info[:, 0].contiguous().view(torch.float64)
+        k = torch.arange(n, device=Y.device, dtype=torch.int64)
+        q = torch.remainder(k[None, :] - first[:, None], n) + (m - n)
+        C = torch.gather(Y, 1, q).to(torch.complex128) * scale[:, None]
+        return C[0] if one else C
+
+    def polarizations_batch(self, S, outs, k0, lib):
+        """polarizations for every row of S ([B][n], contiguous): one transform pair over the
+        rows and one efd_hann_polarizations per row into outs[i] = (hp, hc)."""
+        from . import _lib
+        torch = require_gpu()
+        S = self._rows(S)
+        Y, info, m = self.transform(S, lib)
         st = torch.cuda.current_stream(S.device).cuda_stream
         for i, (hp, hc) in enumerate(outs):
             _lib.check(lib.efd_hann_polarizations(
-                torch.view_as_real(S[i]).data_ptr(),
-                torch.view_as_real(c[i, self.n - 1:]).data_ptr(), scale[i].data_ptr(), self.n,
-                k0, torch.view_as_real(hp).data_ptr(), torch.view_as_real(hc).data_ptr(), st),
-                "efd_hann_polarizations", lib)
+                torch.view_as_real(S[i]).data_ptr(), torch.view_as_real(Y[i]).data_ptr(),
+                info[i].data_ptr(), m, self.n, k0, torch.view_as_real(hp).data_ptr(),
+                torch.view_as_real(hc).data_ptr(), st), "efd_hann_polarizations", lib)
         return outs
 
     def polarizations(self, S, hp, hc, k0, lib):
-        """h+/hx over bins [k0, n) of the windowed S (one row) into hp, hc
-        (efd_hann_polarizations: the stencil and the split in one pass)."""
+        """h+/hx over bins [k0, n) of the windowed S (one row) into hp, hc."""
+        self.polarizations_batch(self._rows(S), [(hp, hc)], k0, lib)
+        return hp, hc
+
+    def loglike_batch(self, S, d, w, k0, out, scratch, lib):
+        """efd_hann_loglike: the logL of every row's windowed template against d, w
+        (efd_loglike's [2][n - k0] layout) into out (float64 device [rows]); scratch holds
+        rows * EFD_LOGLIKE_SCRATCH doubles."""
         from . import _lib
         torch = require_gpu()
-        c, scale = self._scaled_correction(S)
+        S = self._rows(S)
+        rows = int(S.shape[0])
+        Y, info, m = self.transform(S, lib)
         st = torch.cuda.current_stream(S.device).cuda_stream
-        _lib.check(lib.efd_hann_polarizations(
-            torch.view_as_real(S).data_ptr(), torch.view_as_real(c[self.n - 1:]).data_ptr(),
-            scale.data_ptr(), self.n, k0, torch.view_as_real(hp).data_ptr(),
-            torch.view_as_real(hc).data_ptr(), st), "efd_hann_polarizations", lib)
-        return hp, hc
+        _lib.check(lib.efd_hann_loglike(
+            torch.view_as_real(S).data_ptr(), self.n, torch.view_as_real(Y).data_ptr(),
+            info.data_ptr(), m, rows, self.n, k0, torch.view_as_real(d).data_ptr(),
+            w.data_ptr(), out.data_ptr(), scratch.data_ptr(), st), "efd_hann_loglike", lib)
+        return out
 
     def __call__(self, S):
         torch = require_gpu()
@@ -315,36 +393,58 @@ class get_fd_waveform_fromFD:
     def can_fill_batch(self):
         return self._hann is not None and self._windowed_s_path()
 
-    def fill_batch(self, outs, params, **kwargs):
-        """fill for a batch of walkers (rows of params, FEW's 14) into outs[i] (complex128
-        [2][num_bins] each): every walker's spectrum queued into one [B][N] buffer without a
-        synchronisation, then the Hann window for all of them (one batched transform pair,
-        HannConvolution.polarizations_batch). Same values as B fill calls up to the batched
-        transform's rounding (the correction term carries ~1e-6 of max|S|; it enters at
-        <= 1e-12). The engine's device-side status is checked once, at the end."""
+    def _spectra(self, params, **kwargs):
+        """Every walker's two-sided spectrum queued into one [B][N] buffer (no
+        synchronisation); returns (rows, create_waveform)."""
         torch = require_gpu()
         if not self.can_fill_batch:
-            raise ValueError("fill_batch: the Hann-window spectrum path only")
+            raise ValueError("the Hann-window spectrum path only")
         gen = self.waveform_generator
         B = len(params)
-        if B == 0:
-            return outs
         n = int(self.positive_frequency_mask.numel())
         dev = self.positive_frequency_mask.device
         buf = getattr(self, "_sbuf", None)
         if buf is None or buf.shape[0] < B or buf.shape[1] != n:
+            self._sbuf = None
             buf = self._sbuf = torch.empty((B, n), dtype=torch.complex128, device=dev)
         for i, p in enumerate(params):
             gen._spectrum(*p, out=buf[i], check=False, **kwargs)
         cw = gen.waveform_generator.create_waveform
         if self._suffix_k0 != cw.positive_start():
             raise ValueError("positive_frequency_mask does not match the generator's grid")
-        self._hann.polarizations_batch(buf[:B], [(o[0], o[1]) for o in outs], self._suffix_k0,
-                                       cw.engine.lib)
+        return buf[:B], cw
+
+    def _status(self, cw):
         if not cw.engine.status():
             from . import _lib
             raise _lib.EFDError(f"efd_modesum: {_lib.last_error(cw.engine.lib)}")
+
+    def fill_batch(self, outs, params, **kwargs):
+        """fill for a batch of walkers (rows of params, FEW's 14) into outs[i] (complex128
+        [2][num_bins] each): the walkers' spectra in one [B][N] buffer, then the Hann window
+        for all of them (one transform pair over the rows, HannConvolution.polarizations_batch).
+        Same values as B fill calls up to the batched transform's rounding (the correction term
+        carries ~1e-6 of max|S|; it enters at <= 1e-12). The engine's device-side status is
+        checked once, at the end."""
+        if len(params) == 0:
+            return outs
+        S, cw = self._spectra(params, **kwargs)
+        self._hann.polarizations_batch(S, [(o[0], o[1]) for o in outs], self._suffix_k0,
+                                       cw.engine.lib)
+        self._status(cw)
         return outs
+
+    def loglike_batch(self, out, params, d, w, scratch, **kwargs):
+        """The windowed templates' log-likelihoods of a batch of walkers into out (float64
+        device [B]) against d, w (efd_loglike's operands, [2][num_bins]): the spectra as in
+        fill_batch, then HannConvolution.loglike_batch (efd_hann_loglike: no template is
+        written). The same logL as fill_batch + efd_loglike up to the reduction order."""
+        if len(params) == 0:
+            return out
+        S, cw = self._spectra(params, **kwargs)
+        self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib)
+        self._status(cw)
+        return out
 
     def fill(self, out, *args, **kwargs):
         """Write [ch1, ch2] into out (complex128 [2][num_bins], device) without copies.

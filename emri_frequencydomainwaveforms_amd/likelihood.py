@@ -213,19 +213,18 @@ class Likelihood:
         elif getattr(tm, "can_fill_batch", False):
             # windowed templates (the drivers' Hann window): groups of WINDOW_GROUP walkers,
             # their spectra in one buffer and the window's transforms batched over them
+            # and the windowed templates' logL reduced in place (efd_hann_loglike)
             G = max(1, int(getattr(tm, "WINDOW_GROUP", 8)))
-            bufs = getattr(self, "_wbufs", None)
-            if bufs is None or bufs.shape[0] < G or tuple(bufs.shape[1:]) != (nch, nb):
-                bufs = self._wbufs = torch.empty((G, nch, nb), dtype=torch.complex128,
-                                                 device=self.device)
+            scr = getattr(self, "_wscratch", None)
+            if scr is None or scr.numel() < G * _lib.EFD_LOGLIKE_SCRATCH:
+                scr = self._wscratch = torch.empty(G * _lib.EFD_LOGLIKE_SCRATCH,
+                                                   dtype=torch.float64, device=self.device)
             if hasattr(tm, "prefetch"):
                 tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
             for g0 in range(0, num_likes, G):
                 rows = params[g0:g0 + G]
-                tm.fill_batch([bufs[i] for i in range(len(rows))], rows, *args, **kwargs)
-                for i in range(len(rows)):
-                    self._red.loglike(bufs[i], self._d, self._w_templ,
-                                      out=out[g0 + i:g0 + i + 1])
+                tm.loglike_batch(out[g0:g0 + len(rows)], rows, self._d, self._w_templ, scr,
+                                 *args, **kwargs)
         elif getattr(tm, "can_fill", False):
             if self._buf is None or tuple(self._buf.shape) != (nch, nb):
                 self._buf = torch.empty((nch, nb), dtype=torch.complex128, device=self.device)

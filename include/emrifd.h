@@ -291,19 +291,35 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
                       void* stream);
 
 /*
- * The h+/hx of efd_polarizations for the spectrum convolved with the reference's Hann window
- * (FDutils.py:66-101 get_fd_windowed with emri_pe.py:261's scipy hann(nf), sym=True), without
- * size-nf DFTs: the windowed spectrum is
- *   S_w[k] = S[k]/2 - (S[k+1] + S[k-1])/4 - c (C[k+1] - C[k-1]),   indices mod nf,
+ * The spectrum convolved with the reference's Hann window (FDutils.py:66-101 get_fd_windowed
+ * with emri_pe.py:261's scipy hann(nf), sym=True) without size-nf DFTs: the windowed spectrum is
+ *   S_w[k] = S[k]/2 - (S[k+1] + S[k-1])/4 - (C[k+1] - C[k-1]) / (4 (nf - 1)),   indices mod nf,
  * C = K (*) S the circular convolution with K[m] = -i pi/nf + (pi/nf) cot(pi m/nf),
- * K[0] = i pi (nf-1)/nf (the derivative of the DFT's trigonometric interpolant), c =
- * (*cscale) / (4 (nf - 1)); the caller computes C (rocFFT, zero-padded power-of-two linear
- * convolution; fdutils.HannConvolution). S complex128 [nf]; C complex64 [nf] (the caller's C
- * divided by *cscale); cscale one device double. Writes bins [k0, nf) into hp, hc.
- * Replaces: no reference function (the reference convolves each channel with scipy/cupy).
+ * K[0] = i pi (nf-1)/nf (the derivative of the DFT's trigonometric interpolant). C is the caller's
+ * linear convolution of each row's support with K on m-point complex64 transforms
+ * (fdutils.HannConvolution): rows of S (complex128 [nf], row r at S + 2 r stride doubles);
+ * info[r] (4 x uint64 per row, device) = {bits of scale = max(|Re|, |Im|) over the row, first
+ * nonzero bin, last nonzero bin + 1, 0} (first = ~0, last = 0 for an all-zero row; a NaN makes
+ * the scale NaN); Y complex64 [rows][m], m >= nf + (last - first) - 1.
+ *   efd_hann_extent: info from S.
+ *   efd_hann_stage:  Y[r][s] = S[r][first + s] / scale for s < last - first, 0 up to m. The
+ *                    caller transforms Y in place: forward, times the lag kernel's spectrum
+ *                    (z[t] = K[(t - (m - nf)) mod nf] / m), backward; then
+ *                    C[k] = scale Y[r][((k - first) mod nf) + m - nf].
+ *   efd_hann_polarizations: h+/hx (efd_polarizations' split) of one row's S_w over bins
+ *                    [k0, nf) into hp, hc (complex [nf - k0]).
+ *   efd_hann_loglike: efd_loglike of every row's windowed h+/hx against d, w ([2][nf - k0],
+ *                    efd_loglike's layout and rounding), out[r] (device doubles [rows]); scratch
+ *                    holds rows * EFD_LOGLIKE_SCRATCH doubles. No template is written.
+ * Replaces: no reference function (the reference convolves each channel with scipy/cupy at
+ * FDutils.py:35-47, 95-96).
  */
-int efd_hann_polarizations(const double* S, const float* C, const double* cscale, int64_t nf,
-                           int64_t k0, double* hp, double* hc, void* stream);
+int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows, uint64_t* info,
+                    void* stream);
+int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                   const uint64_t* info, int64_t m, float* Y, void* stream);
+int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
+                           int64_t nf, int64_t k0, double* hp, double* hc, void* stream);
 
 /*
  * Fused Gaussian log-likelihood over nchan channels of nbin bins each:
@@ -316,6 +332,10 @@ int efd_hann_polarizations(const double* S, const float* C, const double* cscale
 #define EFD_LOGLIKE_SCRATCH 1024
 int efd_loglike(const double* h, const double* d, const double* w, int32_t nchan, int64_t nbin,
                 double* out, double* scratch, void* stream);
+/* the windowed log-likelihood of rows of spectra (see efd_hann_extent above) */
+int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint64_t* info,
+                     int64_t m, int32_t rows, int64_t nf, int64_t k0, const double* d,
+                     const double* w, double* out, double* scratch, void* stream);
 
 /*
  * Noise-weighted inner product over nchan channels of nbin bins each:

@@ -70,6 +70,15 @@ def test_windowed_likelihood_test_sh_full_grid():
     finally:
         del gen.WINDOW_GROUP
     np.testing.assert_allclose(ll1, ll, rtol=1e-12, atol=0.0)
+    # the in-place reduction (efd_hann_loglike) against the written templates + efd_loglike
+    nch, nb = like._d.shape
+    bufs = torch.empty((len(batch), nch, nb), dtype=torch.complex128, device=like.device)
+    params14 = s.transform.both_transforms(batch)
+    gen.fill_batch([bufs[i] for i in range(len(batch))], params14, **s.kwargs)
+    ll_w = np.array([float(like._red.loglike(bufs[i], like._d, like._w_templ)[0])
+                     for i in range(len(batch))])
+    np.testing.assert_allclose(ll_w, ll, rtol=1e-12, atol=0.0)
+    del bufs
 
     f = s.f_like
     w = lo.noise_factor(f, [get_sensitivity(f)] * 2)
@@ -80,7 +89,6 @@ def test_windowed_likelihood_test_sh_full_grid():
     S0 = s.few._spectrum(*s.truth14, **s.kwargs).cpu().numpy()
     d_gpu = _windowed_channels(S0, window, grid) * w
     e_d = np.sqrt(np.sum(np.abs(d_gpu - d_R) ** 2))
-    params14 = s.transform.both_transforms(batch)
     rows, ok_all = [], True
     for i, p in enumerate(params14):
         R, Rps, _, E = oracle_spectra(s.few, p, s.kwargs, perturb_seeds=(20 + i, 2000 + i))
@@ -110,20 +118,27 @@ def test_windowed_likelihood_test_sh_full_grid():
     assert ok_all, rec
 
 
-@pytest.mark.parametrize("n", [100001, 1577909])
-def test_hann_convolution_matches_dft_form(n):
+@pytest.mark.parametrize("n,support", [(100001, (1 / 3, 1.0)), (1577909, (1 / 3, 1.0)),
+                                       (100001, (0.45, 0.55)), (100001, (0.0, 1.0))])
+def test_hann_convolution_matches_dft_form(n, support):
     """fdutils.HannConvolution (stencil + complex64 power-of-two correction, the path the
     reference's hann(N) window takes) against the exact size-N DFT form windowed_spectrum (FP64
-    rocFFT), on a random odd-grid spectrum with a third of its bins zero (a walker batch of two
-    rows): within 5/N^2 + 1e-13 of max|S| (the first-order form's truncation, ~3.5/N^2 for a
+    rocFFT), on a random odd-grid spectrum nonzero on a sub-range (the support the transforms
+    are sized for: 2/3, 1/10 and all of the grid; a walker batch of two rows): within 5/N^2 + 1e-13 of max|S| (the first-order form's truncation, ~3.5/N^2 for a
     random-phase spectrum: 3.6e-10 at N = 1e5, 2e-14 at test.sh's 12.6 M); and the one-pass
-    kernel (efd_hann_polarizations) against efd_polarizations of the same windowed spectrum."""
+    kernel (efd_hann_polarizations, one row's correction transform) against efd_polarizations
+    of the two-row call's windowed spectrum: the complex64 correction C rounds differently in a
+    batch of two rows and in one row (|dC| ~ 2^-23 |C|, |C| <= max|S| ln N, times e/4 =
+    1/(4(N-1))), so within 2^-23 ln(N) / (N - 1) + 1e-14 of max|S| (measured 1.0e-12 at
+    N = 1e5, 6.7e-14 at 1.58 M)."""
     from scipy.signal.windows import hann
     from emri_frequencydomainwaveforms_amd.fdutils import (HannConvolution, window_multiplier,
                                                            windowed_spectrum)
     rng = np.random.default_rng(n)
     S = rng.normal(size=(2, n)) + 1j * rng.normal(size=(2, n))
-    S[:, : n // 3] = 0.0
+    lo, hi = int(support[0] * n), int(support[1] * n)
+    S[:, :lo] = 0.0
+    S[:, hi:] = 0.0
     S[1] *= 1e-21                                  # spectra are ~1e-18..1e-24
     St = torch.as_tensor(S, device="cuda")
     w = hann(n)
@@ -138,6 +153,7 @@ def test_hann_convolution_matches_dft_form(n):
     from emri_frequencydomainwaveforms_amd import _lib
     lib = _lib.load()
     k0 = n // 2
+    tol_pol = 2.0 ** -23 * np.log(n) / (n - 1) + 1e-14
     for r in range(2):
         hp = torch.empty(n - k0, dtype=torch.complex128, device="cuda")
         hc = torch.empty_like(hp)
@@ -151,5 +167,40 @@ def test_hann_convolution_matches_dft_form(n):
                                          torch.view_as_real(hc_ref).data_ptr(), None), "pol", lib)
         torch.cuda.synchronize()
         mx = float(St[r].abs().max())
-        assert float((hp - hp_ref).abs().max()) <= 1e-14 * mx
-        assert float((hc - hc_ref).abs().max()) <= 1e-14 * mx
+        assert float((hp - hp_ref).abs().max()) <= tol_pol * mx
+        assert float((hc - hc_ref).abs().max()) <= tol_pol * mx
+
+
+def test_hann_loglike_matches_templates():
+    """efd_hann_loglike (the windowed logL reduced without writing templates) against
+    efd_hann_polarizations + efd_loglike on the same rows, including an all-zero row (its logL
+    is the data-only term) and rows of different supports: 1e-12 relative (reduction order)."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.fdutils import HannConvolution
+    from emri_frequencydomainwaveforms_amd.reductions import Reducer
+    lib = _lib.load()
+    n = 200001
+    k0 = n // 2
+    nb = n - k0
+    rng = np.random.default_rng(7)
+    S = (rng.normal(size=(3, n)) + 1j * rng.normal(size=(3, n))) * 1e-20
+    S[0, : n // 4] = S[0, 3 * n // 4:] = 0.0
+    S[1, : 2 * n // 5] = S[1, 3 * n // 5:] = 0.0
+    S[2] = 0.0
+    St = torch.as_tensor(S, device="cuda")
+    d = torch.as_tensor((rng.normal(size=(2, nb)) + 1j * rng.normal(size=(2, nb))) * 1e-20,
+                        device="cuda")
+    w = torch.as_tensor(rng.uniform(0.5, 2.0, size=(2, nb)), device="cuda")
+    hcv = HannConvolution(n, St.device)
+    out = torch.empty(3, dtype=torch.float64, device="cuda")
+    scr = torch.empty(3 * _lib.EFD_LOGLIKE_SCRATCH, dtype=torch.float64, device="cuda")
+    hcv.loglike_batch(St, d, w, k0, out, scr, lib)
+    red = Reducer(St.device)
+    ref = []
+    for r in range(3):
+        h = torch.empty((2, nb), dtype=torch.complex128, device="cuda")
+        hcv.polarizations(St[r].contiguous(), h[0], h[1], k0, lib)
+        ref.append(float(red.loglike(h, d, w)[0]))
+    got = out.cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0.0)
+    np.testing.assert_allclose(got[2], float(red.loglike(None, d, w)[0]), rtol=1e-12, atol=0.0)
