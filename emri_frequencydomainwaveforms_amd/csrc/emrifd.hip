@@ -60,13 +60,10 @@ namespace {
 constexpr int TILE = 256;           // threads per workgroup in k_modesum (round 2: 512-thread
                                     // tiles of 8 waves ran 0.974x)
 constexpr int NWAVE = TILE / 64;    // waves per workgroup
-#ifndef EFD_BPL
-#define EFD_BPL 2
-#endif
-#ifndef EFD_SPLIT_B
-#define EFD_SPLIT_B 0
-#endif
-constexpr int BPL = EFD_BPL;        // bins (lanes) per thread in k_modesum (3 or 4: +3-5%)
+// bins (lanes) per thread in k_modesum. Round 4: 3 with the own/mirror amplitude cubics split
+// (below) fits the 128-VGPR budget without spills in the record loop: config 2 +2.1-2.4% over 2
+// (paired A/B, 3 rounds on two boxes, profiles/r04_ab_bpl3.jsonl); 4 spilled (-4%)
+constexpr int BPL = 3;
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
@@ -542,9 +539,6 @@ __device__ __forceinline__ void group_body(const int32_t* __restrict__ marr,
         hdr->groups = 0;
         hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
         hdr->lane_hi = INT32_MIN;
-#ifdef EFD_PERSIST
-        hdr->pad[0] = 0;            // k_modesum_batch's persistent tile counter (two int32)
-#endif
         if (!init) {
             hdr->runs_overflow = 0;
             hdr->bad_mn = 0;
@@ -2304,8 +2298,7 @@ __device__ __forceinline__ void modesum_tile(
     // every walker (efd_loglike_tile_constants); NULL: such tiles compute it
     const double* __restrict__ llconst,
     int64_t b,     // b: this workgroup's place in the waveform's dispatch order
-    bool direct = false,     // b is the tile itself (k_modesum_batch's sparse form)
-    bool* tab_loaded = nullptr) {   // persistent workgroups: the sin/cos table is in LDS already
+    bool direct = false) {   // b is the tile itself (k_modesum_batch's sparse form)
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -2384,13 +2377,10 @@ __device__ __forceinline__ void modesum_tile(
                            reinterpret_cast<uint4*>(keys) + rd * TILE + wave * 64);
             }
         }
-        if (tab_loaded == nullptr || !*tab_loaded) {
 #pragma unroll
-            for (int rd = 0; rd < SCTAB / TILE; ++rd)
-                glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
-                       reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
-            if (tab_loaded != nullptr) *tab_loaded = true;
-        }
+        for (int rd = 0; rd < SCTAB / TILE; ++rd)
+            glds16(reinterpret_cast<const uint4*>(sctab_g) + rd * TILE + tid,
+                   reinterpret_cast<uint4*>(sctab) + rd * TILE + wave * 64);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
         __syncthreads();
     }
@@ -2676,7 +2666,6 @@ __device__ __forceinline__ void modesum_tile(
                         needany |= needm[i];
                     }
                     anyneed = needany != 0;
-#if EFD_SPLIT_B
                     // the own bins' amplitude cubics (b[0], 16 VGPRs) first, then the mirrors'
                     // (b[1], read after a compiler fence so they can reuse the registers)
 #pragma unroll
@@ -2698,16 +2687,6 @@ __device__ __forceinline__ void modesum_tile(
                             mir_i[i] = fma(-zi, wr[i], mir_i[i]);
                         }
                     }
-#else
-#pragma unroll
-                    for (int i = 0; i < BPL; ++i) {
-                        const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
-                        const double zr = PAIRED ? cubic(xm, w[i]) : 0.0;
-                        const double zi = PAIRED ? cubic(xm + 4, w[i]) : 0.0;
-                        accumulate<0, PAIRED>(wr[i], wi[i], xr, xi, zr, zi, own_r[i], own_i[i],
-                                              mir_r[i], mir_i[i]);
-                    }
-#endif
                     if (__builtin_expect(anyneed, 0)) {   // cold: general path, some lanes
 #ifdef EFD_EXP
                         {
@@ -2954,45 +2933,6 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
         d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm, d.segbase, d.stb0,
         d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld, llw, d.llpart, llconst, pos);
 }
-
-#ifdef EFD_PERSIST
-// The dense batch in persistent form: one workgroup per resident slot takes (waveform, place)
-// items in dispatch order from a counter in waveform 0's header (k_group zeroes it, the last
-// workgroup to finish resets it); the sin/cos table (the same bits in every waveform's workspace)
-// comes into LDS once per workgroup instead of once per tile.
-template <bool PAIRED, int CAUSTIC, int BPL>
-__global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
-void k_modesum_persist(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t ntiles,
-                       int accumulate_out) {
-    const int n = batch.n;
-    int32_t* ctr = reinterpret_cast<int32_t*>(&batch.d[0].hdr->pad[0]);
-    const int64_t gq = 8 * XCD_GROUP, ngrid = (ntiles + gq - 1) / gq * gq;
-    const int64_t total = ngrid * n;
-    __shared__ int32_t s_item;
-    bool tl = false;
-    while (true) {
-        if (threadIdx.x == 0) s_item = atomicAdd(ctr, 1);
-        __syncthreads();
-        const int64_t item = s_item;
-        if (item >= total) break;
-        const int wv = (int)(item % n);
-        const BatchDesc& e = batch.d[wv];
-        modesum_tile<PAIRED, CAUSTIC, BPL>(
-            e.items, e.ranges, e.seglh, e.seginfo, e.nseg, e.freq, nf, nlanes, ntiles, e.nt,
-            e.K, e.gm, e.gn, e.t, e.coefA, e.coefT, e.sctab, e.tkeys, e.tcnt, e.tperm,
-            e.segbase, e.stb0, e.stb1, e.hdr, accumulate_out, e.out, e.hp, e.hc, e.k0,
-            nullptr, nullptr, nullptr, nullptr, item / n, false, &tl);
-        __syncthreads();   // s_item and the LDS stages reused by the next item
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(ctr + 1, 1) == (int)gridDim.x - 1) {
-            atomicExch(ctr, 0);
-            atomicExch(ctr + 1, 0);
-        }
-    }
-}
-#endif
 
 // The fused likelihood's partial of a tile whose waveform has no record on it (every bin's
 // h = 0): modesum_tile's epilogue with zero accumulators, the same operations in the same order,
@@ -3576,7 +3516,22 @@ __global__ __launch_bounds__(256) void k_hann_extent(const double2* __restrict__
         lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, o, 64));
         hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, o, 64));
     }
+    // the block's 4 waves through LDS, then one thread's 3 atomics per block (a few hundred
+    // per row: contention on the row's 3 words stays small)
+    __shared__ uint64_t red[3][4];
+    const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
+        red[0][wv] = mx;
+        red[1][wv] = lo;
+        red[2][wv] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 4; ++i) {
+            mx = max(mx, red[0][i]);
+            lo = min(lo, red[1][i]);
+            hi = max(hi, red[2][i]);
+        }
         uint64_t* in = info + 4 * blockIdx.y;
         if (mx) atomicMax((unsigned long long*)&in[0], (unsigned long long)mx);
         if (hi) {
@@ -4188,13 +4143,7 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         const int64_t cap = std::max<int64_t>(64, (SPARSE_WG / count + 7) / 8 * 8);
         nper = std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
     }
-    int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;
-#ifdef EFD_PERSIST
-    const bool persist = !d;   // the persistent dense form: resident slots only
-    if (persist) nblk = std::min<int64_t>(resident_tile_slots(), nblk);
-#else
-    constexpr bool persist = false;
-#endif
+    const int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;
     if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, F + ": grid too large");
     const dim3 grid((unsigned)nblk), block(TILE);
     const int acc = a[0]->accumulate ? 1 : 0;
@@ -4207,28 +4156,15 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         else                                                                                  \
             hipLaunchKernelGGL((k_modesum_batch<P, C, BPL, false>), grid, block, 0, st, batch, \
                                a[0]->nf, L0.nlanes, L0.ntiles, acc, d, w,                     \
-                               d ? llconst : nullptr, nper);                                  \
+                               d ? llconst : nullptr, (int64_t)0);                            \
     } while (0)
-#ifdef EFD_PERSIST
-#define EFD_LAUNCH_P(P, C)                                                                    \
-    do {                                                                                      \
-        if (persist)                                                                          \
-            hipLaunchKernelGGL((k_modesum_persist<P, C, BPL>), grid, block, 0, st, batch,      \
-                               a[0]->nf, L0.nlanes, L0.ntiles, acc);                          \
-        else                                                                                  \
-            EFD_LAUNCH(P, C);                                                                 \
-    } while (0)
-#else
-#define EFD_LAUNCH_P(P, C) EFD_LAUNCH(P, C)
-#endif
     if (a[0]->grid_symmetric) {
-        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH_P(true, EFD_CAUSTIC_UNIFORM);
-        else EFD_LAUNCH_P(true, EFD_CAUSTIC_SPA);
+        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(true, EFD_CAUSTIC_UNIFORM);
+        else EFD_LAUNCH(true, EFD_CAUSTIC_SPA);
     } else {
-        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH_P(false, EFD_CAUSTIC_UNIFORM);
-        else EFD_LAUNCH_P(false, EFD_CAUSTIC_SPA);
+        if (a[0]->caustic == EFD_CAUSTIC_UNIFORM) EFD_LAUNCH(false, EFD_CAUSTIC_UNIFORM);
+        else EFD_LAUNCH(false, EFD_CAUSTIC_SPA);
     }
-#undef EFD_LAUNCH_P
 #undef EFD_LAUNCH
     HIP_TRY(hipGetLastError());
     if (d) {
@@ -4527,7 +4463,7 @@ int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows, u
     hipLaunchKernelGGL(k_hann_info_init, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, info,
                        rows);
     HIP_TRY(hipGetLastError());
-    const int64_t blocks = std::min<int64_t>(2048, (nf + 255) / 256);
+    const int64_t blocks = std::min<int64_t>(std::max(64, 1024 / rows), (nf + 255) / 256);
     hipLaunchKernelGGL(k_hann_extent, dim3((unsigned)blocks, (unsigned)rows), dim3(256), 0, st,
                        (const double2*)S, stride, nf, info);
     HIP_TRY(hipGetLastError());

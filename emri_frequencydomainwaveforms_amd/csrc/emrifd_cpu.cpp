@@ -11,7 +11,7 @@
 //   not-a-knot splines: trajectory (Phi_phi, Phi_r, f_phi, f_r, knot slopes of f_phi and f_r),
 //   group amplitudes, inverse splines t(F) per monotonic run   k_prep
 //   one interval record per (group, knot interval)              k_items
-//   output-stationary sum over 512-lane tiles (per-tile record lists, one SPA evaluation per
+//   output-stationary sum over 768-lane tiles (per-tile record lists, one SPA evaluation per
 //   (record, lane) feeding the lane's bin and its mirror), uniform K_{1/3} factor in polar
 //   form from the record's series length, sin/cos from the 512-entry table
 //                                                               k_tile_keys + k_modesum
@@ -43,7 +43,7 @@ struct double2 {
 #include "spa_tables.inc"
 #undef EFD_TABLE
 
-constexpr int TL = 512;             // lanes per tile (the kernel's TILE * BPL)
+constexpr int TL = 768;             // lanes per tile (the kernel's TILE * BPL)
 constexpr int MAXRUNS = 8;
 constexpr int MAX_NT = 1024;
 constexpr int MAX_K = 8192;

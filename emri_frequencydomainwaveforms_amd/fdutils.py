@@ -394,8 +394,8 @@ class get_fd_waveform_fromFD:
         return self._hann is not None and self._windowed_s_path()
 
     def _spectra(self, params, **kwargs):
-        """Every walker's two-sided spectrum queued into one [B][N] buffer (no
-        synchronisation); returns (rows, create_waveform)."""
+        """Every walker's two-sided spectrum in one [B][N] buffer; returns (rows,
+        create_waveform, whether the per-walker path ran: its device status is still unread)."""
         torch = require_gpu()
         if not self.can_fill_batch:
             raise ValueError("the Hann-window spectrum path only")
@@ -407,15 +407,22 @@ class get_fd_waveform_fromFD:
         if buf is None or buf.shape[0] < B or buf.shape[1] != n:
             self._sbuf = None
             buf = self._sbuf = torch.empty((B, n), dtype=torch.complex128, device=dev)
-        for i, p in enumerate(params):
-            gen._spectrum(*p, out=buf[i], check=False, **kwargs)
+        single = not (hasattr(gen, "spectrum_batch") and
+                      gen.waveform_generator.output_type == "fd")
+        if not single:
+            # packed uploads, batched preparation and one sum launch per group of walkers
+            # (device-side errors raise in there)
+            gen.spectrum_batch(params, buf[:B], **kwargs)
+        else:
+            for i, p in enumerate(params):
+                gen._spectrum(*p, out=buf[i], check=False, **kwargs)
         cw = gen.waveform_generator.create_waveform
         if self._suffix_k0 != cw.positive_start():
             raise ValueError("positive_frequency_mask does not match the generator's grid")
-        return buf[:B], cw
+        return buf[:B], cw, single
 
-    def _status(self, cw):
-        if not cw.engine.status():
+    def _status(self, cw, single):
+        if single and not cw.engine.status():
             from . import _lib
             raise _lib.EFDError(f"efd_modesum: {_lib.last_error(cw.engine.lib)}")
 
@@ -428,10 +435,10 @@ class get_fd_waveform_fromFD:
         checked once, at the end."""
         if len(params) == 0:
             return outs
-        S, cw = self._spectra(params, **kwargs)
+        S, cw, single = self._spectra(params, **kwargs)
         self._hann.polarizations_batch(S, [(o[0], o[1]) for o in outs], self._suffix_k0,
                                        cw.engine.lib)
-        self._status(cw)
+        self._status(cw, single)
         return outs
 
     def loglike_batch(self, out, params, d, w, scratch, **kwargs):
@@ -441,9 +448,9 @@ class get_fd_waveform_fromFD:
         written). The same logL as fill_batch + efd_loglike up to the reduction order."""
         if len(params) == 0:
             return out
-        S, cw = self._spectra(params, **kwargs)
+        S, cw, single = self._spectra(params, **kwargs)
         self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib)
-        self._status(cw)
+        self._status(cw, single)
         return out
 
     def fill(self, out, *args, **kwargs):

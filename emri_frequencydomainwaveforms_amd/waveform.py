@@ -412,25 +412,51 @@ class GenerateEMRIWaveform:
         that group's stream, one efd_modesum_sum_batch writing the group's h+/hx, two groups in
         flight. Returns out, ordered after the work on the current stream."""
         torch = require_gpu()
-        from .summation import BatchPreparer, sum_batch
+        npos = self._batch_grid(T, dt, f_arr)[1]
+        B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
+        if tuple(out.shape) != (B, 2, npos) or out.dtype != torch.complex128:
+            raise ValueError(f"out must be complex128 [{B}][2][{npos}]")
+        return self._run_batch(params, out, lambda j: dict(hp=torch.view_as_real(out[j, 0]),
+                                                           hc=torch.view_as_real(out[j, 1])),
+                               T, dt, eps, f_arr, kwargs)
+
+    def spectrum_batch(self, params, out, T=1.0, dt=10.0, eps=1e-5, f_arr=None, **kwargs):
+        """The two-sided spectra S = h+ - i hx of every row of params into the rows of out
+        (complex128 [B][N], contiguous rows, on the device): generate_batch's device groups
+        with the sum writing S (the windowed templates' input, fdutils.HannConvolution); bitwise
+        the spectrum path's S of each row."""
+        torch = require_gpu()
+        n = self._batch_grid(T, dt, f_arr)[0]
+        B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
+        if (out.dim() != 2 or tuple(out.shape) != (B, n) or out.dtype != torch.complex128
+                or not out.is_contiguous()):
+            raise ValueError(f"out must be contiguous complex128 [{B}][{n}]")
+        return self._run_batch(params, out, lambda j: dict(out=torch.view_as_real(out[j])),
+                               T, dt, eps, f_arr, kwargs)
+
+    def _batch_grid(self, T, dt, f_arr):
         gen = self.waveform_generator
         if gen.output_type != "fd":
-            raise ValueError("generate_batch is the FD path")
-        params = np.asarray(params, dtype=np.float64).reshape(-1, 14)
-        B = len(params)
+            raise ValueError("the batched generator is the FD path")
         cw = gen.create_waveform
         freq, sym = cw._grid(T, dt, f_arr)
         if not sym:
-            raise ValueError("generate_batch needs a symmetric grid")
-        npos = int(freq.numel()) - cw._k0
-        if tuple(out.shape) != (B, 2, npos) or out.dtype != torch.complex128:
-            raise ValueError(f"out must be complex128 [{B}][2][{npos}]")
+            raise ValueError("the batched generator needs a symmetric grid")
+        return int(freq.numel()), int(freq.numel()) - cw._k0
+
+    def _run_batch(self, params, out, outputs, T, dt, eps, f_arr, kwargs):
+        torch = require_gpu()
+        from .summation import BatchPreparer, sum_batch
+        cw = self.waveform_generator.create_waveform
+        params = np.asarray(params, dtype=np.float64).reshape(-1, 14)
+        B = len(params)
         if B == 0:
             return out
         self.prefetch(params, T=T, dt=dt, eps=eps, **kwargs)
         G = min(self.BATCH_GROUP, _lib.EFD_BATCH_MAX)
         st = getattr(self, "_gen_batch", None)
-        if st is None or st["prep"].caustic != cw.caustic or st["device"] != out.device:
+        if (st is None or st["prep"].caustic != cw.caustic or st["device"] != out.device
+                or st["prep"].group != G):
             st = self._gen_batch = dict(
                 prep=BatchPreparer(group=G, depth=2, caustic=cw.caustic, device=out.device),
                 stream=torch.cuda.Stream(out.device), device=out.device,
@@ -445,8 +471,7 @@ class GenerateEMRIWaveform:
                 self.submit_batch(prep, rows, T=T, dt=dt, eps=eps, f_arr=f_arr, **kwargs)
                 gi, jobs = prep.flush()
                 s_sum.wait_stream(prep.stream(gi))
-                sum_batch([(eng, dict(kw, hp=torch.view_as_real(out[g0 + i, 0]),
-                                      hc=torch.view_as_real(out[g0 + i, 1])))
+                sum_batch([(eng, dict(kw, **outputs(g0 + i)))
                            for i, (eng, kw) in enumerate(jobs)], stream=s_sum.cuda_stream)
                 ev = st["ev"][gi]
                 ev.record(s_sum)

@@ -155,7 +155,7 @@ def test_tile_constants_and_ordering_argument_errors_are_host_side():
     fake = ctypes.c_void_p(16)
     buf = ctypes.create_string_buffer(256)
     assert lib.efd_loglike_tile_count(0) == 0
-    assert lib.efd_loglike_tile_count(6311631) == 6164   # config 4: 3,155,816 lane pairs / 512
+    assert lib.efd_loglike_tile_count(6311631) == 4110   # config 4: 3,155,816 lane pairs / 768
     assert lib.efd_loglike_tile_count(1001) >= 1
     assert lib.efd_loglike_tile_constants(None, fake, 1001, 500, fake, None) == -1
     lib.efd_last_error(buf, 256)

@@ -247,3 +247,18 @@ def test_generate_batch_matches_calls(setup):
         del gen_list.BATCH_GROUP
     with pytest.raises(ValueError):
         gen_list.generate_batch(rows, out[:4], **kw)
+    # spectrum_batch: the two-sided S of each row (the windowed templates' input), bitwise the
+    # spectrum path's; stale buffer contents are overwritten everywhere
+    refS = [gen_list._spectrum(*r, **kw).clone() for r in rows]
+    S = torch.full((5, refS[0].numel()), complex(np.nan, np.nan), dtype=torch.complex128,
+                   device="cuda")
+    gen_list.BATCH_GROUP = 3
+    try:
+        gen_list.spectrum_batch(rows, S, **kw)
+    finally:
+        del gen_list.BATCH_GROUP
+    torch.cuda.synchronize()
+    for b in range(5):
+        assert torch.equal(S[b], refS[b]), b
+    with pytest.raises(ValueError):
+        gen_list.spectrum_batch(rows, S[:4], **kw)
