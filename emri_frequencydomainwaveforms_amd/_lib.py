@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "efd_polarizations",
     "efd_hann_extent",
     "efd_hann_stage",
+    "efd_hann_convolve",
     "efd_hann_polarizations",
     "efd_hann_loglike",
     "efd_loglike",
@@ -222,6 +223,8 @@ def load(path=None):
     lib.efd_hann_extent.argtypes = [vp, i64, i64, i32, vp, vp]
     lib.efd_hann_stage.restype = ctypes.c_int
     lib.efd_hann_stage.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp]
+    lib.efd_hann_convolve.restype = ctypes.c_int
+    lib.efd_hann_convolve.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp, vp]
     lib.efd_hann_polarizations.restype = ctypes.c_int
     lib.efd_hann_polarizations.argtypes = [vp, vp, vp, i64, i64, i64, vp, vp, vp]
     lib.efd_hann_loglike.restype = ctypes.c_int

@@ -3573,6 +3573,254 @@ __global__ __launch_bounds__(256) void k_hann_stage(const double2* __restrict__ 
         y[s] = v;
     }
 }
+// ---- The Hann correction's convolution as one four-step FFT pipeline (efd_hann_convolve).
+// Y = ifft_m(fft_m(y) * kf) for power-of-two m = R * C, C = 8192, R = m / C (256..4096), in
+// complex64, with y the scaled support of each row (efd_hann_stage's values, computed on the
+// fly). Index s = C r + c (row r, column c), frequency f = f_r + R f_c:
+//   (A) columns: length-R FFT over r of every column c, times w_m^(c f_r)   -> [f_r][c]
+//   (B) rows:    length-C FFT over c of every row f_r gives X[f_r + R f_c] at [f_r][f_c]; times
+//                the lag kernel's spectrum in the same order (kfp[f_r C + f_c] = kf[f_r + R f_c],
+//                1/m included); inverse length-C FFT                           -> [f_r][c]
+//   (C) columns: times w_m^(-c f_r), inverse length-R FFT over f_r          -> [r][c] = Y[s]
+// The spectrum is never put in natural order: the two transposes on each side of rocFFT's
+// 2^24-point transform (five kernels per direction) and the separate stage and multiply passes
+// are gone; three passes over Y remain. Stockham radix-8 passes (a radix-4 or -2 one last) in
+// LDS, ~70 KB per workgroup so two share a CU (one's global loads overlap the other's
+// transforms), twiddles from __sincosf (absolute error ~5e-7: the correction needs ~3 digits).
+constexpr int FC_C = 8192;             // row length (LDS: 8192 x 8 B + 1/16 padding = 68 KB)
+constexpr int FC_NT = 512;             // threads of a column or row workgroup
+constexpr float FC_2PI = 6.283185307179586f;
+constexpr float FC_SQRT_HALF = 0.70710678118654752f;
+
+__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 caddf(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csubf(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// x times -i (SIGN -1) or +i (SIGN +1)
+template <int SIGN>
+__device__ __forceinline__ float2 cmuli(float2 x) {
+    return SIGN < 0 ? make_float2(x.y, -x.x) : make_float2(-x.y, x.x);
+}
+// natural-order DFTs of 2, 4, 8 points in registers, exp(SIGN 2 pi i n k / N)
+template <int SIGN>
+__device__ __forceinline__ void fc_dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = caddf(a0, a2), t1 = csubf(a0, a2), t2 = caddf(a1, a3);
+    const float2 t3 = cmuli<SIGN>(csubf(a1, a3));
+    a0 = caddf(t0, t2);
+    a1 = caddf(t1, t3);
+    a2 = csubf(t0, t2);
+    a3 = csubf(t1, t3);
+}
+template <int SIGN>
+__device__ __forceinline__ void fc_dft8(float2* v) {
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    fc_dft4<SIGN>(e0, e1, e2, e3);
+    fc_dft4<SIGN>(o0, o1, o2, o3);
+    // o_k times w8^k: w8 = (1 + SIGN i) / sqrt 2
+    o1 = make_float2(FC_SQRT_HALF * (o1.x - SIGN * o1.y), FC_SQRT_HALF * (o1.y + SIGN * o1.x));
+    o2 = cmuli<SIGN>(o2);
+    o3 = make_float2(FC_SQRT_HALF * (-o3.x - SIGN * o3.y), FC_SQRT_HALF * (-o3.y + SIGN * o3.x));
+    v[0] = caddf(e0, o0);
+    v[1] = caddf(e1, o1);
+    v[2] = caddf(e2, o2);
+    v[3] = caddf(e3, o3);
+    v[4] = csubf(e0, o0);
+    v[5] = csubf(e1, o1);
+    v[6] = csubf(e2, o2);
+    v[7] = csubf(e3, o3);
+}
+// element e of line j in LDS: columns pass [e][j] rows padded to NCOL + 1, rows pass one line
+// with a pad element every 16
+template <int NCOL>
+struct FcColIdx {
+    __device__ __forceinline__ int operator()(int j, int e) const { return e * (NCOL + 1) + j; }
+};
+struct FcRowIdx {
+    __device__ __forceinline__ int operator()(int, int e) const { return e + (e >> 4); }
+};
+
+// One Stockham pass of radix RAD over 2^LOGL lines of length L held in LDS (in place: every
+// thread reads its butterflies into registers, barrier, writes). SIGN -1: forward.
+template <int RAD, int SIGN, int NITEM, int LOGL, class Idx>
+__device__ __forceinline__ void fc_pass(float2* sm, int L, int lgNs, Idx idx) {
+    float2 v[NITEM][RAD];
+    const int Ns = 1 << lgNs;
+    const int tid = threadIdx.x;
+    const int bfly = L / RAD;
+#pragma unroll
+    for (int q = 0; q < NITEM; ++q) {
+        const int item = tid + q * FC_NT;
+        const int j = item & ((1 << LOGL) - 1), b = item >> LOGL;
+        const int k = b & (Ns - 1);
+#pragma unroll
+        for (int r = 0; r < RAD; ++r) v[q][r] = sm[idx(j, b + r * bfly)];
+        if (lgNs > 0) {
+            float sn, cs;
+            // 2 pi k / (Ns RAD): the power-of-two division as an exponent shift
+            __sincosf((float)SIGN * FC_2PI * ldexpf((float)k, -(lgNs + (RAD == 8 ? 3 : RAD == 4 ? 2 : 1))),
+                      &sn, &cs);
+            const float2 w1 = make_float2(cs, sn);
+            float2 w = w1;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) {
+                v[q][r] = cmulf(v[q][r], w);
+                if (r + 1 < RAD) w = cmulf(w, w1);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NITEM; ++q) {
+        const int item = tid + q * FC_NT;
+        const int j = item & ((1 << LOGL) - 1), b = item >> LOGL;
+        const int d = ((b >> lgNs) << lgNs) * RAD + (b & (Ns - 1));
+        if (RAD == 8) {
+            fc_dft8<SIGN>(v[q]);
+        } else if (RAD == 4) {
+            fc_dft4<SIGN>(v[q][0], v[q][1], v[q][2], v[q][3]);
+        } else {
+            const float2 a0 = v[q][0], a1 = v[q][1];
+            v[q][0] = caddf(a0, a1);
+            v[q][1] = csubf(a0, a1);
+        }
+#pragma unroll
+        for (int r = 0; r < RAD; ++r) sm[idx(j, d + r * Ns)] = v[q][r];
+    }
+    __syncthreads();
+}
+
+// the whole length-L transform of 2^LOGL lines (natural order in, natural order out): radix-8
+// passes, then one radix-4 or radix-2 pass for the rest
+template <int SIGN, int L, int LOGL, class Idx>
+__device__ __forceinline__ void fc_fft(float2* sm, Idx idx) {
+    constexpr int N8 = ((L / 8) << LOGL) / FC_NT;
+    static_assert(((L / 8) << LOGL) % FC_NT == 0, "radix-8 butterflies: whole rounds per thread");
+    int lg = 0;
+#pragma unroll 1
+    for (; (8 << lg) <= L; lg += 3) fc_pass<8, SIGN, N8, LOGL>(sm, L, lg, idx);
+    if ((4 << lg) == L) fc_pass<4, SIGN, ((L / 4) << LOGL) / FC_NT, LOGL>(sm, L, lg, idx);
+    else if ((2 << lg) == L) fc_pass<2, SIGN, ((L / 2) << LOGL) / FC_NT, LOGL>(sm, L, lg, idx);
+}
+
+template <int R>
+struct FcCols {
+    static constexpr int NCOL = R >= 4096 ? 2 : R >= 2048 ? 4 : R >= 1024 ? 8 : 16;
+    static constexpr int LOGL = NCOL == 2 ? 1 : NCOL == 4 ? 2 : NCOL == 8 ? 3 : 4;
+};
+
+// (A) and (C): NCOL columns per workgroup. FWD: load the scaled support of row blockIdx.y
+// straight from S (efd_hann_stage's values), forward FFT, twiddle, store. Inverse: load,
+// conjugate twiddle, inverse FFT, store in natural order.
+// (<= 128 VGPRs: two 8-wave workgroups per CU, 4 waves per SIMD)
+template <bool FWD, int R>
+__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
+               float2* __restrict__ Y) {
+    constexpr int NCOL = FcCols<R>::NCOL, LOGL = FcCols<R>::LOGL;
+    constexpr int64_t M = (int64_t)R * FC_C;
+    constexpr int NQ = R * NCOL / FC_NT;   // elements per thread
+    static_assert(R * NCOL % FC_NT == 0, "whole rounds of elements per thread");
+    __shared__ float2 sm[R * (NCOL + 1)];
+    const FcColIdx<NCOL> idx;
+    const int row = blockIdx.y;
+    // XCD-aware column blocks: workgroups are dealt round-robin over the 8 XCDs (x = b mod 8),
+    // so XCD x takes the contiguous eighth [x G/8, (x+1) G/8) of the G column blocks in order;
+    // a block's rows are NCOL * 8 or 16 B wide, and the neighbouring blocks sharing their
+    // 128-B lines then hit the same L2
+    constexpr int G = FC_C / NCOL;
+    static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
+    const int c0 = ((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * NCOL;
+    float2* y = Y + (int64_t)row * M;
+    if (FWD) {
+        const HannRow h = hann_row(info, row);
+        const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;
+        const double2* src = S + (int64_t)row * stride + h.first;
+        const bool bad = h.len > M;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = threadIdx.x + q * FC_NT;
+            const int e = i / NCOL, j = i % NCOL;
+            const int64_t s = (int64_t)e * FC_C + c0 + j;
+            float2 v = make_float2(0.f, 0.f);
+            if (bad) {
+                v = make_float2(__int_as_float(0x7fc00000), 0.f);
+            } else if (s < h.len) {
+                const double2 x = src[s];
+                v = make_float2((float)(x.x * inv), (float)(x.y * inv));
+            }
+            sm[idx(j, e)] = v;
+        }
+        __syncthreads();
+        fc_fft<-1, R, LOGL>(sm, idx);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = threadIdx.x + q * FC_NT;
+            const int e = i / NCOL, j = i % NCOL;   // e = f_r
+            const int c = c0 + j;
+            const uint32_t p = (uint32_t)c * (uint32_t)e;   // < C R = M: no reduction
+            float sn, cs;
+            __sincosf(-FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
+            y[(int64_t)e * FC_C + c] = cmulf(sm[idx(j, e)], make_float2(cs, sn));
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = threadIdx.x + q * FC_NT;
+            const int e = i / NCOL, j = i % NCOL;   // e = f_r
+            const int c = c0 + j;
+            const uint32_t p = (uint32_t)c * (uint32_t)e;   // < C R = M: no reduction
+            float sn, cs;
+            __sincosf(FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
+            sm[idx(j, e)] = cmulf(y[(int64_t)e * FC_C + c], make_float2(cs, sn));
+        }
+        __syncthreads();
+        fc_fft<1, R, LOGL>(sm, idx);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = threadIdx.x + q * FC_NT;
+            const int e = i / NCOL, j = i % NCOL;
+            y[(int64_t)e * FC_C + c0 + j] = sm[idx(j, e)];
+        }
+    }
+}
+
+// (B): one row f_r per workgroup: forward FFT, times the kernel's spectrum, inverse FFT
+__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_fc_rows(const float2* __restrict__ kfp, int64_t m, int rows, float2* __restrict__ Y) {
+    __shared__ float2 sm[FC_C + FC_C / 16];
+    const FcRowIdx idx;
+    // (row f_r, walker) pairs: XCD x = b mod 8 takes the contiguous eighth of them in f_r-major
+    // order, so a kernel-spectrum row is read from HBM once per XCD and from its L2 for the
+    // group's other walkers (gridDim.x = R * rows, a multiple of 8)
+    const int64_t npair = (int64_t)gridDim.x;
+    const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
+    const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
+    float2* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C;
+    const float2* k = kfp + (int64_t)fr * FC_C;
+    constexpr int NQ = FC_C / FC_NT;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + q * FC_NT;
+        sm[idx(0, e)] = y[e];
+    }
+    __syncthreads();
+    fc_fft<-1, FC_C, 0>(sm, idx);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + q * FC_NT;
+        sm[idx(0, e)] = cmulf(sm[idx(0, e)], k[e]);
+    }
+    __syncthreads();
+    fc_fft<1, FC_C, 0>(sm, idx);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + q * FC_NT;
+        y[e] = sm[idx(0, e)];
+    }
+}
+
 // S_w at bin k: the 3-point stencil on S and the correction's difference (neighbours mod nf)
 __device__ __forceinline__ double2 hann_sw(const double2* __restrict__ S,
                                            const float2* __restrict__ Y, int64_t nf, int64_t k,
@@ -3610,39 +3858,63 @@ __global__ void k_hann_polarizations(const double2* __restrict__ S, const float2
     hp[i] = vp;
     hc[i] = vc;
 }
-// the windowed templates' log-likelihood partials, row blockIdx.y: efd_loglike's terms
-// (d - h w, product rounded then difference) for both channels of every bin [k0, nf)
+// the windowed templates' log-likelihood partials of every row: efd_loglike's terms (d - h w,
+// product rounded then difference) for both channels of every bin [k0, nf). A thread takes a bin
+// for all rows, so d and w (48 B per bin, the same for every walker) are read once per group
+// instead of once per row.
+constexpr int HANN_ROWS_MAX = 16;
 __global__ __launch_bounds__(256) void k_hann_loglike_partial(
     const double2* __restrict__ S, int64_t stride, const float2* __restrict__ Y,
     const uint64_t* __restrict__ info, int64_t m, int64_t nf, int64_t k0,
-    const double2* __restrict__ d, const double* __restrict__ w, double* __restrict__ part) {
+    const double2* __restrict__ d, const double* __restrict__ w, int rows,
+    double* __restrict__ part) {
 #pragma clang fp contract(off)
-    const int r = blockIdx.y;
-    const HannRow h = hann_row(info, r);
-    const double c = h.scale / (4.0 * (double)(nf - 1));
-    const double2* row = S + (int64_t)r * stride;
-    const float2* y = Y + (int64_t)r * m;
+    __shared__ double sc[HANN_ROWS_MAX];
+    __shared__ int64_t sfirst[HANN_ROWS_MAX];
+    if (threadIdx.x < HANN_ROWS_MAX && (int)threadIdx.x < rows) {
+        const HannRow h = hann_row(info, threadIdx.x);
+        sc[threadIdx.x] = h.scale / (4.0 * (double)(nf - 1));
+        sfirst[threadIdx.x] = h.first;
+    }
+    __syncthreads();
     const int64_t nb = nf - k0;
-    double acc = 0.0;
+    double acc[HANN_ROWS_MAX];
+#pragma unroll
+    for (int r = 0; r < HANN_ROWS_MAX; ++r) acc[r] = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
          i += (int64_t)gridDim.x * blockDim.x) {
-        double2 vp, vc;
-        hann_pol(row, y, nf, k0 + i, c, h.first, m - nf, vp, vc);
         const double2 d0 = d[i], d1 = d[nb + i];
         const double w0 = w[i], w1 = w[nb + i];
-        const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
-        const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
-        acc = fma(r0, r0, fma(i0, i0, acc));
-        acc = fma(r1, r1, fma(i1, i1, acc));
+#pragma unroll
+        for (int r = 0; r < HANN_ROWS_MAX; ++r) {
+            if (r < rows) {
+                double2 vp, vc;
+                hann_pol(S + (int64_t)r * stride, Y + (int64_t)r * m, nf, k0 + i, sc[r],
+                         sfirst[r], m - nf, vp, vc);
+                const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
+                const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
+                acc[r] = fma(r0, r0, fma(i0, i0, acc[r]));
+                acc[r] = fma(r1, r1, fma(i1, i1, acc[r]));
+            }
+        }
     }
-    __shared__ double red[256];
-    red[threadIdx.x] = acc;
+    // per row: a butterfly over each wave, then the 4 waves in turn (fixed order)
+    __shared__ double red[HANN_ROWS_MAX][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < HANN_ROWS_MAX; ++r) {
+        if (r < rows) {
+            double v = acc[r];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) red[r][wv] = v;
+        }
+    }
     __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) part[(int64_t)r * gridDim.x + blockIdx.x] = red[0];
+    if ((int)threadIdx.x < rows)
+        part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] =
+            ((red[threadIdx.x][0] + red[threadIdx.x][1]) + red[threadIdx.x][2]) +
+            red[threadIdx.x][3];
 }
 
 // fused log-likelihood partials: one workgroup per chunk, then a second pass
@@ -4479,6 +4751,39 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }
+int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                      const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream) {
+    if (!hann_rows_ok("efd_hann_convolve", S, stride, nf, rows) || !info || !kfp || !Y ||
+        m < nf || m < ((int64_t)1 << 21) || m > ((int64_t)1 << 25) || (m & (m - 1)) != 0)
+        return fail(EFD_ERR_ARG, "efd_hann_convolve: bad arguments (m: a power of two in "
+                                 "[2^21, 2^25], >= nf)");
+    hipStream_t st = (hipStream_t)stream;
+    const int R = (int)(m / FC_C);
+    float2* y = (float2*)Y;
+#define EFD_FC(RR)                                                                            \
+    do {                                                                                      \
+        constexpr int NC = FcCols<RR>::NCOL;                                                  \
+        hipLaunchKernelGGL((k_fc_cols<true, RR>), dim3(FC_C / NC, (unsigned)rows), dim3(FC_NT), \
+                           0, st, (const double2*)S, stride, info, y);                        \
+        HIP_TRY(hipGetLastError());                                                           \
+        hipLaunchKernelGGL(k_fc_rows, dim3(RR * (unsigned)rows), dim3(FC_NT), 0, st,          \
+                           (const float2*)kfp, m, (int)rows, y);                              \
+        HIP_TRY(hipGetLastError());                                                           \
+        hipLaunchKernelGGL((k_fc_cols<false, RR>), dim3(FC_C / NC, (unsigned)rows),          \
+                           dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,           \
+                           (const uint64_t*)nullptr, y);                                      \
+        HIP_TRY(hipGetLastError());                                                           \
+    } while (0)
+    switch (R) {
+        case 256: EFD_FC(256); break;
+        case 512: EFD_FC(512); break;
+        case 1024: EFD_FC(1024); break;
+        case 2048: EFD_FC(2048); break;
+        default: EFD_FC(4096); break;
+    }
+#undef EFD_FC
+    return EFD_OK;
+}
 int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
                            int64_t nf, int64_t k0, double* hp, double* hc, void* stream) {
     if (!S || !Y || !info || !hp || !hc || nf < 3 || m < nf || k0 < 0 || k0 > nf)
@@ -4497,15 +4802,15 @@ int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint
                      int64_t m, int32_t rows, int64_t nf, int64_t k0, const double* d,
                      const double* w, double* out, double* scratch, void* stream) {
     if (!hann_rows_ok("efd_hann_loglike", S, stride, nf, rows) || !Y || !info || !d || !w ||
-        !out || !scratch || m < nf || k0 < 0 || k0 >= nf)
-        return fail(EFD_ERR_ARG, "efd_hann_loglike: bad arguments");
+        !out || !scratch || m < nf || k0 < 0 || k0 >= nf || rows > HANN_ROWS_MAX)
+        return fail(EFD_ERR_ARG, "efd_hann_loglike: bad arguments (rows <= 16)");
     const int64_t nb = nf - k0;
     const int threads = 256;
     const int np = (int)std::min<int64_t>(EFD_LOGLIKE_SCRATCH, (nb + threads - 1) / threads);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)np, (unsigned)rows), dim3(threads),
-                       0, st, (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
-                       (const double2*)d, w, scratch);
+    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)np), dim3(threads), 0, st,
+                       (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
+                       (const double2*)d, w, (int)rows, scratch);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_loglike_final, dim3((unsigned)rows), dim3(256), 0, st, scratch, np, out);
     HIP_TRY(hipGetLastError());

@@ -112,8 +112,10 @@ class HannConvolution:
     first) - 1 (include/emrifd.h, efd_hann_extent). test.sh's 12.6 M-bin grid with its
     harmonics below ~15% of Nyquist takes m = 2^24, where the full-support form needs 2^25 and
     the size-N DFT form two Bluestein transforms of 2^25 each. The transforms are in place
-    (hipFFT plans per (m, rows), _hipfft); efd_hann_loglike then reduces the windowed templates'
-    logL without writing them."""
+    (power-of-two m from 2^21 to 2^25: efd_hann_convolve, one four-step FFT pipeline of three
+    passes over the rows with the staging and the kernel multiply folded in; other lengths:
+    hipFFT plans per (m, rows), _hipfft); efd_hann_loglike then reduces the windowed
+    templates' logL without writing them."""
 
     KEEP_KERNELS = 2   # lag-kernel spectra kept (one per m)
 
@@ -136,22 +138,35 @@ class HannConvolution:
         w = np.asarray(window.cpu().numpy() if hasattr(window, "detach") else window)
         return w.ndim == 1 and len(w) >= 3 and np.array_equal(w, hann(len(w)))
 
-    @staticmethod
-    def size_for(n, support):
-        """The transform length for a support of `support` bins: the smallest 2^a or 3 2^a
-        that is >= n + support - 1."""
+    @classmethod
+    def size_for(cls, n, support, four_step=True):
+        """The transform length for a support of `support` bins: >= n + support - 1, the power
+        of two when efd_hann_convolve takes it (three passes over the rows beat hipFFT's ~11 on
+        a length up to 4/3 shorter), else the smallest 2^a or 3 2^a."""
         need = int(n) + max(int(support), 1) - 1
         best = None
         for base in (1, 3):
             m = base
             while m < need:
                 m *= 2
+            if base == 1 and four_step and cls.FOUR_STEP_MIN <= m <= cls.FOUR_STEP_MAX:
+                return m
             best = m if best is None else min(best, m)
         return best
 
-    def kernel_spectrum(self, m):
-        """fft(z) / m in complex64, z[t] = K[(t - (m - n)) mod n] (computed in complex128)."""
-        kf = self._kf.get(m)
+    # efd_hann_convolve (one four-step FFT pipeline, 3 passes over the rows) takes power-of-two
+    # m in [FOUR_STEP_MIN, FOUR_STEP_MAX]; other lengths go through hipFFT
+    FOUR_STEP_MIN, FOUR_STEP_MAX, FOUR_STEP_C = 1 << 21, 1 << 25, 8192
+    four_step = True
+
+    def _four(self, m):
+        return (self.four_step and m & (m - 1) == 0
+                and self.FOUR_STEP_MIN <= m <= self.FOUR_STEP_MAX)
+
+    def kernel_spectrum(self, m, four=False):
+        """fft(z) / m in complex64, z[t] = K[(t - (m - n)) mod n] (computed in complex128); with
+        four=True in efd_hann_convolve's order: [f_r][f_c] = kf[f_r + R f_c], R = m / 8192."""
+        kf = self._kf.get((m, four))
         if kf is None:
             torch = require_gpu()
             n = self.n
@@ -162,9 +177,11 @@ class HannConvolution:
             im = torch.where(zero, torch.full_like(mm, np.pi * (n - 1) / n),
                              torch.full_like(mm, -np.pi / n))
             kf = (torch.fft.fft(torch.complex(re, im)) / m).to(torch.complex64)
+            if four:
+                kf = kf.view(self.FOUR_STEP_C, m // self.FOUR_STEP_C).t().contiguous()
             while len(self._kf) >= self.KEEP_KERNELS:
                 self._kf.pop(next(iter(self._kf)))
-            self._kf[m] = kf
+            self._kf[(m, four)] = kf
         return kf
 
     def _rows(self, S):
@@ -196,13 +213,19 @@ class HannConvolution:
         ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
         live = ext[:, 1] > 0
         support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
-        m = self.size_for(n, support)
+        m = self.size_for(n, support, self.four_step)
         need = rows * m
         if self._ybuf is None or self._ybuf.numel() < need:
             self._ybuf = None
             self._ybuf = torch.empty(need, dtype=torch.complex64, device=S.device)
         Y = self._ybuf[:need].view(rows, m)
         yp = torch.view_as_real(Y).data_ptr()
+        if self._four(m):
+            kfp = self.kernel_spectrum(m, four=True)
+            _lib.check(lib.efd_hann_convolve(sp, n, n, rows, info.data_ptr(), m,
+                                             torch.view_as_real(kfp).data_ptr(), yp, st),
+                       "efd_hann_convolve", lib)
+            return Y, info, m
         _lib.check(lib.efd_hann_stage(sp, n, n, rows, info.data_ptr(), m, yp, st),
                    "efd_hann_stage", lib)
         plan = self._plans.get((m, rows))

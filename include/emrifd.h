@@ -309,8 +309,9 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
  *   efd_hann_polarizations: h+/hx (efd_polarizations' split) of one row's S_w over bins
  *                    [k0, nf) into hp, hc (complex [nf - k0]).
  *   efd_hann_loglike: efd_loglike of every row's windowed h+/hx against d, w ([2][nf - k0],
- *                    efd_loglike's layout and rounding), out[r] (device doubles [rows]); scratch
- *                    holds rows * EFD_LOGLIKE_SCRATCH doubles. No template is written.
+ *                    efd_loglike's layout and rounding), out[r] (device doubles [rows],
+ *                    rows <= 16); scratch holds rows * EFD_LOGLIKE_SCRATCH doubles. No template
+ *                    is written.
  * Replaces: no reference function (the reference convolves each channel with scipy/cupy at
  * FDutils.py:35-47, 95-96).
  */
@@ -318,6 +319,13 @@ int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows, u
                     void* stream);
 int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
                    const uint64_t* info, int64_t m, float* Y, void* stream);
+/* efd_hann_stage + the caller's transform pair in one call, for power-of-two m in [2^21, 2^25]
+ * (a four-step FFT: column FFTs of length R = m / 8192 with the staging folded in, row FFTs
+ * of 8192 with the kernel multiply between forward and inverse, inverse column FFTs; the
+ * spectrum is never reordered). kfp: the lag kernel's spectrum / m, complex64 in the four-step
+ * order kfp[f_r 8192 + f_c] = kf[f_r + R f_c]. Leaves Y as efd_hann_stage + transforms do. */
+int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                      const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream);
 int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
                            int64_t nf, int64_t k0, double* hp, double* hc, void* stream);
 

@@ -204,3 +204,46 @@ def test_hann_loglike_matches_templates():
     got = out.cpu().numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0.0)
     np.testing.assert_allclose(got[2], float(red.loglike(None, d, w)[0]), rtol=1e-12, atol=0.0)
+
+
+@pytest.mark.parametrize("n,support,rows", [(1000001, (0.4, 0.9), 3), (12623261, (0.43, 0.57), 2)])
+def test_four_step_convolution(n, support, rows):
+    """efd_hann_convolve (the four-step complex64 FFT pipeline: m = 2^21 and 2^24 here) against
+    the same correction on hipFFT transforms and against an exact complex128 convolution
+    (torch.fft on the zero-padded support): C within 1e-5 of max|C| in both comparisons (float
+    transforms: ~1e-6; the correction needs ~3 digits), rows of different supports, one of
+    them all zero."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.fdutils import HannConvolution
+    lib = _lib.load()
+    rng = np.random.default_rng(n % 1000)
+    S = torch.zeros((rows, n), dtype=torch.complex128, device="cuda")
+    lo, hi = int(support[0] * n), int(support[1] * n)
+    for r in range(rows - 1):
+        a, b = lo + 1000 * r, hi - 7 * r
+        S[r, a:b] = torch.complex(torch.randn(b - a, dtype=torch.float64, device="cuda"),
+                                  torch.randn(b - a, dtype=torch.float64, device="cuda")) * 1e-21
+    hcv = HannConvolution(n, S.device)
+    C4 = hcv.correction(S, lib)
+    m = hcv.size_for(n, hi - lo)
+    assert hcv._four(m), m
+    hcv.four_step = False
+    C_fft = hcv.correction(S, lib)
+    hcv.four_step = True
+    # exact: the circular convolution with K as one complex128 linear convolution
+    k = torch.arange(-(n - 1), n, device="cuda", dtype=torch.int64)
+    mm = torch.remainder(k, n).to(torch.float64)
+    zero = mm == 0
+    K = torch.complex(torch.where(zero, torch.zeros_like(mm), (np.pi / n) / torch.tan(np.pi * mm / n)),
+                      torch.where(zero, torch.full_like(mm, np.pi * (n - 1) / n),
+                                  torch.full_like(mm, -np.pi / n)))
+    L = 1 << (3 * n - 2).bit_length()
+    Kf = torch.fft.fft(K, L)
+    for r in range(rows - 1):
+        # K at lag u = k - j in (-n, n) sits at u + n - 1, so C[k] = (S * K)[k + n - 1]
+        C = torch.fft.ifft(torch.fft.fft(S[r], L) * Kf)[n - 1:2 * n - 1]
+        scale = float(C.abs().max())
+        assert float((C4[r] - C_fft[r]).abs().max()) <= 1e-5 * scale
+        assert float((C4[r] - C).abs().max()) <= 1e-5 * scale
+        del C
+    assert float(C4[-1].abs().max()) == 0.0 and float(C_fft[-1].abs().max()) == 0.0
