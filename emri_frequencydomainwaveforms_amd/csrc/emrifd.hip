@@ -3635,7 +3635,9 @@ __device__ __forceinline__ void fc_dft8(float2* v) {
 // with a pad element every 16
 template <int NCOL>
 struct FcColIdx {
-    __device__ __forceinline__ int operator()(int j, int e) const { return e * (NCOL + 1) + j; }
+    // (2 columns: no pad, so m = 2^25's 4096-row blocks fit two workgroups per CU)
+    static constexpr int STRIDE = NCOL > 2 ? NCOL + 1 : NCOL;
+    __device__ __forceinline__ int operator()(int j, int e) const { return e * STRIDE + j; }
 };
 struct FcRowIdx {
     __device__ __forceinline__ int operator()(int, int e) const { return e + (e >> 4); }
@@ -3722,7 +3724,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
     constexpr int64_t M = (int64_t)R * FC_C;
     constexpr int NQ = R * NCOL / FC_NT;   // elements per thread
     static_assert(R * NCOL % FC_NT == 0, "whole rounds of elements per thread");
-    __shared__ float2 sm[R * (NCOL + 1)];
+    __shared__ float2 sm[R * FcColIdx<NCOL>::STRIDE];
     const FcColIdx<NCOL> idx;
     const int row = blockIdx.y;
     // XCD-aware column blocks: workgroups are dealt round-robin over the 8 XCDs (x = b mod 8),
