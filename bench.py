@@ -9,7 +9,7 @@ p0 solved so the inspiral lasts 0.99 * Tobs (README's p0 = 12 is overwritten lik
 emri_pe.py:623-635), Tobs = 2 yr, dt = 10 s (N_f = 6,311,631 two-sided bins), eps = 1e-5
 (~3000 harmonics), K_{1/3} uniform SPA (the reference notebook's form). Inputs (sparse
 trajectory, amplitudes, Ylm; host stand-ins, NOT FEW physics) are resident in HBM before timing.
-One step = a batch of B (--batch, default 4) full FD waveforms on the device, each with its own
+One step = a batch of B (--batch, default 8) full FD waveforms on the device, each with its own
 workspace and outputs: spline build -> inverse splines -> interval records -> tile lists -> mode
 sum -> h+/hx over f >= 0 (the Likelihood path, emri_pe.py:241, for a batch of walkers). With
 --pipeline overlap (default) batch i+1's preparation (grouping, splines, records: latency-bound
@@ -17,7 +17,9 @@ kernels on few CUs; one efd_modesum_prepare_batch for the B waveforms) runs on a
 beside batch i's
 mode sums, which run as one launch (efd_modesum_sum_batch: the B waveforms' tiles in one
 longest-first dispatch) and write h+/hx themselves (fused polarisations). value counts
-waveforms (B per step); --batch 1 runs one efd_modesum_sum per waveform.
+waveforms (B per step); --batch 1 runs one efd_modesum_sum per waveform. B = 8 since round 4's
+768-lane tiles (paired A/B against 2 / 4 / 6 / 12 / 16: 0.951 / 0.987 / 0.997 / 0.997 / 0.997,
+profiles/r04_ab_batch.jsonl); round 3's 512-lane tiles were best at 4.
 
 Multi-GPU: one process per GPU; each rank generates its own waveforms (the walker batch of
 emri_pe.py shards with no data-path exchange: weak scaling); value = all ranks' waveforms / the
@@ -289,7 +291,7 @@ def main():
     ap.add_argument("--slots", type=int, default=2,
                     help="overlap pipeline depth: batches in flight (preparation runs up to "
                          "slots - 1 batches ahead of the sum)")
-    ap.add_argument("--batch", type=int, default=4,
+    ap.add_argument("--batch", type=int, default=8,
                     help="overlap pipeline: waveforms per step, their mode sums in one launch "
                          "(efd_modesum_sum_batch; 1 = one efd_modesum_sum per waveform)")
     ap.add_argument("--prep", default="batch", choices=["single", "batch"],
