@@ -206,9 +206,13 @@ def test_hann_loglike_matches_templates():
     np.testing.assert_allclose(got[2], float(red.loglike(None, d, w)[0]), rtol=1e-12, atol=0.0)
 
 
-@pytest.mark.parametrize("n,support,rows", [(1000001, (0.4, 0.9), 3), (12623261, (0.43, 0.57), 2)])
-def test_four_step_convolution(n, support, rows):
-    """efd_hann_convolve (the four-step complex64 FFT pipeline: m = 2^21 and 2^24 here) against
+@pytest.mark.parametrize("n,support,rows,m", [
+    (1000001, (0.4, 0.9), 3, 1 << 21), (2000001, (0.3, 0.9), 2, 1 << 22),
+    (4000001, (0.3, 0.9), 2, 1 << 23), (12623261, (0.43, 0.57), 2, 1 << 24),
+    (12623261, (0.2, 0.8), 2, 1 << 25)])
+def test_four_step_convolution(n, support, rows, m):
+    """efd_hann_convolve (the four-step complex64 FFT pipeline, every column length it has:
+    m = 2^21 .. 2^25, R = m / 8192 = 256 .. 4096) against
     the same correction on hipFFT transforms and against an exact complex128 convolution
     (torch.fft on the zero-padded support): C within 1e-5 of max|C| in both comparisons (float
     transforms: ~1e-6; the correction needs ~3 digits), rows of different supports, one of
@@ -225,8 +229,7 @@ def test_four_step_convolution(n, support, rows):
                                   torch.randn(b - a, dtype=torch.float64, device="cuda")) * 1e-21
     hcv = HannConvolution(n, S.device)
     C4 = hcv.correction(S, lib)
-    m = hcv.size_for(n, hi - lo)
-    assert hcv._four(m), m
+    assert hcv.size_for(n, hi - lo) == m and hcv._four(m), m
     hcv.four_step = False
     C_fft = hcv.correction(S, lib)
     hcv.four_step = True
