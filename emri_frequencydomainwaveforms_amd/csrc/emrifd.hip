@@ -3592,44 +3592,48 @@ constexpr int FC_NT = 512;             // threads of a column or row workgroup
 constexpr float FC_2PI = 6.283185307179586f;
 constexpr float FC_SQRT_HALF = 0.70710678118654752f;
 
-__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+// complex64 values as 2-wide float vectors: the arithmetic below compiles to packed FP32
+// instructions (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32, one issue slot per complex add or
+// half a complex multiply), about half the VALU instructions of scalar float2 code
+typedef float fcv __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fcv cmulf(fcv a, fcv b) {
+    const fcv t = a.xx * b;
+    return __builtin_elementwise_fma(a.yy, b.yx * (fcv){-1.0f, 1.0f}, t);
 }
-__device__ __forceinline__ float2 caddf(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csubf(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 // x times -i (SIGN -1) or +i (SIGN +1)
 template <int SIGN>
-__device__ __forceinline__ float2 cmuli(float2 x) {
-    return SIGN < 0 ? make_float2(x.y, -x.x) : make_float2(-x.y, x.x);
+__device__ __forceinline__ fcv cmuli(fcv x) {
+    return x.yx * (SIGN < 0 ? (fcv){1.0f, -1.0f} : (fcv){-1.0f, 1.0f});
 }
-// natural-order DFTs of 2, 4, 8 points in registers, exp(SIGN 2 pi i n k / N)
+// natural-order DFTs of 4 and 8 points in registers, exp(SIGN 2 pi i n k / N)
 template <int SIGN>
-__device__ __forceinline__ void fc_dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
-    const float2 t0 = caddf(a0, a2), t1 = csubf(a0, a2), t2 = caddf(a1, a3);
-    const float2 t3 = cmuli<SIGN>(csubf(a1, a3));
-    a0 = caddf(t0, t2);
-    a1 = caddf(t1, t3);
-    a2 = csubf(t0, t2);
-    a3 = csubf(t1, t3);
+__device__ __forceinline__ void fc_dft4(fcv& a0, fcv& a1, fcv& a2, fcv& a3) {
+    const fcv t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3;
+    const fcv t3 = cmuli<SIGN>(a1 - a3);
+    a0 = t0 + t2;
+    a1 = t1 + t3;
+    a2 = t0 - t2;
+    a3 = t1 - t3;
 }
 template <int SIGN>
-__device__ __forceinline__ void fc_dft8(float2* v) {
-    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
-    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+__device__ __forceinline__ void fc_dft8(fcv* v) {
+    fcv e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    fcv o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
     fc_dft4<SIGN>(e0, e1, e2, e3);
     fc_dft4<SIGN>(o0, o1, o2, o3);
-    // o_k times w8^k: w8 = (1 + SIGN i) / sqrt 2
-    o1 = make_float2(FC_SQRT_HALF * (o1.x - SIGN * o1.y), FC_SQRT_HALF * (o1.y + SIGN * o1.x));
+    // o_k times w8^k, w8 = (1 + SIGN i) / sqrt 2: w8 o = (o + SIGN i o) / sqrt 2,
+    // w8^3 o = (-o + SIGN i o) / sqrt 2
+    o1 = FC_SQRT_HALF * (o1 + cmuli<SIGN>(o1));
     o2 = cmuli<SIGN>(o2);
-    o3 = make_float2(FC_SQRT_HALF * (-o3.x - SIGN * o3.y), FC_SQRT_HALF * (-o3.y + SIGN * o3.x));
-    v[0] = caddf(e0, o0);
-    v[1] = caddf(e1, o1);
-    v[2] = caddf(e2, o2);
-    v[3] = caddf(e3, o3);
-    v[4] = csubf(e0, o0);
-    v[5] = csubf(e1, o1);
-    v[6] = csubf(e2, o2);
-    v[7] = csubf(e3, o3);
+    o3 = FC_SQRT_HALF * (cmuli<SIGN>(o3) - o3);
+    v[0] = e0 + o0;
+    v[1] = e1 + o1;
+    v[2] = e2 + o2;
+    v[3] = e3 + o3;
+    v[4] = e0 - o0;
+    v[5] = e1 - o1;
+    v[6] = e2 - o2;
+    v[7] = e3 - o3;
 }
 // element e of line j in LDS: columns pass [e][j] rows padded to NCOL + 1, rows pass one line
 // with a pad element every 16
@@ -3646,8 +3650,8 @@ struct FcRowIdx {
 // One Stockham pass of radix RAD over 2^LOGL lines of length L held in LDS (in place: every
 // thread reads its butterflies into registers, barrier, writes). SIGN -1: forward.
 template <int RAD, int SIGN, int NITEM, int LOGL, class Idx>
-__device__ __forceinline__ void fc_pass(float2* sm, int L, int lgNs, Idx idx) {
-    float2 v[NITEM][RAD];
+__device__ __forceinline__ void fc_pass(fcv* sm, int L, int lgNs, Idx idx) {
+    fcv v[NITEM][RAD];
     const int Ns = 1 << lgNs;
     const int tid = threadIdx.x;
     const int bfly = L / RAD;
@@ -3663,8 +3667,8 @@ __device__ __forceinline__ void fc_pass(float2* sm, int L, int lgNs, Idx idx) {
             // 2 pi k / (Ns RAD): the power-of-two division as an exponent shift
             __sincosf((float)SIGN * FC_2PI * ldexpf((float)k, -(lgNs + (RAD == 8 ? 3 : RAD == 4 ? 2 : 1))),
                       &sn, &cs);
-            const float2 w1 = make_float2(cs, sn);
-            float2 w = w1;
+            const fcv w1 = {cs, sn};
+            fcv w = w1;
 #pragma unroll
             for (int r = 1; r < RAD; ++r) {
                 v[q][r] = cmulf(v[q][r], w);
@@ -3683,9 +3687,9 @@ __device__ __forceinline__ void fc_pass(float2* sm, int L, int lgNs, Idx idx) {
         } else if (RAD == 4) {
             fc_dft4<SIGN>(v[q][0], v[q][1], v[q][2], v[q][3]);
         } else {
-            const float2 a0 = v[q][0], a1 = v[q][1];
-            v[q][0] = caddf(a0, a1);
-            v[q][1] = csubf(a0, a1);
+            const fcv a0 = v[q][0], a1 = v[q][1];
+            v[q][0] = a0 + a1;
+            v[q][1] = a0 - a1;
         }
 #pragma unroll
         for (int r = 0; r < RAD; ++r) sm[idx(j, d + r * Ns)] = v[q][r];
@@ -3696,7 +3700,7 @@ __device__ __forceinline__ void fc_pass(float2* sm, int L, int lgNs, Idx idx) {
 // the whole length-L transform of 2^LOGL lines (natural order in, natural order out): radix-8
 // passes, then one radix-4 or radix-2 pass for the rest
 template <int SIGN, int L, int LOGL, class Idx>
-__device__ __forceinline__ void fc_fft(float2* sm, Idx idx) {
+__device__ __forceinline__ void fc_fft(fcv* sm, Idx idx) {
     constexpr int N8 = ((L / 8) << LOGL) / FC_NT;
     static_assert(((L / 8) << LOGL) % FC_NT == 0, "radix-8 butterflies: whole rounds per thread");
     int lg = 0;
@@ -3719,12 +3723,13 @@ struct FcCols {
 template <bool FWD, int R>
 __global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
-               float2* __restrict__ Y) {
+               float2* __restrict__ Yv) {
     constexpr int NCOL = FcCols<R>::NCOL, LOGL = FcCols<R>::LOGL;
     constexpr int64_t M = (int64_t)R * FC_C;
     constexpr int NQ = R * NCOL / FC_NT;   // elements per thread
     static_assert(R * NCOL % FC_NT == 0, "whole rounds of elements per thread");
-    __shared__ float2 sm[R * FcColIdx<NCOL>::STRIDE];
+    __shared__ fcv sm[R * FcColIdx<NCOL>::STRIDE];
+    fcv* Y = reinterpret_cast<fcv*>(Yv);
     const FcColIdx<NCOL> idx;
     const int row = blockIdx.y;
     // XCD-aware column blocks: workgroups are dealt round-robin over the 8 XCDs (x = b mod 8),
@@ -3734,7 +3739,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
     constexpr int G = FC_C / NCOL;
     static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
     const int c0 = ((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * NCOL;
-    float2* y = Y + (int64_t)row * M;
+    fcv* y = Y + (int64_t)row * M;
     if (FWD) {
         const HannRow h = hann_row(info, row);
         const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;
@@ -3745,12 +3750,12 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
             const int i = threadIdx.x + q * FC_NT;
             const int e = i / NCOL, j = i % NCOL;
             const int64_t s = (int64_t)e * FC_C + c0 + j;
-            float2 v = make_float2(0.f, 0.f);
+            fcv v = {0.f, 0.f};
             if (bad) {
-                v = make_float2(__int_as_float(0x7fc00000), 0.f);
+                v = (fcv){__int_as_float(0x7fc00000), 0.f};
             } else if (s < h.len) {
                 const double2 x = src[s];
-                v = make_float2((float)(x.x * inv), (float)(x.y * inv));
+                v = (fcv){(float)(x.x * inv), (float)(x.y * inv)};
             }
             sm[idx(j, e)] = v;
         }
@@ -3764,7 +3769,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
             const uint32_t p = (uint32_t)c * (uint32_t)e;   // < C R = M: no reduction
             float sn, cs;
             __sincosf(-FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
-            y[(int64_t)e * FC_C + c] = cmulf(sm[idx(j, e)], make_float2(cs, sn));
+            y[(int64_t)e * FC_C + c] = cmulf(sm[idx(j, e)], (fcv){cs, sn});
         }
     } else {
 #pragma unroll
@@ -3775,7 +3780,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
             const uint32_t p = (uint32_t)c * (uint32_t)e;   // < C R = M: no reduction
             float sn, cs;
             __sincosf(FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
-            sm[idx(j, e)] = cmulf(y[(int64_t)e * FC_C + c], make_float2(cs, sn));
+            sm[idx(j, e)] = cmulf(y[(int64_t)e * FC_C + c], (fcv){cs, sn});
         }
         __syncthreads();
         fc_fft<1, R, LOGL>(sm, idx);
@@ -3790,8 +3795,10 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
 
 // (B): one row f_r per workgroup: forward FFT, times the kernel's spectrum, inverse FFT
 __global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
-void k_fc_rows(const float2* __restrict__ kfp, int64_t m, int rows, float2* __restrict__ Y) {
-    __shared__ float2 sm[FC_C + FC_C / 16];
+void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
+    __shared__ fcv sm[FC_C + FC_C / 16];
+    const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
+    fcv* Y = reinterpret_cast<fcv*>(Yv);
     const FcRowIdx idx;
     // (row f_r, walker) pairs: XCD x = b mod 8 takes the contiguous eighth of them in f_r-major
     // order, so a kernel-spectrum row is read from HBM once per XCD and from its L2 for the
@@ -3799,8 +3806,8 @@ void k_fc_rows(const float2* __restrict__ kfp, int64_t m, int rows, float2* __re
     const int64_t npair = (int64_t)gridDim.x;
     const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
     const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
-    float2* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C;
-    const float2* k = kfp + (int64_t)fr * FC_C;
+    fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C;
+    const fcv* k = kfp + (int64_t)fr * FC_C;
     constexpr int NQ = FC_C / FC_NT;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
