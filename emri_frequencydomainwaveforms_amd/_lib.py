@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "efd_download",
     "efd_stream_order",
     "efd_polarizations",
+    "efd_modesum_lane_ranges",
     "efd_hann_extent",
     "efd_hann_stage",
     "efd_hann_convolve",
@@ -219,8 +220,10 @@ def load(path=None):
         lib.efd_stream_order.argtypes = [vp, ctypes.POINTER(vp), i32]
     lib.efd_polarizations.restype = ctypes.c_int
     lib.efd_polarizations.argtypes = [vp, i64, i64, vp, vp, vp]
+    lib.efd_modesum_lane_ranges.restype = ctypes.c_int
+    lib.efd_modesum_lane_ranges.argtypes = [vp, i32, vp, vp]
     lib.efd_hann_extent.restype = ctypes.c_int
-    lib.efd_hann_extent.argtypes = [vp, i64, i64, i32, vp, vp]
+    lib.efd_hann_extent.argtypes = [vp, i64, i64, i32, vp, vp, vp]
     lib.efd_hann_stage.restype = ctypes.c_int
     lib.efd_hann_stage.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp]
     lib.efd_hann_convolve.restype = ctypes.c_int

@@ -3012,6 +3012,14 @@ struct StatusBatch {
     Header* h[EFD_BATCH_MAX];
     int32_t n;
 };
+// efd_modesum_lane_ranges: each workspace's [lane_lo, lane_hi) (k_segment_compact's union of the
+// segments' lane ranges) into out[2 i], out[2 i + 1]
+__global__ __launch_bounds__(64) void k_lane_gather(const StatusBatch sb, int32_t* out) {
+    const int i = threadIdx.x;
+    if (i >= sb.n) return;
+    out[2 * i] = sb.h[i]->lane_lo;
+    out[2 * i + 1] = sb.h[i]->lane_hi;
+}
 __global__ __launch_bounds__(64) void k_status_gather(const StatusBatch sb, int32_t* out) {
     const int i = threadIdx.x;
     if (i >= sb.n) return;
@@ -3495,11 +3503,25 @@ __global__ void k_hann_info_init(uint64_t* __restrict__ info, int32_t rows) {
     info[4 * r + 2] = 0;
     info[4 * r + 3] = 0;
 }
+// lanes (optional, int32 [rows][2]): each row's paired-grid lane range from its mode sum
+// (efd_modesum_lane_ranges); bins outside {l, nf-1-l : lo <= l < hi} hold no term, so the scan
+// covers [min(lo, nf-hi), max(hi, nf-lo)) only
 __global__ __launch_bounds__(256) void k_hann_extent(const double2* __restrict__ S, int64_t stride,
-                                                     int64_t nf, uint64_t* __restrict__ info) {
+                                                     int64_t nf, const int32_t* __restrict__ lanes,
+                                                     uint64_t* __restrict__ info) {
     const double2* row = S + (int64_t)blockIdx.y * stride;
+    int64_t k_lo = 0, k_hi = nf;
+    if (lanes != nullptr) {
+        const int64_t llo = lanes[2 * blockIdx.y], lhi = lanes[2 * blockIdx.y + 1];
+        if (llo >= lhi) {
+            k_hi = 0;   // no segment: an all-zero row
+        } else {
+            k_lo = max((int64_t)0, min(llo, nf - lhi));
+            k_hi = min(nf, max(lhi, nf - llo));
+        }
+    }
     uint64_t mx = 0, lo = ~0ull, hi = 0;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nf;
+    for (int64_t k = k_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < k_hi;
          k += (int64_t)gridDim.x * blockDim.x) {
         const double2 v = row[k];
         const uint64_t bx = (uint64_t)__double_as_longlong(fabs(v.x));
@@ -4529,6 +4551,21 @@ int efd_modesum_status(const void* workspace, void* stream) {
     return EFD_OK;
 }
 
+int efd_modesum_lane_ranges(void* const* workspace, int32_t count, int32_t* out, void* stream) {
+    if (!workspace || !out || count < 1 || count > EFD_BATCH_MAX)
+        return fail(EFD_ERR_ARG, "efd_modesum_lane_ranges: NULL argument or count out of range "
+                                 "[1, EFD_BATCH_MAX]");
+    StatusBatch sb{};
+    sb.n = count;
+    for (int i = 0; i < count; ++i) {
+        if (!workspace[i]) return fail(EFD_ERR_ARG, "efd_modesum_lane_ranges: NULL workspace");
+        sb.h[i] = (Header*)workspace[i];
+    }
+    hipLaunchKernelGGL(k_lane_gather, dim3(1), dim3(64), 0, (hipStream_t)stream, sb, out);
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+
 int efd_modesum_status_batch(void* const* workspace, int32_t count, int32_t* flags,
                              void* stream) {
     if (!workspace || count < 1 || count > EFD_BATCH_MAX)
@@ -4736,17 +4773,19 @@ static bool hann_rows_ok(const char* fn, const void* S, int64_t stride, int64_t 
     }
     return true;
 }
-int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows, uint64_t* info,
-                    void* stream) {
+int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                    const int32_t* lanes, uint64_t* info, void* stream) {
     if (!hann_rows_ok("efd_hann_extent", S, stride, nf, rows) || !info)
         return fail(EFD_ERR_ARG, "efd_hann_extent: bad arguments");
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_hann_info_init, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, info,
                        rows);
     HIP_TRY(hipGetLastError());
-    const int64_t blocks = std::min<int64_t>(std::max(64, 1024 / rows), (nf + 255) / 256);
+    // (with lane ranges the rows' supports are a fraction of the grid: fewer workgroups)
+    const int64_t cap = lanes ? std::max(16, 256 / rows) : std::max(64, 1024 / rows);
+    const int64_t blocks = std::min<int64_t>(cap, (nf + 255) / 256);
     hipLaunchKernelGGL(k_hann_extent, dim3((unsigned)blocks, (unsigned)rows), dim3(256), 0, st,
-                       (const double2*)S, stride, nf, info);
+                       (const double2*)S, stride, nf, lanes, info);
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }

@@ -194,11 +194,12 @@ class HannConvolution:
                              f"{self.device}")
         return S
 
-    def transform(self, S, lib):
+    def transform(self, S, lib, lanes=None):
         """(Y, info, m) for the rows of S ([rows][n], complex128, contiguous): Y complex64
         [rows][m] holds each row's C / scale at ((k - first) mod n) + m - n (efd_hann_stage's
         layout after the transform pair); info int64 [rows][4] (efd_hann_extent). One host
-        synchronisation: the rows' supports choose m."""
+        synchronisation: the rows' supports choose m. lanes: the rows' lane ranges
+        (GenerateEMRIWaveform.spectrum_batch), so the extent reads only their bins."""
         from . import _hipfft, _lib
         torch = require_gpu()
         S = self._rows(S)
@@ -208,8 +209,13 @@ class HannConvolution:
             self._info = torch.empty((rows, 4), dtype=torch.int64, device=S.device)
         info = self._info[:rows]
         sp = torch.view_as_real(S).data_ptr()
-        _lib.check(lib.efd_hann_extent(sp, n, n, rows, info.data_ptr(), st), "efd_hann_extent",
-                   lib)
+        lp = None
+        if lanes is not None:
+            if tuple(lanes.shape) != (rows, 2) or lanes.dtype != torch.int32:
+                raise ValueError("lanes: int32 [rows][2]")
+            lp = lanes.data_ptr()
+        _lib.check(lib.efd_hann_extent(sp, n, n, rows, lp, info.data_ptr(), st),
+                   "efd_hann_extent", lib)
         ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
         live = ext[:, 1] > 0
         support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
@@ -250,13 +256,13 @@ class HannConvolution:
         C = torch.gather(Y, 1, q).to(torch.complex128) * scale[:, None]
         return C[0] if one else C
 
-    def polarizations_batch(self, S, outs, k0, lib):
+    def polarizations_batch(self, S, outs, k0, lib, lanes=None):
         """polarizations for every row of S ([B][n], contiguous): one transform pair over the
         rows and one efd_hann_polarizations per row into outs[i] = (hp, hc)."""
         from . import _lib
         torch = require_gpu()
         S = self._rows(S)
-        Y, info, m = self.transform(S, lib)
+        Y, info, m = self.transform(S, lib, lanes)
         st = torch.cuda.current_stream(S.device).cuda_stream
         for i, (hp, hc) in enumerate(outs):
             _lib.check(lib.efd_hann_polarizations(
@@ -270,7 +276,7 @@ class HannConvolution:
         self.polarizations_batch(self._rows(S), [(hp, hc)], k0, lib)
         return hp, hc
 
-    def loglike_batch(self, S, d, w, k0, out, scratch, lib):
+    def loglike_batch(self, S, d, w, k0, out, scratch, lib, lanes=None):
         """efd_hann_loglike: the logL of every row's windowed template against d, w
         (efd_loglike's [2][n - k0] layout) into out (float64 device [rows]); scratch holds
         rows * EFD_LOGLIKE_SCRATCH doubles."""
@@ -278,7 +284,7 @@ class HannConvolution:
         torch = require_gpu()
         S = self._rows(S)
         rows = int(S.shape[0])
-        Y, info, m = self.transform(S, lib)
+        Y, info, m = self.transform(S, lib, lanes)
         st = torch.cuda.current_stream(S.device).cuda_stream
         _lib.check(lib.efd_hann_loglike(
             torch.view_as_real(S).data_ptr(), self.n, torch.view_as_real(Y).data_ptr(),
@@ -418,7 +424,8 @@ class get_fd_waveform_fromFD:
 
     def _spectra(self, params, **kwargs):
         """Every walker's two-sided spectrum in one [B][N] buffer; returns (rows,
-        create_waveform, whether the per-walker path ran: its device status is still unread)."""
+        create_waveform, whether the per-walker path ran: its device status is still unread,
+        the rows' lane ranges or None)."""
         torch = require_gpu()
         if not self.can_fill_batch:
             raise ValueError("the Hann-window spectrum path only")
@@ -432,17 +439,22 @@ class get_fd_waveform_fromFD:
             buf = self._sbuf = torch.empty((B, n), dtype=torch.complex128, device=dev)
         single = not (hasattr(gen, "spectrum_batch") and
                       gen.waveform_generator.output_type == "fd")
+        lanes = None
         if not single:
             # packed uploads, batched preparation and one sum launch per group of walkers
-            # (device-side errors raise in there)
-            gen.spectrum_batch(params, buf[:B], **kwargs)
+            # (device-side errors raise in there); each row's lane range for the extent scan
+            lb = getattr(self, "_lanes", None)
+            if lb is None or lb.shape[0] < B or lb.device != dev:
+                lb = self._lanes = torch.empty((max(B, 16), 2), dtype=torch.int32, device=dev)
+            lanes = lb[:B]
+            gen.spectrum_batch(params, buf[:B], lanes=lanes, **kwargs)
         else:
             for i, p in enumerate(params):
                 gen._spectrum(*p, out=buf[i], check=False, **kwargs)
         cw = gen.waveform_generator.create_waveform
         if self._suffix_k0 != cw.positive_start():
             raise ValueError("positive_frequency_mask does not match the generator's grid")
-        return buf[:B], cw, single
+        return buf[:B], cw, single, lanes
 
     def _status(self, cw, single):
         if single and not cw.engine.status():
@@ -458,9 +470,9 @@ class get_fd_waveform_fromFD:
         checked once, at the end."""
         if len(params) == 0:
             return outs
-        S, cw, single = self._spectra(params, **kwargs)
+        S, cw, single, lanes = self._spectra(params, **kwargs)
         self._hann.polarizations_batch(S, [(o[0], o[1]) for o in outs], self._suffix_k0,
-                                       cw.engine.lib)
+                                       cw.engine.lib, lanes)
         self._status(cw, single)
         return outs
 
@@ -471,8 +483,8 @@ class get_fd_waveform_fromFD:
         written). The same logL as fill_batch + efd_loglike up to the reduction order."""
         if len(params) == 0:
             return out
-        S, cw, single = self._spectra(params, **kwargs)
-        self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib)
+        S, cw, single, lanes = self._spectra(params, **kwargs)
+        self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib, lanes)
         self._status(cw, single)
         return out
 

@@ -420,19 +420,24 @@ class GenerateEMRIWaveform:
                                                            hc=torch.view_as_real(out[j, 1])),
                                T, dt, eps, f_arr, kwargs)
 
-    def spectrum_batch(self, params, out, T=1.0, dt=10.0, eps=1e-5, f_arr=None, **kwargs):
+    def spectrum_batch(self, params, out, T=1.0, dt=10.0, eps=1e-5, f_arr=None, lanes=None,
+                       **kwargs):
         """The two-sided spectra S = h+ - i hx of every row of params into the rows of out
         (complex128 [B][N], contiguous rows, on the device): generate_batch's device groups
         with the sum writing S (the windowed templates' input, fdutils.HannConvolution); bitwise
-        the spectrum path's S of each row."""
+        the spectrum path's S of each row. lanes (int32 [B][2] on the device, optional): each
+        row's lane range (efd_modesum_lane_ranges), the bins its terms can reach."""
         torch = require_gpu()
         n = self._batch_grid(T, dt, f_arr)[0]
         B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
         if (out.dim() != 2 or tuple(out.shape) != (B, n) or out.dtype != torch.complex128
                 or not out.is_contiguous()):
             raise ValueError(f"out must be contiguous complex128 [{B}][{n}]")
+        if lanes is not None and (tuple(lanes.shape) != (B, 2) or lanes.dtype != torch.int32
+                                  or not lanes.is_contiguous()):
+            raise ValueError(f"lanes must be contiguous int32 [{B}][2]")
         return self._run_batch(params, out, lambda j: dict(out=torch.view_as_real(out[j])),
-                               T, dt, eps, f_arr, kwargs)
+                               T, dt, eps, f_arr, kwargs, lanes=lanes)
 
     def _batch_grid(self, T, dt, f_arr):
         gen = self.waveform_generator
@@ -444,7 +449,7 @@ class GenerateEMRIWaveform:
             raise ValueError("the batched generator needs a symmetric grid")
         return int(freq.numel()), int(freq.numel()) - cw._k0
 
-    def _run_batch(self, params, out, outputs, T, dt, eps, f_arr, kwargs):
+    def _run_batch(self, params, out, outputs, T, dt, eps, f_arr, kwargs, lanes=None):
         torch = require_gpu()
         from .summation import BatchPreparer, sum_batch
         cw = self.waveform_generator.create_waveform
@@ -473,6 +478,10 @@ class GenerateEMRIWaveform:
                 s_sum.wait_stream(prep.stream(gi))
                 sum_batch([(eng, dict(kw, **outputs(g0 + i)))
                            for i, (eng, kw) in enumerate(jobs)], stream=s_sum.cuda_stream)
+                if lanes is not None:   # before the group's workspaces are released
+                    _lib.check(prep.lib.efd_modesum_lane_ranges(
+                        prep.groups[gi]["pw"], len(jobs), lanes[g0].data_ptr(),
+                        s_sum.cuda_stream), "efd_modesum_lane_ranges", prep.lib)
                 ev = st["ev"][gi]
                 ev.record(s_sum)
                 prep.release(gi, ev)

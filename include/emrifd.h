@@ -202,6 +202,11 @@ int efd_modesum_sum_loglike_ex(const efd_modesum_args* const* a, void* const* wo
  * workspace another call prepared) -> EFD_ERR_HIP. Reported flags are cleared. */
 int efd_modesum_status(const void* workspace, void* stream);
 
+/* Each workspace's lane range [lane_lo, lane_hi) after its preparation: the union of its
+ * harmonics' segment lane ranges (on symmetric grids lane l is bin l and its mirror nf-1-l; no
+ * term reaches a bin outside), into out[2 i], out[2 i + 1] (device int32), stream-ordered. */
+int efd_modesum_lane_ranges(void* const* workspace, int32_t count, int32_t* out, void* stream);
+
 /*
  * efd_modesum_status for `count` workspaces (1 <= count <= EFD_BATCH_MAX) used on `stream`: one
  * gather launch and one synchronisation for a walker batch. flags (optional, int32[count])
@@ -301,7 +306,9 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
  * info[r] (4 x uint64 per row, device) = {bits of scale = max(|Re|, |Im|) over the row, first
  * nonzero bin, last nonzero bin + 1, 0} (first = ~0, last = 0 for an all-zero row; a NaN makes
  * the scale NaN); Y complex64 [rows][m], m >= nf + (last - first) - 1.
- *   efd_hann_extent: info from S.
+ *   efd_hann_extent: info from S. lanes (NULL, or device int32 [rows][2] from
+ *                    efd_modesum_lane_ranges on the rows' workspaces, symmetric grids): only
+ *                    the bins those lanes and their mirrors cover are read.
  *   efd_hann_stage:  Y[r][s] = S[r][first + s] / scale for s < last - first, 0 up to m. The
  *                    caller transforms Y in place: forward, times the lag kernel's spectrum
  *                    (z[t] = K[(t - (m - nf)) mod nf] / m), backward; then
@@ -315,8 +322,8 @@ int efd_polarizations(const double* S, int64_t nf, int64_t k0, double* hp, doubl
  * Replaces: no reference function (the reference convolves each channel with scipy/cupy at
  * FDutils.py:35-47, 95-96).
  */
-int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows, uint64_t* info,
-                    void* stream);
+int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                    const int32_t* lanes, uint64_t* info, void* stream);
 int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
                    const uint64_t* info, int64_t m, float* Y, void* stream);
 /* efd_hann_stage + the caller's transform pair in one call, for power-of-two m in [2^21, 2^25]

@@ -250,3 +250,30 @@ def test_four_step_convolution(n, support, rows, m):
         assert float((C4[r] - C).abs().max()) <= 1e-5 * scale
         del C
     assert float(C4[-1].abs().max()) == 0.0 and float(C_fft[-1].abs().max()) == 0.0
+
+
+def test_extent_from_lane_ranges():
+    """The extent scan restricted to each row's lane range (efd_modesum_lane_ranges after
+    GenerateEMRIWaveform.spectrum_batch) gives bitwise the full scan's scale, support and
+    transformed rows; the lane range covers every nonzero bin (and its mirror)."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.fdutils import HannConvolution
+    s = pe.setup(nwalkers=16, ntemps=1, window_flag=True, **TEST_SH)
+    lib = _lib.load()
+    params = s.transform.both_transforms(s.half_steps()[0][:3])
+    n = s.info["N_f"]
+    S = torch.empty((3, n), dtype=torch.complex128, device="cuda")
+    lanes = torch.empty((3, 2), dtype=torch.int32, device="cuda")
+    s.few.spectrum_batch(params, S, lanes=lanes, **s.kwargs)
+    torch.cuda.synchronize()
+    hcv = HannConvolution(n, S.device)
+    Y1, info1, m1 = hcv.transform(S, lib, lanes)
+    Y1, info1 = Y1.clone(), info1.clone()
+    Y0, info0, m0 = hcv.transform(S, lib)
+    assert m1 == m0 and torch.equal(info1, info0) and torch.equal(Y1, Y0)
+    ln = lanes.cpu().numpy()
+    nz = (S != 0).cpu().numpy()
+    for r in range(3):
+        lo, hi = int(ln[r, 0]), int(ln[r, 1])
+        k = np.nonzero(nz[r])[0]
+        assert len(k) and k.min() >= min(lo, n - hi) and k.max() < max(hi, n - lo)
