@@ -1,6 +1,7 @@
 """Interleaved end-to-end A/B of library variants through bench.py (GPU box).
 
     python tools/ab_bench.py ROUNDS NAME[@ARG,...] [NAME[@ARG,...] ...]
+    (an ARG of the form env:NAME=VALUE sets the child's environment instead)
 
 Each round runs `bench.py --no-cpu-baseline` once per variant, in a rotated order, each in its
 own child process with EFD_LIB pointing at the variant (names as in tools/exp_variants.py:
@@ -27,6 +28,11 @@ def run_one(name, extra):
     lib, _, own = name.partition("@")
     env = dict(os.environ, EFD_LIB=lib_path(lib))
     own = [x for x in own.split(",") if x]
+    # "env:NAME=VALUE" items set the child's environment instead of bench.py arguments
+    for x in [x for x in own if x.startswith("env:")]:
+        k, _, v = x[4:].partition("=")
+        env[k] = v
+    own = [x for x in own if not x.startswith("env:")]
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline",
                         *extra, *own], capture_output=True, text=True, timeout=300, env=env,
                        cwd=ROOT)
