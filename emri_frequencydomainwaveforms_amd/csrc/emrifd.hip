@@ -709,17 +709,16 @@ __global__ __launch_bounds__(256) void k_group_b(const PrepBatch B) {
 //   Bp = sum_l y0_l A_l(t_i),  Bm = sum_l y1_l A_l(t_i),  y0 = -scale Y+,  y1 = conj(-scale Y-)
 // (y1 = 0 for m = 0: no partner), summed in ascending h. gamp is [nt][4K]: (Bp re, Bp im,
 // Bm re, Bm im) of group g at 4g. S = -h_nb(-f) * scale: the minus sign and scale live here.
-__device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
-                                                   const double* __restrict__ ylm_p,
-                                                   const double* __restrict__ ylm_m, double sc_re,
-                                                   double sc_im, const int32_t* __restrict__ gm,
-                                                   const int32_t* __restrict__ gstart,
-                                                   const int32_t* __restrict__ gmem, int nt, int K,
-                                                   const Header* __restrict__ hdr,
-                                                   double* __restrict__ gamp) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = blockIdx.y;
-    if (g >= hdr->groups || i >= nt) return;
+// group_amp_at is the one evaluation: k_group_amp_b stores it for k_prep_b's Thomas roles, and
+// k_prep_pcr_b's amplitude waves call it for their own component (no gamp pass, one launch
+// fewer in the chain; the same operations in the same order, so the same values).
+__device__ __forceinline__ double4 group_amp_at(const double* __restrict__ amp,
+                                                const double* __restrict__ ylm_p,
+                                                const double* __restrict__ ylm_m, double sc_re,
+                                                double sc_im, const int32_t* __restrict__ gm,
+                                                const int32_t* __restrict__ gstart,
+                                                const int32_t* __restrict__ gmem, int K, int i,
+                                                int g) {
     const bool partner = gm[g] != 0;
     double bpr = 0.0, bpi = 0.0, bmr = 0.0, bmi = 0.0;
     for (int p = gstart[g], pe = gstart[g + 1]; p < pe; ++p) {
@@ -736,8 +735,22 @@ __device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
             bmi += ar * y1i + ai * y1r;
         }
     }
+    return make_double4(bpr, bpi, bmr, bmi);
+}
+__device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
+                                                   const double* __restrict__ ylm_p,
+                                                   const double* __restrict__ ylm_m, double sc_re,
+                                                   double sc_im, const int32_t* __restrict__ gm,
+                                                   const int32_t* __restrict__ gstart,
+                                                   const int32_t* __restrict__ gmem, int nt, int K,
+                                                   const Header* __restrict__ hdr,
+                                                   double* __restrict__ gamp) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (g >= hdr->groups || i >= nt) return;
+    const double4 v = group_amp_at(amp, ylm_p, ylm_m, sc_re, sc_im, gm, gstart, gmem, K, i, g);
     double* o = gamp + (size_t)i * 4 * K + 4 * g;
-    o[0] = bpr; o[1] = bpi; o[2] = bmr; o[3] = bmi;
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
 }
 __global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ amp,
                                                    const double* __restrict__ ylm_p,
@@ -751,6 +764,7 @@ __global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ am
 }
 __global__ __launch_bounds__(256) void k_group_amp_b(const PrepBatch B) {
     PREP_WALKER(B);
+    if (D.pcr & 2) return;   // k_prep_pcr_b evaluates this waveform's group amplitudes itself
     group_amp_body(D.amp, D.ylm_p, D.ylm_m, D.sc_re, D.sc_im, ws_at<int32_t>(W, L.gm),
                    ws_at<int32_t>(W, L.gstart), ws_at<int32_t>(W, L.gmem), D.nt, D.K,
                    ws_at<Header>(W, L.header), ws_at<double>(W, L.gamp));
@@ -1084,10 +1098,15 @@ __global__ __launch_bounds__(64) void k_prep_b(const PrepBatch B) {
 // grid stops at 4 + K). Blocks past this waveform's G leave at once.
 // The same coefficients as k_prep's (scipy's construction, to rounding); for 4 <= N_t <=
 // PCR_NMAX (the host takes k_prep_b otherwise). Dynamic LDS: 9 N_t doubles.
+struct GroupAmpSrc {   // group_amp_at's operands
+    const double *amp, *ylm_p, *ylm_m;
+    double sc_re, sc_im;
+    const int32_t *gstart, *gmem;
+};
 __device__ __forceinline__ void prep_pcr_body(
     const double* __restrict__ t, const double* __restrict__ phi_phi,
     const double* __restrict__ phi_r, const double* __restrict__ f_phi,
-    const double* __restrict__ f_r, const double* __restrict__ gamp,
+    const double* __restrict__ f_r, const GroupAmpSrc ga,
     const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int nt, int K,
     double* __restrict__ coefT, double* __restrict__ kslope, double* __restrict__ coefA,
     int32_t* __restrict__ runs, Item* __restrict__ items, double* __restrict__ invcp,
@@ -1136,7 +1155,13 @@ __device__ __forceinline__ void prep_pcr_body(
         const int q = b - 4 - K;
         if (q >= 4 * G) return;
         const size_t ninterp = (size_t)4 * K;
-        auto Y = [&](int i) { return gamp[(size_t)i * ninterp + q]; };
+        // component q & 3 of group q >> 2 at knot i (group_amp_at; no gamp pass)
+        auto Y = [&](int i) {
+            const double4 v = group_amp_at(ga.amp, ga.ylm_p, ga.ylm_m, ga.sc_re, ga.sc_im, gm,
+                                           ga.gstart, ga.gmem, K, i, q >> 2);
+            const int c = q & 3;
+            return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+        };
         auto OUT = [&](int i, int c, double v) { coefA[((size_t)i * 4 + c) * ninterp + q] = v; };
         pcr_not_a_knot(nt, X, Y, OUT, lds);
         return;
@@ -1212,8 +1237,10 @@ __device__ __forceinline__ void prep_pcr_body(
 __global__ __launch_bounds__(64) void k_prep_pcr_b(const PrepBatch B) {
     PREP_WALKER(B);
     if (!(D.pcr & 1) || (int)blockIdx.x >= 4 + ((D.pcr & 2) ? 5 : 1) * D.K) return;
-    prep_pcr_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ws_at<double>(W, L.gamp),
-                  ws_at<int32_t>(W, L.gm), ws_at<int32_t>(W, L.gn), D.nt, D.K,
+    const GroupAmpSrc ga{D.amp, D.ylm_p, D.ylm_m, D.sc_re, D.sc_im,
+                         ws_at<int32_t>(W, L.gstart), ws_at<int32_t>(W, L.gmem)};
+    prep_pcr_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ga, ws_at<int32_t>(W, L.gm),
+                  ws_at<int32_t>(W, L.gn), D.nt, D.K,
                   ws_at<double>(W, L.coefT), ws_at<double>(W, L.kslope), ws_at<double>(W, L.coefA),
                   ws_at<int32_t>(W, L.runs), ws_at<Item>(W, L.items), ws_at<double>(W, L.invcp),
                   ws_at<double>(W, L.invdp), ws_at<Header>(W, L.header));
@@ -4225,13 +4252,16 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
     (void)nimax;
     hipStream_t st = (hipStream_t)stream;
     const unsigned nz = (unsigned)count;
-    // K0: (m, n) groups and their amplitudes at the knots
+    // K0: (m, n) groups and, for the Thomas kernel's amplitude role, their amplitudes at the
+    // knots (the PCR amplitude waves evaluate their own)
     {
         hipLaunchKernelGGL(k_group_b, dim3(1, 1, nz), dim3(256), 0, st, B);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax + 255) / 256, ntmax, nz), dim3(256), 0, st,
-                           B);
-        HIP_TRY(hipGetLastError());
+        if (any_thomas) {
+            hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax + 255) / 256, ntmax, nz), dim3(256), 0,
+                               st, B);
+            HIP_TRY(hipGetLastError());
+        }
     }
     // K1-K3: trajectory splines, group amplitude splines, inverse splines (one fused launch;
     // grids sized for G = K, blocks past the device-side G return at once)

@@ -26,6 +26,8 @@ Time-domain templates (dt only) are not part of this path: get_ll raises NotImpl
 """
 
 import ctypes
+import os
+import sys
 
 import numpy as np
 
@@ -250,6 +252,11 @@ class Likelihood:
     # config 4's 8 walkers are one group either way (groups of 4 or 3: -5 to -10%)
     FUSED_GROUP = 16
     FUSED_DEPTH = 2
+    # each group's sum on the group's own stream, right behind its preparation: no
+    # cross-stream wait between the two (~12 us of idle device per group on config 4's chain,
+    # tools/chain_timeline.py), and the groups' sums need no common stream (each writes its own
+    # slice of out); the streams join once, before the copy out. False: round 3's sum stream.
+    FUSED_SUM_OWN_STREAM = os.environ.get("EFD_SUM_STREAM", "0") != "1"
 
     def _get_ll_fused(self, tm, params, args, kwargs, out):
         """The pipelined path with the likelihood fused into the mode sum: per group of
@@ -300,6 +307,8 @@ class Likelihood:
         pin = F.get("pin")
         if pin is None or pin.numel() < n:
             pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
+        own = self.FUSED_SUM_OWN_STREAM
+        used = []
         try:
             batch = getattr(tm, "submit_batch", None)
             for g0 in range(0, n, G):
@@ -310,6 +319,13 @@ class Likelihood:
                         tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
                                   **kwargs)
                 gi, jobs = B.flush()
+                used.append(gi)
+                if own:
+                    sst = B.groups[gi]["stream"]
+                    tc = self._tile_constants(jobs[0][1], sst, F)
+                    B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)],
+                                  sst.cuda_stream, tile_const=tc)
+                    continue   # (the group's next flush is behind this sum on its stream)
                 _lib.check(lib.efd_stream_order(F["gst"][gi], F["sum1"], 1), "efd_stream_order",
                            lib)
                 tc = self._tile_constants(jobs[0][1], s_sum)
@@ -318,13 +334,29 @@ class Likelihood:
                 ev = F["ev"][gi]   # (flush waited on its previous record before this one)
                 ev.record(s_sum)
                 B.release(gi, ev)
-            _lib.check(lib.efd_download(pin.data_ptr(), out.data_ptr(), 8 * n, s_sum.cuda_stream),
+            if own:
+                # the other groups' streams join the last one, which copies out
+                last = used[-1]
+                vp = ctypes.c_void_p
+                for gj in sorted(set(used) - {last}):
+                    _lib.check(lib.efd_stream_order(F["gst"][gj], (vp * 1)(F["gst"][last]), 1),
+                               "efd_stream_order", lib)
+                dl = F["gst"][last]
+            else:
+                dl = s_sum.cuda_stream
+            _lib.check(lib.efd_download(pin.data_ptr(), out.data_ptr(), 8 * n, dl),
                        "efd_download", lib)
         finally:
             B._pending = []
             # `out` belongs to the current stream: nothing may still write it when it is
             # returned, or freed after an exception
-            s_sum.synchronize()
+            if not own:
+                s_sum.synchronize()
+            elif used:
+                B.groups[used[-1]]["stream"].synchronize()
+                if len(set(used)) > 1 and sys.exc_info()[0] is not None:
+                    for gj in set(used):
+                        B.groups[gj]["stream"].synchronize()
         host = pin[:n].numpy().copy()
         if np.isnan(host).any():
             B.wait()   # device-side errors of the groups' workspaces (sticky across reuse)
@@ -334,9 +366,11 @@ class Likelihood:
     # (efd_loglike_tile_constants; bitwise the same logL)
     fused_tile_constants = True
 
-    def _tile_constants(self, job, stream):
+    def _tile_constants(self, job, stream, fused=None):
         """The fused sum's per-tile constants for (d, w_templ) on this grid, made once on
-        `stream` (ordered after the data's creation: the caller's stream waits on current)."""
+        `stream` (ordered after the data's creation: the caller's stream waits on current).
+        With `fused` (the sums on the groups' own streams) every stream of fused["order"] is
+        then ordered after `stream`, so any group's later sum may read them."""
         if not self.fused_tile_constants:
             return None
         from .summation import loglike_tile_constants
@@ -346,6 +380,10 @@ class Likelihood:
         if tc is None or tc[0] != key:
             tc = self._tile_const = (key, loglike_tile_constants(
                 self._d, self._w_templ, nf, k0, stream.cuda_stream))
+            if fused is not None:
+                lib = fused["prep"].lib
+                _lib.check(lib.efd_stream_order(stream.cuda_stream, fused["order"],
+                                                len(fused["order"])), "efd_stream_order", lib)
         return tc[1]
 
     def _fused_grid_ok(self, tm, kwargs):

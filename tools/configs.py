@@ -278,10 +278,11 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
             "fused_likelihood": fused and not windowed,
             "device_note": "Likelihood.get_ll over the half-step batch with the host upstream "
                            "memoised: " + (
-                               "per walker the FD spectrum S (mode sum), the Hann window "
-                               "convolution as one rocFFT transform pair on S "
-                               "(fdutils.windowed_spectrum), h+/hx over f >= 0 and efd_loglike"
-                               if windowed else 
+                               "per group of 8 walkers the FD spectra S in one batched mode "
+                               "sum, the Hann window's correction as one four-step transform "
+                               "pipeline over the rows' supports (efd_hann_convolve) and the "
+                               "windowed logL reduced in place (efd_hann_loglike)"
+                               if windowed else
                                "per balanced group of up to 16 walkers one packed input "
                                "upload (efd_stage_batch), one efd_modesum_prepare_batch and "
                                "one mode-sum launch with the likelihood fused in (no "
