@@ -159,6 +159,7 @@ struct Header {
 };
 static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
+
 struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
         seginfo, nseg, slotlh, slotinfo, slotcnt, slottiles, segbase, stb0, stb1, gm, gn, gstart,
@@ -1500,13 +1501,44 @@ __device__ void build_item(
     const double gsc = span > 0.0 ? (double)(nf - 1) / span : 0.0;
     auto guess = [&](double v) { return (int64_t)floor((v - f0) * gsc); };
     // s = 0: g = -f  ->  f in (-xhi, -xlo]  (or (-xhi, -xlo) if strict)
-    int64_t lo0 = grid_bound<true>(freq, nf, -xhi, guess(-xhi));
-    int64_t hi0 = strict_lo ? grid_bound<false>(freq, nf, -xlo, guess(-xlo))
-                            : grid_bound<true>(freq, nf, -xlo, guess(-xlo));
     // s = 1: g = +f  ->  f in [xlo, xhi)  (or (xlo, xhi))
-    int64_t lo1 = strict_lo ? grid_bound<true>(freq, nf, xlo, guess(xlo))
-                            : grid_bound<false>(freq, nf, xlo, guess(xlo));
-    int64_t hi1 = grid_bound<false>(freq, nf, xhi, guess(xhi));
+    // The four bounds' grid values around their guesses are loaded together (one round trip
+    // instead of the ~2 dependent ones of each grid_bound in turn); a bound the three values do
+    // not settle (a non-uniform grid) takes grid_bound. Same indices either way.
+    const double bv[4] = {-xhi, -xlo, xlo, xhi};
+    const bool bu[4] = {true, !strict_lo, strict_lo, false};   // UPPER: first f > v, else f >= v
+    int64_t bg[4];
+    double b3[4][3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t g = guess(bv[q]);
+        bg[q] = g < 0 ? 0 : (g > nf ? nf : g);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t g = bg[q];
+        b3[q][0] = freq[g >= 1 ? g - 1 : 0];
+        b3[q][1] = freq[g < nf ? g : nf - 1];
+        b3[q][2] = freq[g + 1 < nf ? g + 1 : nf - 1];
+    }
+    int64_t bk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double v = bv[q];
+        const int64_t g = bg[q];
+        auto pred = [&](double x) { return bu[q] ? (x > v) : (x >= v); };
+        int64_t k = -1;
+        if (!(g >= 1 && pred(b3[q][0]))) {           // f[g - 1] fails: the answer is >= g
+            if (g == nf) k = nf;
+            else if (pred(b3[q][1])) k = g;
+            else if (g + 1 == nf) k = nf;
+            else if (pred(b3[q][2])) k = g + 1;
+        }
+        if (k < 0)
+            k = bu[q] ? grid_bound<true>(freq, nf, v, g) : grid_bound<false>(freq, nf, v, g);
+        bk[q] = k;
+    }
+    int64_t lo0 = bk[0], hi0 = bk[1], lo1 = bk[2], hi1 = bk[3];
     const int64_t lim0 = paired ? nl : nf;
     const int64_t lim1 = paired ? nl1 : (partner ? nf : 0);
     auto clampr = [](int64_t& lo, int64_t& hi, int64_t lim) {
@@ -1534,6 +1566,50 @@ __device__ void build_item(
 // is deterministic.
 // seglh = (lo, hi) lane range; seginfo = (first record, count, dir, s).
 // ----------------------------------------------------------------------------------------
+// The segment of slot i = (group h, run r, sub-branch sb): its lane range lh and (first record,
+// count, dir, s) info, or info.y == 0 when the slot holds none. G = the call's group count.
+__device__ __forceinline__ void slot_segment(int i, const int32_t* __restrict__ runs,
+                                             const int4* __restrict__ ranges, int nt, int G,
+                                             int lim0, int lim1, int2& lh, int4& info) {
+    const int h = i / (2 * MAXRUNS), r = (i >> 1) % MAXRUNS, sb = i & 1;
+    const int ni = nt - 1;
+    lh = make_int2(0, 0);
+    info = make_int4(0, 0, 0, 0);
+    const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS + 4 * r;
+    if (h < G && rr[2] != 0) {
+        const int ja = rr[0], jb = rr[1], n = jb - ja;
+        const int dir = (sb == 0) ? -rr[2] : rr[2];   // s = 0 walks g downward in lane order
+        const int lim = sb ? lim1 : lim0;
+        const int4* rg = ranges + (size_t)h * ni;
+        // Records whose branch lies outside the lane range are empty and clamped to its
+        // ends (lane 0 or lim); they sit at the two ends of the segment in lane order and
+        // are trimmed, so the tiles holding lane 0 and lim do not collect all of them.
+        int lo = 0, hi = n;                            // first p with khi > 0
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int4 v = rg[dir > 0 ? ja + mid : jb - 1 - mid];
+            if ((sb ? v.w : v.y) > 0) hi = mid; else lo = mid + 1;
+        }
+        const int pa = lo;
+        hi = n;                                        // first p with klo >= lim
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int4 v = rg[dir > 0 ? ja + mid : jb - 1 - mid];
+            if ((sb ? v.z : v.x) >= lim) hi = mid; else lo = mid + 1;
+        }
+        const int pb = lo;
+        if (pb > pa) {
+            const int4 rf = rg[dir > 0 ? ja + pa : jb - 1 - pa];
+            const int4 rl = rg[dir > 0 ? ja + pb - 1 : jb - pb];
+            const int klo = sb ? rf.z : rf.x, khi = sb ? rl.w : rl.y;
+            if (khi > klo) {
+                lh = make_int2(klo, khi);
+                const int jfirst = dir > 0 ? ja + pa : jb - pb;   // lowest record index kept
+                info = make_int4(h * ni + jfirst, pb - pa, dir, sb);
+            }
+        }
+    }
+}
 __device__ __forceinline__ void segment_slots_body(const int32_t* __restrict__ runs,
                                                        const int4* __restrict__ ranges, int nt,
                                                        int K, int lim0, int lim1,
@@ -1548,44 +1624,9 @@ __device__ __forceinline__ void segment_slots_body(const int32_t* __restrict__ r
     bool valid = false;
     if (i < K * MAXRUNS * 2) {
         const int G = hdr->groups;
-        const int h = i / (2 * MAXRUNS), r = (i >> 1) % MAXRUNS, sb = i & 1;
-        const int ni = nt - 1;
-        int2 lh = make_int2(0, 0);
-        int4 info = make_int4(0, 0, 0, 0);
-        const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS + 4 * r;
-        if (h < G && rr[2] != 0) {
-            const int ja = rr[0], jb = rr[1], n = jb - ja;
-            const int dir = (sb == 0) ? -rr[2] : rr[2];   // s = 0 walks g downward in lane order
-            const int lim = sb ? lim1 : lim0;
-            const int4* rg = ranges + (size_t)h * ni;
-            // Records whose branch lies outside the lane range are empty and clamped to its
-            // ends (lane 0 or lim); they sit at the two ends of the segment in lane order and
-            // are trimmed, so the tiles holding lane 0 and lim do not collect all of them.
-            int lo = 0, hi = n;                            // first p with khi > 0
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                const int4 v = rg[dir > 0 ? ja + mid : jb - 1 - mid];
-                if ((sb ? v.w : v.y) > 0) hi = mid; else lo = mid + 1;
-            }
-            const int pa = lo;
-            hi = n;                                        // first p with klo >= lim
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                const int4 v = rg[dir > 0 ? ja + mid : jb - 1 - mid];
-                if ((sb ? v.z : v.x) >= lim) hi = mid; else lo = mid + 1;
-            }
-            const int pb = lo;
-            if (pb > pa) {
-                const int4 rf = rg[dir > 0 ? ja + pa : jb - 1 - pa];
-                const int4 rl = rg[dir > 0 ? ja + pb - 1 : jb - pb];
-                const int klo = sb ? rf.z : rf.x, khi = sb ? rl.w : rl.y;
-                if (khi > klo) {
-                    lh = make_int2(klo, khi);
-                    const int jfirst = dir > 0 ? ja + pa : jb - pb;   // lowest record index kept
-                    info = make_int4(h * ni + jfirst, pb - pa, dir, sb);
-                }
-            }
-        }
+        int2 lh;
+        int4 info;
+        slot_segment(i, runs, ranges, nt, G, lim0, lim1, lh, info);
         slot_lh[i] = lh;
         slot_info[i] = info;
         valid = info.y > 0;
@@ -1710,6 +1751,28 @@ __global__ __launch_bounds__(256) void k_segment_compact(const PrepBatch B) {
 // klo >= (t+1)*TL). Lane ranges are monotone in p, so each tile gets exactly one of each: the
 // same answers as k_modesum's bisection, from two loads instead of ~2 log2(n) dependent ones.
 __device__ __forceinline__ int div_floor_nn(int64_t a) { return (int)(a / TILE_LANES); }   // a >= 0
+// record p (0 <= p <= n: n is the end marker) of the segment (lh, info) with pair base sbase
+__device__ __forceinline__ void seg_tiles_record(const int4* __restrict__ ranges, int2 lh,
+                                                 int4 info, int32_t sbase, int p,
+                                                 int32_t* __restrict__ stb0,
+                                                 int32_t* __restrict__ stb1) {
+    const int base = info.x, n = info.y, dir = info.z, sb = info.w;
+    const int t0 = lh.x / TILE_LANES, t1 = (lh.y - 1) / TILE_LANES;
+    auto rng = [&](int q) {   // (klo, khi) of record q in lane order
+        const int4 rg = ranges[base + (dir > 0 ? q : n - 1 - q)];
+        return sb ? make_int2(rg.z, rg.w) : make_int2(rg.x, rg.y);
+    };
+    const int2 cur = p < n ? rng(p) : make_int2(0, 0);
+    const int2 prv = p > 0 ? rng(p - 1) : make_int2(0, 0);
+    // p0: khi_{p-1} <= t TL < khi_p
+    int a = p > 0 ? (int)((prv.y + TILE_LANES - 1) / TILE_LANES) : t0;
+    int b = p < n ? (cur.y > 0 ? div_floor_nn(cur.y - 1) : -1) : t1;
+    for (int t = max(a, t0); t <= min(b, t1); ++t) stb0[sbase + t] = p;
+    // p1: klo_{p-1} < (t+1) TL <= klo_p
+    a = p > 0 ? div_floor_nn(prv.x) : t0;
+    b = p < n ? div_floor_nn(cur.x) - 1 : t1;
+    for (int t = max(a, t0); t <= min(b, t1); ++t) stb1[sbase + t] = p;
+}
 __device__ __forceinline__ void seg_tiles_body(const int4* __restrict__ ranges,
                                                    const int2* __restrict__ seglh,
                                                    const int4* __restrict__ seginfo,
@@ -1723,24 +1786,8 @@ __device__ __forceinline__ void seg_tiles_body(const int4* __restrict__ ranges,
         if (sbase == SEG_NO_STB) continue;
         const int2 lh = seglh[sg];
         const int4 info = seginfo[sg];
-        const int base = info.x, n = info.y, dir = info.z, sb = info.w;
-        const int t0 = lh.x / TILE_LANES, t1 = (lh.y - 1) / TILE_LANES;
-        auto rng = [&](int p) {   // (klo, khi) of record p in lane order
-            const int4 rg = ranges[base + (dir > 0 ? p : n - 1 - p)];
-            return sb ? make_int2(rg.z, rg.w) : make_int2(rg.x, rg.y);
-        };
-        for (int p = threadIdx.x; p <= n; p += blockDim.x) {
-            const int2 cur = p < n ? rng(p) : make_int2(0, 0);
-            const int2 prv = p > 0 ? rng(p - 1) : make_int2(0, 0);
-            // p0: khi_{p-1} <= t TL < khi_p
-            int a = p > 0 ? (int)((prv.y + TILE_LANES - 1) / TILE_LANES) : t0;
-            int b = p < n ? (cur.y > 0 ? div_floor_nn(cur.y - 1) : -1) : t1;
-            for (int t = max(a, t0); t <= min(b, t1); ++t) stb0[sbase + t] = p;
-            // p1: klo_{p-1} < (t+1) TL <= klo_p
-            a = p > 0 ? div_floor_nn(prv.x) : t0;
-            b = p < n ? div_floor_nn(cur.x) - 1 : t1;
-            for (int t = max(a, t0); t <= min(b, t1); ++t) stb1[sbase + t] = p;
-        }
+        for (int p = threadIdx.x; p <= info.y; p += blockDim.x)
+            seg_tiles_record(ranges, lh, info, sbase, p, stb0, stb1);
     }
 }
 __global__ __launch_bounds__(256) void k_seg_tiles(const PrepBatch B) {
@@ -1748,6 +1795,100 @@ __global__ __launch_bounds__(256) void k_seg_tiles(const PrepBatch B) {
     seg_tiles_body(ws_at<int4>(W, L.ranges), ws_at<int2>(W, L.seglh), ws_at<int4>(W, L.seginfo),
                    ws_at<int32_t>(W, L.segbase), ws_at<int32_t>(W, L.nseg),
                    ws_at<int32_t>(W, L.stb0), ws_at<int32_t>(W, L.stb1));
+}
+
+// K5 in one workgroup per waveform when its 2 MAXRUNS K slots fit one (K <= 64: the walker
+// batches' sparse spectra): the slots' segments, their compaction in slot order (block scans in
+// place of k_segment_compact's per-block offsets), the lane union, then the tile pairs of every
+// (segment, record) (k_seg_tiles' work flattened over the workgroup: a record's segment found by
+// bisection of the segments' record offsets in LDS). The same tables as the three kernels, in
+// one launch instead of three.
+constexpr int SEG1_NT = 1024;
+constexpr int SEG1_MAX_K = SEG1_NT / (2 * MAXRUNS);
+__device__ __forceinline__ int seg1_excl_scan(int v, int* wsum, int& total) {
+    constexpr int NW = SEG1_NT / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+    for (int w = 0; w < NW; ++w) {
+        const int x = wsum[w];
+        if (w < wave) before += x;
+        total += x;
+    }
+    __syncthreads();   // wsum free for the next scan
+    return before + incl - v;
+}
+__global__ __launch_bounds__(SEG1_NT) void k_segments_one(const PrepBatch B) {
+    PREP_WALKER(B);
+    constexpr int NW = SEG1_NT / 64;
+    __shared__ int wsum[NW];
+    __shared__ int2 wr[NW];
+    __shared__ int2 s_lh[SEG1_NT];
+    __shared__ int4 s_info[SEG1_NT];
+    __shared__ int32_t s_base[SEG1_NT];
+    __shared__ int32_t s_roff[SEG1_NT];
+    Header* hdr = ws_at<Header>(W, L.header);
+    const int4* ranges = ws_at<int4>(W, L.ranges);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nslot = 2 * MAXRUNS * D.K;   // <= SEG1_NT (host: every waveform has K <= SEG1_MAX_K)
+    int2 lh = make_int2(0, 0);
+    int4 info = make_int4(0, 0, 0, 0);
+    if (tid < nslot)
+        slot_segment(tid, ws_at<int32_t>(W, L.runs), ranges, D.nt, hdr->groups,
+                     (int)(B.paired ? B.nl : B.nf), (int)(B.paired ? B.nl1 : B.nf), lh, info);
+    const bool valid = info.y > 0;
+    const int ntl = valid ? (lh.y - 1) / TILE_LANES - lh.x / TILE_LANES + 1 : 0;
+    int nseg, ntot;
+    const int pos = seg1_excl_scan(valid ? 1 : 0, wsum, nseg);
+    const int toff = seg1_excl_scan(ntl, wsum, ntot);
+    int32_t sbase = SEG_NO_STB;
+    if (valid) {
+        sbase = ((int64_t)toff + ntl <= L.stbcap) ? (int32_t)(toff - lh.x / TILE_LANES)
+                                                  : SEG_NO_STB;
+        ws_at<int2>(W, L.seglh)[pos] = lh;
+        ws_at<int4>(W, L.seginfo)[pos] = info;
+        ws_at<int32_t>(W, L.segbase)[pos] = sbase;
+        s_lh[pos] = lh;
+        s_info[pos] = info;
+        s_base[pos] = sbase;
+    }
+    int nrec_all;
+    const int nrec = (valid && sbase != SEG_NO_STB) ? info.y + 1 : 0;
+    const int roff = seg1_excl_scan(nrec, wsum, nrec_all);
+    if (valid) s_roff[pos] = roff;
+    // the lane union (k_segment_compact's, one workgroup: no atomics)
+    int lo = valid ? lh.x : INT32_MAX, hi = valid ? lh.y : INT32_MIN;
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    if (lane == 0) wr[wave] = make_int2(lo, hi);
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < NW; ++w) { lo = min(lo, wr[w].x); hi = max(hi, wr[w].y); }
+        if (lo < hi) {
+            hdr->lane_lo = lo;
+            hdr->lane_hi = hi;
+        }
+        *ws_at<int32_t>(W, L.nseg) = nseg;
+    }
+    int32_t* stb0 = ws_at<int32_t>(W, L.stb0);
+    int32_t* stb1 = ws_at<int32_t>(W, L.stb1);
+    for (int f = tid; f < nrec_all; f += SEG1_NT) {
+        int a = 0, b = nseg - 1;   // the last segment q with s_roff[q] <= f
+        while (a < b) {
+            const int mid = (a + b + 1) >> 1;
+            if (s_roff[mid] <= f) a = mid; else b = mid - 1;
+        }
+        seg_tiles_record(ranges, s_lh[a], s_info[a], s_base[a], f - s_roff[a], stb0, stb1);
+    }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2913,10 +3054,51 @@ struct SumBatch {
     int32_t n;
 };
 static_assert(sizeof(SumBatch) <= 3584, "batch descriptors must fit the kernel arguments");
+// One waveform's logL from its tile partials p (with llconst: tiles outside the lane union take
+// their constants): each thread's tiles i, i + 256, ... added in that order, then a tree; out =
+// -1/2 * 4 * sum, or NaN when the workspace holds a device-side error flag (the flags stay set:
+// efd_modesum_status_batch reports and clears them), so a caller that finds no NaN in the batch
+// needs no status synchronisation. 256 threads.
+__device__ __forceinline__ void ll_final_reduce(const double* __restrict__ p,
+                                                const Header* __restrict__ h,
+                                                const double* __restrict__ llconst,
+                                                int64_t ntiles, double* __restrict__ out) {
+    __shared__ double red[256];
+    int64_t t0 = 0, t1 = ntiles - 1;
+    if (llconst != nullptr) {
+        const int32_t lo = h->lane_lo, hi = h->lane_hi;
+        t0 = lo < hi ? lo / TILE_LANES : ntiles;
+        t1 = lo < hi ? (int64_t)(hi - 1) / TILE_LANES : -1;
+    }
+    auto val = [&](int64_t i) { return (i < t0 || i > t1) ? llconst[i] : p[i]; };
+    // four loads in flight at a time
+    double acc = 0.0;
+    int64_t i = threadIdx.x;
+    for (; i + 3 * 256 < ntiles; i += 4 * 256) {
+        const double v0 = val(i), v1 = val(i + 256), v2 = val(i + 512), v3 = val(i + 768);
+        acc += v0;
+        acc += v1;
+        acc += v2;
+        acc += v3;
+    }
+    for (; i < ntiles; i += 256) acc += val(i);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const bool bad = h->runs_overflow | h->bad_mn | h->bad_tile;
+        *out = bad ? __longlong_as_double(0x7ff8000000000000LL) : -0.5 * 4.0 * red[0];
+    }
+}
 // SPARSE (the fused likelihood with tile constants, no written outputs): only the tiles inside the
 // union of the waveform's segment lane ranges ([lane_lo, lane_hi) in its header, k_segment_compact)
 // are visited, by nper workgroups per waveform striding over them; k_ll_final takes the constant
-// of every tile outside. A sparse spectrum (config 4: 15 harmonics cover 576 of 6,164 tiles) then
+// of every tile outside. (Folding k_ll_final into the launch's last workgroup per waveform, with
+// agent-scope partial stores and a completion count, made config 4's sum 6 us longer than the two
+// kernels: the reduction then runs in the launch's tail.) A sparse spectrum (config 4: 15 harmonics cover 576 of 6,164 tiles) then
 // launches a few hundred workgroups per walker instead of one per tile.
 template <bool PAIRED, int CAUSTIC, int BPL, bool SPARSE>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
@@ -2941,17 +3123,18 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
         pos = (int64_t)(r / (unsigned)n) * 8 + (g & 7u);
     }
     const BatchDesc& d = batch.d[w];
-    if (SPARSE) {
+    if constexpr (SPARSE) {
         const int32_t lo = d.hdr->lane_lo, hi = d.hdr->lane_hi;
-        if (lo >= hi) return;
-        const int64_t t1 = min((int64_t)(hi - 1) / TILE_LANES, ntiles - 1);
-        for (int64_t tile = lo / TILE_LANES + pos; tile <= t1; tile += nper) {
-            modesum_tile<PAIRED, CAUSTIC, BPL>(
-                d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt,
-                d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm,
-                d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld,
-                llw, d.llpart, llconst, tile, true);
-            __syncthreads();   // the next tile's LDS writes after every wave's last reads
+        if (lo < hi) {
+            const int64_t t1 = min((int64_t)(hi - 1) / TILE_LANES, ntiles - 1);
+            for (int64_t tile = lo / TILE_LANES + pos; tile <= t1; tile += nper) {
+                modesum_tile<PAIRED, CAUSTIC, BPL>(
+                    d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles,
+                    d.nt, d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt,
+                    d.tperm, d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc,
+                    d.k0, lld, llw, d.llpart, llconst, tile, true);
+                __syncthreads();   // the next tile's LDS writes after every wave's last reads
+            }
         }
         return;
     }
@@ -3061,42 +3244,8 @@ __global__ __launch_bounds__(64) void k_status_gather(const StatusBatch sb, int3
 }
 
 __global__ __launch_bounds__(256) void k_ll_final(const LlBatch lb) {
-    __shared__ double red[256];
-    const double* p = lb.part[blockIdx.x];
-    const Header* h = lb.hdr[blockIdx.x];
-    // tiles [t0, t1] hold their own partials; with llconst (k_modesum_batch's sparse form) the
-    // others are empty and take their constants
-    int64_t t0 = 0, t1 = lb.ntiles - 1;
-    if (lb.llconst != nullptr) {
-        const int32_t lo = h->lane_lo, hi = h->lane_hi;
-        t0 = lo < hi ? lo / TILE_LANES : lb.ntiles;
-        t1 = lo < hi ? (int64_t)(hi - 1) / TILE_LANES : -1;
-    }
-    auto val = [&](int64_t i) { return (i < t0 || i > t1) ? lb.llconst[i] : p[i]; };
-    // each thread's tiles i, i + 256, ... added in that order; four loads in flight at a time
-    double acc = 0.0;
-    int64_t i = threadIdx.x;
-    for (; i + 3 * 256 < lb.ntiles; i += 4 * 256) {
-        const double v0 = val(i), v1 = val(i + 256), v2 = val(i + 512), v3 = val(i + 768);
-        acc += v0;
-        acc += v1;
-        acc += v2;
-        acc += v3;
-    }
-    for (; i < lb.ntiles; i += 256) acc += val(i);
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        // a walker whose workspace holds a device-side error flag gets a NaN log-likelihood
-        // (the flags stay set: efd_modesum_status_batch reports and clears them), so a caller
-        // that finds no NaN in the batch needs no status synchronisation
-        const bool bad = h->runs_overflow | h->bad_mn | h->bad_tile;
-        lb.out[blockIdx.x] = bad ? __longlong_as_double(0x7ff8000000000000LL) : -0.5 * 4.0 * red[0];
-    }
+    ll_final_reduce(lb.part[blockIdx.x], lb.hdr[blockIdx.x], lb.llconst, lb.ntiles,
+                           lb.out + blockIdx.x);
 }
 
 // K6: the tiles' record lists, built in the preparation phase (k_modesum DMAs them in). The same
@@ -4285,7 +4434,10 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         HIP_TRY(hipGetLastError());
     }
     // K5: segment table
-    {
+    if (Kmax <= SEG1_MAX_K) {
+        hipLaunchKernelGGL(k_segments_one, dim3(1, 1, nz), dim3(SEG1_NT), 0, st, B);
+        HIP_TRY(hipGetLastError());
+    } else {
         const int nslot = Kmax * MAXRUNS * 2;
         const int nblk = (nslot + 255) / 256;
         hipLaunchKernelGGL(k_segment_slots, dim3(nblk, 1, nz), dim3(256), 0, st, B);

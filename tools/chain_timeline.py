@@ -18,18 +18,17 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                 for r in rows)
-    # a chain starts at k_group_b and ends at the k_ll_final after it
+    # a chain runs from one k_group_b to the last kernel before the next
     chains, cur = [], None
     for s, e, n in ev:
         if n in ("k_ll_tile_const", "vectorized_elementwise_kernel", "__amd_rocclr_copyBuffer"):
             continue
         if n == "k_group_b":
+            if cur:
+                chains.append(cur)
             cur = [(s, e, n)]
         elif cur is not None:
             cur.append((s, e, n))
-            if n == "k_ll_final":
-                chains.append(cur)
-                cur = None
     chains = chains[len(chains) // 5:]   # skip warm-up
     names = [n for _, _, n in chains[0]]
     chains = [c for c in chains if [n for _, _, n in c] == names]

@@ -49,22 +49,27 @@ def fused(self, tm, params, args, kwargs, out):
         pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
     t2 = pc(); acc["setup"] += t2 - t1
     batch = tm.submit_batch
+    used = []
     for g0 in range(0, n, G):
         ta = pc()
         batch(B, params[g0:g0 + G], *args, **kwargs)
         tb = pc(); acc["submit_batch"] += tb - ta
         gi, jobs = B.flush()
+        used.append(gi)
         tc = pc(); acc["flush"] += tc - tb
-        lib.efd_stream_order(F["gst"][gi], F["sum1"], 1)
-        tcon = self._tile_constants(jobs[0][1], s_sum)
-        B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)], s_sum.cuda_stream,
+        # each group's sum on its own stream (Likelihood.FUSED_SUM_OWN_STREAM)
+        sst = B.groups[gi]["stream"]
+        tcon = self._tile_constants(jobs[0][1], sst, F)
+        B.sum_loglike(gi, self._d, self._w_templ, out[g0:g0 + len(jobs)], sst.cuda_stream,
                       tile_const=tcon)
-        ev = F["ev"][gi]; ev.record(s_sum); B.release(gi, ev)
         td = pc(); acc["sum+events"] += td - tc
-    lib.efd_download(pin.data_ptr(), out.data_ptr(), 8 * n, s_sum.cuda_stream)
+    last = used[-1]
+    for gj in sorted(set(used) - {last}):
+        lib.efd_stream_order(F["gst"][gj], (ctypes.c_void_p * 1)(F["gst"][last]), 1)
+    lib.efd_download(pin.data_ptr(), out.data_ptr(), 8 * n, F["gst"][last])
     t3 = pc()
     B._pending = []
-    s_sum.synchronize()
+    B.groups[last]["stream"].synchronize()
     t4 = pc(); acc["sync"] += t4 - t3
     host = pin[:n].numpy().copy()
     if np.isnan(host).any():
