@@ -237,6 +237,7 @@ struct PrepBatch {
     PrepDesc d[EFD_BATCH_MAX];
     int64_t nf, nl, nl1;
     int32_t paired, n;
+    int32_t pcr_groups;   // k_prep_pcr_b groups the harmonics itself (k_group_b not launched)
 };
 static_assert(sizeof(PrepBatch) <= 3072, "kernel arguments stay well inside 4 KB");
 
@@ -509,6 +510,21 @@ __device__ void pcr_not_a_knot(int n, FX X, FY Y, FOUT OUT, double* L) {
 // GB_CAP cells (FEW's l <= 10, |n| <= 30: 21 x 61); otherwise a bitonic sort of (m, n, h) keys
 // in the global scratch gkeys. Both give the same groups and member order.
 constexpr int GB_CAP = 2048;
+__device__ __forceinline__ void header_init(Header* hdr) {
+    const bool init = hdr->magic == HDR_MAGIC;
+    hdr->contributions = 0;
+    hdr->evaluations = 0;
+    hdr->groups = 0;
+    hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
+    hdr->lane_hi = INT32_MIN;
+    if (!init) {
+        hdr->runs_overflow = 0;
+        hdr->bad_mn = 0;
+        hdr->bad_tile = 0;
+        hdr->pad[0] = hdr->pad[1] = 0;
+        hdr->magic = HDR_MAGIC;
+    }
+}
 __device__ __forceinline__ void group_minmax(int& v_lo, int& v_hi, int* red, int slot) {
     for (int o = 32; o > 0; o >>= 1) {
         v_lo = min(v_lo, __shfl_xor(v_lo, o));
@@ -533,21 +549,7 @@ __device__ __forceinline__ void group_body(const int32_t* __restrict__ marr,
     // the call's counters start at zero (this is the preparation's first kernel; every later
     // writer runs after it in stream order): no separate hipMemsetAsync per waveform. The error
     // flags stay set until efd_modesum_status clears them (sticky; see Header)
-    if (tid == 0) {
-        const bool init = hdr->magic == HDR_MAGIC;
-        hdr->contributions = 0;
-        hdr->evaluations = 0;
-        hdr->groups = 0;
-        hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
-        hdr->lane_hi = INT32_MIN;
-        if (!init) {
-            hdr->runs_overflow = 0;
-            hdr->bad_mn = 0;
-            hdr->bad_tile = 0;
-            hdr->pad[0] = hdr->pad[1] = 0;
-            hdr->magic = HDR_MAGIC;
-        }
-    }
+    if (tid == 0) header_init(hdr);
     __syncthreads();
     // k_modesum's (sin, cos)(k pi/256) table, computed once per waveform here and copied into
     // each tile's LDS by LDS-DMA (cheaper than 512 sincospi per tile at small harmonic counts)
@@ -713,17 +715,15 @@ __global__ __launch_bounds__(256) void k_group_b(const PrepBatch B) {
 // group_amp_at is the one evaluation: k_group_amp_b stores it for k_prep_b's Thomas roles, and
 // k_prep_pcr_b's amplitude waves call it for their own component (no gamp pass, one launch
 // fewer in the chain; the same operations in the same order, so the same values).
-__device__ __forceinline__ double4 group_amp_at(const double* __restrict__ amp,
-                                                const double* __restrict__ ylm_p,
-                                                const double* __restrict__ ylm_m, double sc_re,
-                                                double sc_im, const int32_t* __restrict__ gm,
-                                                const int32_t* __restrict__ gstart,
-                                                const int32_t* __restrict__ gmem, int K, int i,
-                                                int g) {
-    const bool partner = gm[g] != 0;
+template <class MEM>
+__device__ __forceinline__ double4 group_amp_sum(const double* __restrict__ amp,
+                                                 const double* __restrict__ ylm_p,
+                                                 const double* __restrict__ ylm_m, double sc_re,
+                                                 double sc_im, bool partner, int p0, int p1,
+                                                 MEM mem, int K, int i) {
     double bpr = 0.0, bpi = 0.0, bmr = 0.0, bmi = 0.0;
-    for (int p = gstart[g], pe = gstart[g + 1]; p < pe; ++p) {
-        const int h = gmem[p];
+    for (int p = p0; p < p1; ++p) {
+        const int h = mem(p);
         const double ar = amp[((size_t)i * K + h) * 2], ai = amp[((size_t)i * K + h) * 2 + 1];
         const double vr = ylm_p[2 * h], vi = ylm_p[2 * h + 1];
         const double y0r = -(sc_re * vr - sc_im * vi), y0i = -(sc_re * vi + sc_im * vr);
@@ -737,6 +737,16 @@ __device__ __forceinline__ double4 group_amp_at(const double* __restrict__ amp,
         }
     }
     return make_double4(bpr, bpi, bmr, bmi);
+}
+__device__ __forceinline__ double4 group_amp_at(const double* __restrict__ amp,
+                                                const double* __restrict__ ylm_p,
+                                                const double* __restrict__ ylm_m, double sc_re,
+                                                double sc_im, const int32_t* __restrict__ gm,
+                                                const int32_t* __restrict__ gstart,
+                                                const int32_t* __restrict__ gmem, int K, int i,
+                                                int g) {
+    return group_amp_sum(amp, ylm_p, ylm_m, sc_re, sc_im, gm[g] != 0, gstart[g], gstart[g + 1],
+                         [&](int p) { return gmem[p]; }, K, i);
 }
 __device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
                                                    const double* __restrict__ ylm_p,
@@ -1104,10 +1114,17 @@ struct GroupAmpSrc {   // group_amp_at's operands
     double sc_re, sc_im;
     const int32_t *gstart, *gmem;
 };
+// The block's (m, n) group when k_prep_pcr_b groups the harmonics itself (PrepBatch::pcr_groups,
+// k_group_b not launched): G, the group's (m, n) and its members in ascending h (LDS)
+struct LocalGroups {
+    bool on;
+    int G, m, n, count;
+    const int* mem;
+};
 __device__ __forceinline__ void prep_pcr_body(
     const double* __restrict__ t, const double* __restrict__ phi_phi,
     const double* __restrict__ phi_r, const double* __restrict__ f_phi,
-    const double* __restrict__ f_r, const GroupAmpSrc ga,
+    const double* __restrict__ f_r, const GroupAmpSrc ga, const LocalGroups lg,
     const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int nt, int K,
     double* __restrict__ coefT, double* __restrict__ kslope, double* __restrict__ coefA,
     int32_t* __restrict__ runs, Item* __restrict__ items, double* __restrict__ invcp,
@@ -1151,15 +1168,18 @@ __device__ __forceinline__ void prep_pcr_body(
         pcr_not_a_knot(nt, X, YV, OUT, lds);
         return;
     }
-    const int G = hdr->groups;
+    const int G = lg.on ? lg.G : hdr->groups;
     if (b >= 4 + K) {
         const int q = b - 4 - K;
         if (q >= 4 * G) return;
         const size_t ninterp = (size_t)4 * K;
         // component q & 3 of group q >> 2 at knot i (group_amp_at; no gamp pass)
         auto Y = [&](int i) {
-            const double4 v = group_amp_at(ga.amp, ga.ylm_p, ga.ylm_m, ga.sc_re, ga.sc_im, gm,
-                                           ga.gstart, ga.gmem, K, i, q >> 2);
+            const double4 v =
+                lg.on ? group_amp_sum(ga.amp, ga.ylm_p, ga.ylm_m, ga.sc_re, ga.sc_im, lg.m != 0,
+                                      0, lg.count, [&](int p) { return lg.mem[p]; }, K, i)
+                      : group_amp_at(ga.amp, ga.ylm_p, ga.ylm_m, ga.sc_re, ga.sc_im, gm,
+                                     ga.gstart, ga.gmem, K, i, q >> 2);
             const int c = q & 3;
             return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
         };
@@ -1169,7 +1189,7 @@ __device__ __forceinline__ void prep_pcr_body(
     }
     const int h = b - 4;   // (m, n) group
     if (h >= G) return;
-    const int m = gm[h], n = gn[h];
+    const int m = lg.on ? lg.m : gm[h], n = lg.on ? lg.n : gn[h];
     const int ni = nt - 1;
     Item* it = items + (size_t)h * ni;
     int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
@@ -1190,6 +1210,7 @@ __device__ __forceinline__ void prep_pcr_body(
             rr[4 * r] = rr[4 * r + 1] = rr[4 * r + 2] = 0;
             rrs[4 * r] = rrs[4 * r + 1] = rrs[4 * r + 2] = 0;
         }
+        rr[3] = 0;   // run-overflow marker, raised into the header by k_items
         int nrun = 0, cur_sign = 0, ja = 0;
         for (int j = 0; j <= ni; ++j) {
             const int sg = j < ni ? sgv[j] : 0;
@@ -1201,7 +1222,9 @@ __device__ __forceinline__ void prep_pcr_body(
                         rr[4 * nrun + 2] = rrs[4 * nrun + 2] = cur_sign;
                         ++nrun;
                     } else {
-                        atomicOr(&hdr->runs_overflow, 1);
+                        // not the header itself: with pcr_groups its initialisation runs in
+                        // this same launch (block 0), unordered with this block
+                        rr[3] = 1;
                     }
                 }
                 cur_sign = sg;
@@ -1235,12 +1258,88 @@ __device__ __forceinline__ void prep_pcr_body(
         }
     }
 }
+// PrepBatch::pcr_groups (every waveform of the batch on the PCR roles with K <= 64): each block
+// groups the K harmonics itself, one per lane: a harmonic's group is the rank of its (m, n) among
+// the distinct pairs, its place in gmem the count of harmonics of smaller (m, n) plus the members
+// of its own before it. The same groups, order and member lists as k_group's counting sort (the
+// same clamping and bad_mn rule). Block 0 also writes them (gm, gn, gstart, gmem, G), initialises
+// the header and fills the sin/cos table: k_group_b's work, without its launch.
+constexpr int PCR_GROUPS_MAX_K = 64;
+__device__ __forceinline__ LocalGroups pcr_local_groups(const PrepDesc& D, char* W,
+                                                        const Layout& L, int* s_mem) {
+    const int lane = threadIdx.x, K = D.K, b = blockIdx.x;
+    int m = 0, n = 0, key = INT32_MAX;
+    bool bad = false;
+    if (lane < K) {
+        const int mr = D.m[lane], nr = D.n[lane];
+        bad = mr < -256 || mr > 255 || nr < -1024 || nr > 1023;
+        m = min(max(mr, -256), 255);
+        n = min(max(nr, -1024), 1023);
+        key = ((m + 256) << 11) | (n + 1024);
+    }
+    int less = 0, eqb = 0;   // harmonics of smaller (m, n); of the same (m, n) before this one
+    for (int j = 0; j < K; ++j) {
+        const int kj = __shfl(key, j, 64);
+        less += kj < key;
+        eqb += (kj == key) & (j < lane);
+    }
+    const bool first = lane < K && eqb == 0;
+    int rank = 0;   // distinct (m, n) below this one: the group index
+    for (int j = 0; j < K; ++j) {
+        const int kj = __shfl(key, j, 64);
+        const int fj = __shfl(first ? 1 : 0, j, 64);
+        rank += fj & (kj < key);
+    }
+    LocalGroups lg{};
+    lg.on = true;
+    lg.G = __popcll(__ballot(first));
+    lg.mem = s_mem;
+    if (b == 0) {
+        Header* hdr = ws_at<Header>(W, L.header);
+        if (first) {
+            ws_at<int32_t>(W, L.gm)[rank] = m;
+            ws_at<int32_t>(W, L.gn)[rank] = n;
+            ws_at<int32_t>(W, L.gstart)[rank] = less;
+        }
+        if (lane < K) ws_at<int32_t>(W, L.gmem)[less + eqb] = lane;
+        const bool anybad = __ballot(bad) != 0ull;
+        if (lane == 0) {
+            header_init(hdr);
+            ws_at<int32_t>(W, L.gstart)[lg.G] = K;
+            hdr->groups = lg.G;
+            if (anybad) hdr->bad_mn = 1;
+        }
+        double2* sctab_g = ws_at<double2>(W, L.sctab);
+        for (int i = lane; i < 512; i += 64) {
+            double sv, cv;
+            sincospi((double)i / 256.0, &sv, &cv);
+            sctab_g[i] = make_double2(sv, cv);
+        }
+    }
+    const int g = b < 4 ? -1 : b < 4 + K ? b - 4 : (b - 4 - K) >> 2;
+    if (g >= 0 && g < lg.G) {
+        const unsigned long long sel = __ballot(first && rank == g);
+        const int src = __ffsll((long long)sel) - 1;
+        lg.m = __shfl(m, src, 64);
+        lg.n = __shfl(n, src, 64);
+        const int kg = __shfl(key, src, 64);
+        const bool mine = lane < K && key == kg;
+        if (mine) s_mem[eqb] = lane;
+        lg.count = __popcll(__ballot(mine));
+    }
+    __syncthreads();
+    return lg;
+}
 __global__ __launch_bounds__(64) void k_prep_pcr_b(const PrepBatch B) {
     PREP_WALKER(B);
     if (!(D.pcr & 1) || (int)blockIdx.x >= 4 + ((D.pcr & 2) ? 5 : 1) * D.K) return;
     const GroupAmpSrc ga{D.amp, D.ylm_p, D.ylm_m, D.sc_re, D.sc_im,
                          ws_at<int32_t>(W, L.gstart), ws_at<int32_t>(W, L.gmem)};
-    prep_pcr_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ga, ws_at<int32_t>(W, L.gm),
+    __shared__ int s_mem[PCR_GROUPS_MAX_K];
+    LocalGroups lg{};
+    if (B.pcr_groups && (blockIdx.x == 0 || blockIdx.x >= 4))   // (blocks 1-3: trajectory only)
+        lg = pcr_local_groups(D, W, L, s_mem);
+    prep_pcr_body(D.t, D.phi_phi, D.phi_r, D.f_phi, D.f_r, ga, lg, ws_at<int32_t>(W, L.gm),
                   ws_at<int32_t>(W, L.gn), D.nt, D.K,
                   ws_at<double>(W, L.coefT), ws_at<double>(W, L.kslope), ws_at<double>(W, L.coefA),
                   ws_at<int32_t>(W, L.runs), ws_at<Item>(W, L.items), ws_at<double>(W, L.invcp),
@@ -1316,7 +1415,7 @@ __device__ __forceinline__ void items_body(const double* __restrict__ t, const d
                         const double* __restrict__ coefT, const int32_t* __restrict__ runs,
                         const double* __restrict__ freq, int64_t nf, int paired, int64_t nl,
                         int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges,
-                        Header* __restrict__ hdr) {
+                        Header* __restrict__ hdr, bool runs_mark) {
     const int ni = nt - 1;
     const int G = hdr->groups;
     // the grid is sized for K >= G groups: whole blocks past the records leave at once
@@ -1326,6 +1425,9 @@ __device__ __forceinline__ void items_body(const double* __restrict__ t, const d
     unsigned long long ev = 0, contrib = 0;
     if (gid < (int64_t)ni * G) {
         const int g = (int)(gid % G), j = (int)(gid / G);
+        // the PCR inverse splines' run-overflow marker (rr[3]) into the header's sticky flag
+        if (runs_mark && j == 0 && runs[(size_t)g * 4 * MAXRUNS + 3] != 0)
+            atomicOr(&hdr->runs_overflow, 1);
         build_item(t, f_phi, f_r, gm, gn, ni, K, coefA, coefT, runs, freq, nf, paired, nl, nl1,
                    items, ranges, g, j, ev);
         contrib = ev * (unsigned long long)(gstart[g + 1] - gstart[g]);
@@ -1352,7 +1454,7 @@ __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
                ws_at<int32_t>(W, L.gstart), D.nt, D.K, ws_at<double>(W, L.coefA),
                ws_at<double>(W, L.coefT), ws_at<int32_t>(W, L.runs), D.freq, B.nf, B.paired, B.nl,
                B.nl1, ws_at<Item>(W, L.items), ws_at<int4>(W, L.ranges),
-               ws_at<Header>(W, L.header));
+               ws_at<Header>(W, L.header), (D.pcr & 1) != 0);
 }
 
 // One interval record of group h; `evals` = its (branch x bin) evaluation count.
@@ -4401,11 +4503,15 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
     (void)nimax;
     hipStream_t st = (hipStream_t)stream;
     const unsigned nz = (unsigned)count;
-    // K0: (m, n) groups and, for the Thomas kernel's amplitude role, their amplitudes at the
-    // knots (the PCR amplitude waves evaluate their own)
+    // K0: (m, n) groups (in k_prep_pcr_b's blocks when the batch allows) and, for the Thomas
+    // kernel's amplitude role, their amplitudes at the knots (the PCR amplitude waves evaluate
+    // their own)
+    B.pcr_groups = (!any_thomas && Kmax <= PCR_GROUPS_MAX_K) ? 1 : 0;
     {
-        hipLaunchKernelGGL(k_group_b, dim3(1, 1, nz), dim3(256), 0, st, B);
-        HIP_TRY(hipGetLastError());
+        if (!B.pcr_groups) {
+            hipLaunchKernelGGL(k_group_b, dim3(1, 1, nz), dim3(256), 0, st, B);
+            HIP_TRY(hipGetLastError());
+        }
         if (any_thomas) {
             hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax + 255) / 256, ntmax, nz), dim3(256), 0,
                                st, B);

@@ -135,6 +135,29 @@ def test_rejected_shapes(base):
         _gpu(many)
 
 
+@pytest.mark.parametrize("K", [8, 100])
+def test_runs_overflow_reported(base, K):
+    """A frequency track with more than MAXRUNS (8) monotonic runs is reported by the status
+    check (sticky runs_overflow flag), whether the preparation groups the harmonics inside its
+    spline kernel (K <= 64, every role on PCR) or in k_group (K > 64); the report clears it, and
+    a clean source on the same engine then runs clean."""
+    t = base["t"]
+    d = _resample(base, np.linspace(t[0], t[-1], 256))
+    idx = np.arange(K) % len(base["m"])
+    d = {**d, "amp": np.asarray(d["amp"])[idx], "m": d["m"][idx], "n": d["n"][idx],
+         "ylm_p": d["ylm_p"][idx], "ylm_m": d["ylm_m"][idx]}
+    tt = d["t"]
+    wiggle = 1.0 + 0.2 * np.sin(2 * np.pi * 12 * (tt - tt[0]) / (tt[-1] - tt[0]))
+    bad = {**d, "f_phi": d["f_phi"] * wiggle}
+    eng = ModeSumEngine()
+    freq = torch.as_tensor(d["freq"], device="cuda")
+    with pytest.raises(_lib.EFDError):
+        eng.run(_inp(bad), freq, scale=float(d["prefactor"]))
+    S = eng.run(_inp(d), freq, scale=float(d["prefactor"])).cpu().numpy()
+    R = _oracle(d)
+    assert np.abs(S - R).max() <= RTOL * np.abs(R).max()
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_sources_finite_and_oracle(seed):
     """Seeded random sources over the configs' parameter ranges (M in [1e5, 1e7], e0 in

@@ -18,12 +18,14 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                 for r in rows)
-    # a chain runs from one k_group_b to the last kernel before the next
+    # a chain runs from one k_group_b (or k_prep_pcr_b when it groups the harmonics itself) to
+    # the last kernel before the next
     chains, cur = [], None
     for s, e, n in ev:
         if n in ("k_ll_tile_const", "vectorized_elementwise_kernel", "__amd_rocclr_copyBuffer"):
             continue
-        if n == "k_group_b":
+        starts = n == "k_group_b" or (n == "k_prep_pcr_b" and not (cur and cur[-1][2] == "k_group_b"))
+        if starts:
             if cur:
                 chains.append(cur)
             cur = [(s, e, n)]
