@@ -301,9 +301,19 @@ class Likelihood:
         lib = B.lib
         cur = torch.cuda.current_stream(self.device)
         curh = cur.cuda_stream
-        # the groups' streams and the sum stream after the work queued so far on the current one
-        _lib.check(lib.efd_stream_order(curh, F["order"], len(F["order"])), "efd_stream_order",
-                   lib)
+        # the streams this batch uses after the work queued so far on the current one: with the
+        # sums on the groups' own streams, only the groups' streams the batch's flushes take
+        # (B's rotation from its next group; one stream wait each)
+        if self.FUSED_SUM_OWN_STREAM:
+            key = ("ord", B._next, min(ngroups, len(B.groups)))
+            arr = F.get(key)
+            if arr is None:
+                gis = [(key[1] + k) % len(B.groups) for k in range(key[2])]
+                arr = F[key] = (ctypes.c_void_p * len(gis))(*[F["gst"][g] for g in gis])
+            _lib.check(lib.efd_stream_order(curh, arr, len(arr)), "efd_stream_order", lib)
+        else:
+            _lib.check(lib.efd_stream_order(curh, F["order"], len(F["order"])),
+                       "efd_stream_order", lib)
         pin = F.get("pin")
         if pin is None or pin.numel() < n:
             pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)

@@ -43,7 +43,12 @@ def fused(self, tm, params, args, kwargs, out):
         F["ev"] = [torch.cuda.Event() for _ in B.groups]
     lib = B.lib
     cur = torch.cuda.current_stream(self.device)
-    lib.efd_stream_order(cur.cuda_stream, F["order"], len(F["order"]))
+    key = ("ord", B._next, min(ngroups, len(B.groups)))
+    arr = F.get(key)
+    if arr is None:
+        gis = [(key[1] + k) % len(B.groups) for k in range(key[2])]
+        arr = F[key] = (ctypes.c_void_p * len(gis))(*[F["gst"][g] for g in gis])
+    lib.efd_stream_order(cur.cuda_stream, arr, len(arr))
     pin = F.get("pin")
     if pin is None or pin.numel() < n:
         pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
