@@ -1204,34 +1204,48 @@ __device__ __forceinline__ void prep_pcr_body(
         sgv[j] = (F1 > F0) ? 1 : ((F1 < F0) ? -1 : 0);
     }
     __syncthreads();
-    if (lane == 0) {
-        // maximal strictly monotonic runs, as inverse_splines scans them
-        for (int r = 0; r < MAXRUNS; ++r) {
-            rr[4 * r] = rr[4 * r + 1] = rr[4 * r + 2] = 0;
-            rrs[4 * r] = rrs[4 * r + 1] = rrs[4 * r + 2] = 0;
-        }
-        rr[3] = 0;   // run-overflow marker, raised into the header by k_items
-        int nrun = 0, cur_sign = 0, ja = 0;
-        for (int j = 0; j <= ni; ++j) {
-            const int sg = j < ni ? sgv[j] : 0;
-            if (sg != cur_sign || j == ni) {
-                if (cur_sign != 0) {
-                    if (nrun < MAXRUNS) {
-                        rr[4 * nrun] = rrs[4 * nrun] = ja;
-                        rr[4 * nrun + 1] = rrs[4 * nrun + 1] = j;
-                        rr[4 * nrun + 2] = rrs[4 * nrun + 2] = cur_sign;
-                        ++nrun;
-                    } else {
-                        // not the header itself: with pcr_groups its initialisation runs in
-                        // this same launch (block 0), unordered with this block
-                        rr[3] = 1;
-                    }
+    {
+        // maximal strictly monotonic runs, as inverse_splines scans them: a run of sign s != 0
+        // starts at j where sgv[j] = s differs from sgv[j - 1] (or j = 0) and ends at the next
+        // index whose sign differs (or ni, sign 0); the k-th start and the k-th end are run k's.
+        // The wave finds them 64 indices at a time with ballots (lane 0 walking every index
+        // serially was a chain of ni dependent LDS reads).
+        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        int nst = 0, nen = 0;   // starts / ends in the earlier chunks
+        for (int c = 0; c <= ni; c += 64) {
+            const int j = c + lane;
+            const int sj = j < ni ? sgv[j] : 0;
+            const int sp = (j >= 1 && j <= ni) ? sgv[j - 1] : 0;
+            const bool st = j < ni && sj != 0 && (j == 0 || sp != sj);
+            const bool en = j >= 1 && j <= ni && sp != 0 && sj != sp;
+            const unsigned long long bs = __ballot(st), be = __ballot(en);
+            if (st) {
+                const int r = nst + __popcll(bs & below);
+                if (r < MAXRUNS) {
+                    rr[4 * r] = rrs[4 * r] = j;
+                    rr[4 * r + 2] = rrs[4 * r + 2] = sj;
                 }
-                cur_sign = sg;
-                ja = j;
             }
+            if (en) {
+                const int r = nen + __popcll(be & below);
+                if (r < MAXRUNS) rr[4 * r + 1] = rrs[4 * r + 1] = j;
+            }
+            nst += __popcll(bs);
+            nen += __popcll(be);
         }
-        nrun_s = nrun;
+        const int nrun = min(nst, MAXRUNS);
+        // the unused run slots zeroed (none of them written above)
+        if (lane < 4 * MAXRUNS && (lane >> 2) >= nrun && (lane & 3) < 3) {
+            rr[lane] = 0;
+            rrs[lane] = 0;
+        }
+        if (lane == 0) {
+            // the run-overflow marker (not the header itself: with pcr_groups its
+            // initialisation runs in this same launch, block 0, unordered with this block),
+            // raised into the header by k_items
+            rr[3] = nst > MAXRUNS ? 1 : 0;
+            nrun_s = nrun;
+        }
     }
     __syncthreads();
     const int nrun = nrun_s;
@@ -1468,17 +1482,21 @@ __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
 // interior bins' rounding, and F' keeps the record's sign over the whole interval with a margin
 // of 1e-12 of its terms. Fold and edge records (overshooting t(g), turning points) keep the
 // tests; a safe record's lanes would all have passed them, so the spectrum is bitwise the same.
-__device__ bool record_safe(const Item& it, const double* __restrict__ freq, int64_t lo0,
-                            int64_t hi0, int64_t lo1, int64_t hi1) {
+// FAT(x) = freq[x] (build_item serves the range ends from the grid values it already holds)
+template <class FAT>
+__device__ bool record_safe(const Item& it, FAT fat, int64_t lo0, int64_t hi0, int64_t lo1,
+                            int64_t hi1) {
     // the g range of the lanes: s = 0 lanes k in [lo0, hi0) at g = -freq[k], s = 1 at +freq[k]
     double ga = INFINITY, gb = -INFINITY;
     if (hi0 > lo0) {
-        ga = fmin(ga, fmin(-freq[lo0], -freq[hi0 - 1]));
-        gb = fmax(gb, fmax(-freq[lo0], -freq[hi0 - 1]));
+        const double fa = fat(0, lo0), fb = fat(1, hi0 - 1);
+        ga = fmin(ga, fmin(-fa, -fb));
+        gb = fmax(gb, fmax(-fa, -fb));
     }
     if (hi1 > lo1) {
-        ga = fmin(ga, fmin(freq[lo1], freq[hi1 - 1]));
-        gb = fmax(gb, fmax(freq[lo1], freq[hi1 - 1]));
+        const double fa = fat(2, lo1), fb = fat(3, hi1 - 1);
+        ga = fmin(ga, fmin(fa, fb));
+        gb = fmax(gb, fmax(fa, fb));
     }
     if (!(ga <= gb)) return false;   // no lanes (or NaN)
     // the fast path's w at both ends (its exact operations)
@@ -1653,7 +1671,16 @@ __device__ void build_item(
     it.klo[0] = (int32_t)lo0; it.khi[0] = (int32_t)hi0;
     it.klo[1] = (int32_t)lo1; it.khi[1] = (int32_t)hi1;
     ranges[(size_t)h * ni + j] = make_int4((int)lo0, (int)hi0, (int)lo1, (int)hi1);
-    if (record_safe(it, freq, lo0, hi0, lo1, hi1)) it.fdneg |= 2;
+    // freq[x] for a range end x: from bound q's three grid values when x is one of them (the
+    // usual case: an end is its bound's answer or the index before), else loaded
+    auto fat = [&](int q, int64_t x) {
+        const int64_t g = bg[q];
+        if (g >= 1 && x == g - 1) return b3[q][0];
+        if (g < nf && x == g) return b3[q][1];
+        if (g + 1 < nf && x == g + 1) return b3[q][2];
+        return freq[x];
+    };
+    if (record_safe(it, fat, lo0, hi0, lo1, hi1)) it.fdneg |= 2;
     // branch x bin evaluations (on a paired grid one lane serves both the branch and its partner)
     const int mult = paired ? 1 + partner : 1;
     evals = (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
