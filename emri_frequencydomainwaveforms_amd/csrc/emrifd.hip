@@ -238,6 +238,7 @@ struct PrepBatch {
     int64_t nf, nl, nl1;
     int32_t paired, n;
     int32_t pcr_groups;   // k_prep_pcr_b groups the harmonics itself (k_group_b not launched)
+    int32_t seg_lds;      // k_segments_one's dynamic LDS bytes for the ranges table (0: none)
 };
 static_assert(sizeof(PrepBatch) <= 3072, "kernel arguments stay well inside 4 KB");
 
@@ -1934,6 +1935,7 @@ __global__ __launch_bounds__(256) void k_seg_tiles(const PrepBatch B) {
 // one launch instead of three.
 constexpr int SEG1_NT = 1024;
 constexpr int SEG1_MAX_K = SEG1_NT / (2 * MAXRUNS);
+constexpr int64_t SEG1_LDS_CAP = 40 * 1024;   // bytes of staged ranges (+ 33 KB static LDS)
 __device__ __forceinline__ int seg1_excl_scan(int v, int* wsum, int& total) {
     constexpr int NW = SEG1_NT / 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1964,9 +1966,19 @@ __global__ __launch_bounds__(SEG1_NT) void k_segments_one(const PrepBatch B) {
     __shared__ int32_t s_base[SEG1_NT];
     __shared__ int32_t s_roff[SEG1_NT];
     Header* hdr = ws_at<Header>(W, L.header);
-    const int4* ranges = ws_at<int4>(W, L.ranges);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nslot = 2 * MAXRUNS * D.K;   // <= SEG1_NT (host: every waveform has K <= SEG1_MAX_K)
+    // the interval records' lane ranges staged in LDS when they fit (one coalesced pass): the
+    // slots' bisections and the tile pairs then read LDS instead of chains of global loads
+    extern __shared__ int4 s_rg[];
+    const int ni = D.nt - 1;
+    const int4* ranges = ws_at<int4>(W, L.ranges);
+    if ((int64_t)D.K * ni * (int64_t)sizeof(int4) <= (int64_t)B.seg_lds) {
+        const int nrec = hdr->groups * ni;
+        for (int i = tid; i < nrec; i += SEG1_NT) s_rg[i] = ranges[i];
+        __syncthreads();
+        ranges = s_rg;
+    }
     int2 lh = make_int2(0, 0);
     int4 info = make_int4(0, 0, 0, 0);
     if (tid < nslot)
@@ -4568,7 +4580,15 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
     }
     // K5: segment table
     if (Kmax <= SEG1_MAX_K) {
-        hipLaunchKernelGGL(k_segments_one, dim3(1, 1, nz), dim3(SEG1_NT), 0, st, B);
+        // the largest ranges table of the batch that fits SEG1_LDS_CAP (K N_t int4s at most)
+        int64_t need = 0;
+        for (int i = 0; i < count; ++i) {
+            const int64_t b = (int64_t)a[i]->K * (a[i]->nt - 1) * 16;
+            if (b <= SEG1_LDS_CAP) need = std::max(need, b);
+        }
+        B.seg_lds = (int32_t)need;
+        hipLaunchKernelGGL(k_segments_one, dim3(1, 1, nz), dim3(SEG1_NT), (size_t)B.seg_lds, st,
+                           B);
         HIP_TRY(hipGetLastError());
     } else {
         const int nslot = Kmax * MAXRUNS * 2;
