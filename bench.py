@@ -112,16 +112,33 @@ def build_workloads(B, T=2.0, dt=10.0, eps=1e-5, sources="walkers", seed=2601996
     return out
 
 
+# The fixed algorithmic count of the FP64 roofline: FP64 FLOP per SPA evaluation, frozen at the
+# value the round-4 end kernel executed (profiles/r04h_pmc.json: (ADD + MUL + 2 FMA + TRANS)_F64
+# wave-instructions x 64 lanes x lane utilisation / evaluations = 51.547). An evaluation is one
+# (group branch, grid bin) pair (the workspace header's count, set by k_items from the records'
+# lane ranges), so evaluations x 51.5 is a property of the workload, not of the kernel build: a
+# cut in per-evaluation work shows as a gain in frac instead of a loss.
+FLOP_PER_EVAL_FIXED = 51.5
+
+
 def fp64_roofline(B, n_eval, kern_ms, caustic, sources="walkers"):
-    """FP64 VALU roofline of the mode-sum kernel: FLOP per launch from the committed rocprofv3
-    PMC pass (profiles/pmc_traffic.json, written by tools/summarize_profiles.py: FP64 FMA counts
-    2, MUL/ADD/TRANS 1, times 64 lanes x measured lane utilisation), taken per SPA evaluation and
-    scaled to this run's evaluation count, over this run's kernel time, against the 78.6 TFLOP/s
-    vector FP64 peak. traffic: HBM bytes per launch of the same PMC pass (2 FETCH_SIZE +
-    WRITE_SIZE, gfx950 correction)."""
+    """FP64 VALU roofline of the mode-sum kernel over the 78.6 TFLOP/s vector FP64 peak.
+
+    achieved / frac: the fixed algorithmic count, FLOP_PER_EVAL_FIXED x this launch's SPA
+    evaluations / this run's kernel time (HIP events). pmc_instructions: the executed-instruction
+    figure beside it, FLOP per evaluation from the committed rocprofv3 PMC pass
+    (profiles/pmc_traffic.json, written by tools/summarize_profiles.py: FP64 FMA counts 2,
+    MUL/ADD/TRANS 1, times 64 lanes x measured lane utilisation; pmc_matches_build says whether
+    that pass was taken on the kernel source being timed). traffic: HBM bytes per launch of the
+    same PMC pass (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction)."""
     import hashlib
-    out = {"bound": "fp64_valu", "achieved": None, "peak": FP64_VALU_PEAK_TFLOPS,
-           "unit": "TFLOP/s", "frac": None, "traffic": None}
+    flops = FLOP_PER_EVAL_FIXED * n_eval   # n_eval: the launch's SPA evaluations (all B waveforms)
+    tf = flops / (kern_ms * 1e-3) / 1e12
+    out = {"bound": "fp64_valu", "achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": tf / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+           "flops_per_launch": flops, "flops_per_evaluation": FLOP_PER_EVAL_FIXED,
+           "flops_count": "fixed algorithmic count: 51.5 FP64 FLOP per SPA evaluation "
+                          "(profiles/r04h_pmc.json) x evaluations per launch"}
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(prof):
         return out
@@ -135,18 +152,43 @@ def fp64_roofline(B, n_eval, kern_ms, caustic, sources="walkers"):
             return out
         src = os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc", "emrifd.hip")
         sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
-        flops = fpe * n_eval   # n_eval: the launch's SPA evaluations (all B waveforms)
-        tf = flops / (kern_ms * 1e-3) / 1e12
-        out.update(achieved=tf, frac=tf / FP64_VALU_PEAK_TFLOPS,
-                   flops_per_launch=flops, flops_per_evaluation=fpe,
-                   valu_busy=f.get("valu_busy"),
-                   pmc_source=pj.get("source"), pmc_matches_build=pj.get("src_sha16") == sha)
+        tfi = fpe * n_eval / (kern_ms * 1e-3) / 1e12
+        out["pmc_instructions"] = {
+            "achieved": tfi, "frac": tfi / FP64_VALU_PEAK_TFLOPS, "flops_per_evaluation": fpe,
+            "valu_busy": f.get("valu_busy"), "fp64_share_of_valu_insts":
+                f.get("fp64_share_of_valu_insts"), "effective_clock_ghz": pj.get("clock_ghz"),
+            "pmc_source": pj.get("source"), "pmc_matches_build": pj.get("src_sha16") == sha}
         if (int(pj.get("batch", 1)) == B and pj.get("workload") == "config2"
                 and pj.get("sources", "same") == sources):
             out["traffic"] = pj.get("hbm_bytes_per_launch")
+            out["traffic_write"] = pj.get("write_bytes_per_launch")
     except (ValueError, OSError, KeyError, TypeError):
         pass
     return out
+
+
+def library_info(lib):
+    """Which libemrifd.so was timed: its compiled-in build id against the hash of the sources in
+    this tree (emri_frequencydomainwaveforms_amd/_build.source_id)."""
+    from emri_frequencydomainwaveforms_amd import _build
+    bid = lib.efd_build_id().decode()
+    return {"build_id": bid, "sources_id": _build.source_id(),
+            "matches_sources": bid == _build.source_id()}
+
+
+def world_size(gpus):
+    """The rank count: WORLD_SIZE from the launcher (torch.distributed.run), which must equal
+    --gpus. A multi-GPU figure needs the launcher (one process per GPU); `bench.py --gpus 8`
+    started without it would time one GPU and print a valid-looking n_gpus = 1 line, so any
+    mismatch exits non-zero before touching a GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if gpus != world:
+        sys.stderr.write(
+            f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch one process per GPU with "
+            f"python -m torch.distributed.run --nnodes=1 --nproc-per-node {gpus} "
+            f"--master-addr 127.0.0.1 --master-port P bench.py --gpus {gpus} ...\n")
+        raise SystemExit(2)
+    return world
 
 
 def cpu_baseline(w, seconds=10.0):
@@ -314,15 +356,22 @@ def main():
     ap.add_argument("--no-tile-constants", action="store_true",
                     help="--likelihood: empty tiles recompute their logL partial (the A/B "
                          "baseline of efd_loglike_tile_constants)")
+    ap.add_argument("--scan", choices=["config3"], default=None,
+                    help="time BASELINE config 3's 10x10 (M, e0) scan instead: points round-robin "
+                         "over the ranks (parallel.ShardedScan), each rank's p0 solves, host "
+                         "upstream and batched device work, per-point records all-gathered")
     ap.add_argument("--api-steps", type=int, default=2,
                     help="--likelihood: half-steps timed with the host upstream in the loop")
     args = ap.parse_args()
+    world_size(args.gpus)
 
     import torch
     import torch.distributed as dist
 
     if args.likelihood:
         return bench_likelihood(args)
+    if args.scan:
+        return bench_scan(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -486,6 +535,7 @@ def main():
             "value": value,
             "unit": "waveforms/s",
             "n_gpus": world,
+            "world_size_rccl": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -524,6 +574,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_reference": cpu_ref,
             "few_gen": api,
+            "library": library_info(lib),
         }
         print(json.dumps(line))
     if world > 1:
@@ -536,6 +587,78 @@ LIKE_CONFIGS = {
     # ... -downsample 100 -Tobs 4 -nwalkers 128 (BASELINE configs[4])
     "config5": dict(Tobs=4.0, dt=10.0, eps=1e-2, nwalkers=128, ntemps=1, downsample=100),
 }
+
+
+def bench_scan(args):
+    """Waveforms/s of config 3's scan (check_mode_by_mode.py:183-229 over BASELINE configs[2]'s
+    grid: M = logspace(5, 7, 10), e0 = linspace(0.1, 0.6, 10), mu = 1e-5 M, Tobs = 1 yr, dt =
+    10 s, eps = 1e-2), host work included as the config asks: per point the p0 solve for 0.99
+    Tobs (get_p_at_t), the stand-in upstream and the device work. The 100 points go round-robin
+    over the ranks (parallel.ShardedScan; a fixed grid split over the ranks: strong scaling),
+    each rank runs its points through GenerateEMRIWaveform.generate_batch on its own host-core
+    share, and the per-point records (power of h+ and hx, max |h+|) are all-gathered. value =
+    100 / the max over ranks of a sweep's time (median of `steps` sweeps after `warmup`)."""
+    import torch
+    import torch.distributed as dist
+    from emri_frequencydomainwaveforms_amd import hostcpu
+    from emri_frequencydomainwaveforms_amd.parallel import ShardedScan
+    from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
+    from emri_frequencydomainwaveforms_amd.waveform import GenerateEMRIWaveform, _pool
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    share = hostcpu.pin()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    T, dt, eps = 1.0, 10.0, 1e-2
+    few = GenerateEMRIWaveform("FastSchwarzschildEccentricFlux",
+                               sum_kwargs=dict(pad_output=True, output_type="fd", odd_len=True),
+                               use_gpu=True, return_list=True)
+    traj = EMRIInspiral()
+    # injection angles and distance of emri_pe.py:603-617; p0 is solved per point
+    params = np.array([[M, 1e-5 * M, 0.0, 0.0, e0, 1.0, 2.4539, 0.2, 0.2, 0.8, 0.8, 1.0, 0.0,
+                        3.0] for M in np.logspace(5, 7, 10) for e0 in np.linspace(0.1, 0.6, 10)])
+
+    def p0_of(row):
+        return get_p_at_t(traj, 0.99 * T, [row[0], row[1], 0.0, row[4], 1.0])
+    scan = ShardedScan(few)
+    pool = _pool()
+    for _ in range(max(1, args.warmup)):
+        scan(params, T=T, dt=dt, eps=eps, p0_solver=p0_of, mapper=pool.map)
+    times = []
+    for _ in range(args.steps):
+        if world > 1:
+            dist.barrier()
+        res = scan(params, T=T, dt=dt, eps=eps, p0_solver=p0_of, mapper=pool.map)
+        times.append(float(res.seconds.max()))
+    sweep = float(np.median(times))
+    if rank == 0:
+        line = {
+            "metric": "FD waveforms/sec (config 3: 10x10 (M, e0) scan, Tobs=1yr, dt=10s, "
+                      "eps=1e-2, host p0 solve + upstream included) at 1/2/4/8 GPUs",
+            "value": len(params) / sweep, "unit": "waveforms/s", "n_gpus": world,
+            "world_size_rccl": dist.get_world_size() if world > 1 else 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": sweep * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (stand-in trajectory/amplitudes; FEW data absent offline)",
+            "config": {"workload": "config3: M=logspace(5,7,10) e0=linspace(0.1,0.6,10) "
+                                   "mu=1e-5 M Tobs=1yr dt=10s eps=1e-2",
+                       "points": len(params), "points_per_rank":
+                           np.bincount(res.owner, minlength=world).tolist(),
+                       "parallelism": f"points round-robin x{world} (all-gather of per-point "
+                                      "records)" if world > 1 else "1 GPU",
+                       "host_cores_rank0": len(share)},
+            "rank_seconds_last_sweep": res.seconds.tolist(),
+            "sweep_seconds": times,
+            "record_checksum": float(np.sum(res.summary[:, :2])),
+            "note": "value: 100 points / the max over ranks of one sweep (p0 solves on the "
+                    "rank's upstream pool, generate_batch's host upstream and device groups of "
+                    "16, per-point records); median over steps",
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def bench_likelihood(args):

@@ -29,11 +29,39 @@ def _inputs():
     return [SRC, CPU_SRC, HOST_SRC, MODES_SRC, hdr] + glob.glob(os.path.join(CSRC, "*.inc"))
 
 
+def source_id():
+    """16 hex digits of the SHA-256 over the library's sources (name and contents, sorted): the
+    build id compiled into libemrifd.so (efd_build_id)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(_inputs()):
+        if os.path.exists(p):
+            h.update(os.path.basename(p).encode() + b"\0")
+            h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def built_id(path=OUT):
+    """The build id tagged into an existing library file (read from its bytes, not loaded), or
+    None."""
+    try:
+        data = open(path, "rb").read()
+    except OSError:
+        return None
+    i = data.find(b"EFD_BUILD_ID=")
+    if i < 0:
+        return None
+    j = data.find(b"\0", i)
+    return data[i + 13:j].decode(errors="replace")
+
+
 def build(force=False, verbose=False, extra=()):
-    if not force and os.path.exists(OUT):
-        t = os.path.getmtime(OUT)
-        if all(os.path.getmtime(p) <= t for p in _inputs() if os.path.exists(p)):
-            return OUT
+    """Compile libemrifd.so unless the in-tree one was built from exactly these sources (its
+    tagged build id equals source_id(): content, not file times, so a library that travelled
+    with the tree is reused only when it matches; anything else is rebuilt)."""
+    sid = source_id()
+    if not force and not extra and built_id() == sid:
+        return OUT
     os.makedirs(OBJDIR, exist_ok=True)
     obj = os.path.join(OBJDIR, "emrifd_cpu.o")
     hobj = os.path.join(OBJDIR, "emrifd_host.o")
@@ -44,7 +72,9 @@ def build(force=False, verbose=False, extra=()):
     mobj = os.path.join(OBJDIR, "emrifd_modes.o")
     modes = ["g++", "-O3", f"-march={CPU_ARCH}", "-ffast-math", "-fopenmp", "-fPIC",
              "-std=c++17", "-c", MODES_SRC, "-o", mobj]
-    hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *extra,
+    bid = [f'-DEFD_BUILD_ID="{sid}"'] if not extra else []
+    hip = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *bid,
+           *extra,
            "-o", OUT + ".tmp", obj, hobj, mobj, SRC, "-lgomp", "-lmvec"]
     for cmd in (cpu, host, modes, hip):
         if verbose:

@@ -4,7 +4,7 @@ torch.fft copies its input before every rocFFT call on this build (an out-of-pla
 overwrite it), which cost the windowed likelihood two full passes over its [rows][m] complex64
 buffer per transform pair; an in-place plan needs neither the copy nor a second buffer. The
 library is the one torch itself loaded (torch/lib/libhipfft.so), so there is one rocFFT in the
-process. Plans are made per (m, rows) by the caller and kept.
+process. Plans are made per (m, rows) by the caller, which bounds how many it keeps.
 """
 
 import ctypes
@@ -59,6 +59,16 @@ class C2CPlan:
             rc = lib.hipfftExecC2C(self._h, ptr, ptr, direction)
         if rc != 0:
             raise RuntimeError(f"hipfftExecC2C(m={self.m}, rows={self.rows}) failed: {rc}")
+
+    def destroy(self):
+        """Release the plan (and its work buffer) once the device has finished the transforms
+        already queued with it."""
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            import torch
+            torch.cuda.synchronize()
+            self._lib.hipfftDestroy(h)
+            self._h = None
 
     def __del__(self):
         h = getattr(self, "_h", None)

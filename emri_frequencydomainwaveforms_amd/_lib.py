@@ -19,10 +19,12 @@ EFD_CAUSTIC_UNIFORM = 1
 EFD_LOGLIKE_SCRATCH = 1024
 EFD_INNER_SCRATCH = 2048
 EFD_BATCH_MAX = 16
+EFD_HANN_ROWS_MAX = 16   # efd_hann_loglike's rows per call (include/emrifd.h)
 
 # every symbol include/emrifd.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = (
     "efd_version",
+    "efd_build_id",
     "efd_last_error",
     "efd_spline_build",
     "efd_modesum_workspace_bytes",
@@ -156,6 +158,8 @@ def load(path=None):
                              ctypes.c_size_t)
     lib.efd_version.restype = ctypes.c_int
     lib.efd_version.argtypes = []
+    lib.efd_build_id.restype = ctypes.c_char_p
+    lib.efd_build_id.argtypes = []
     lib.efd_last_error.restype = ctypes.c_int
     lib.efd_last_error.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.efd_spline_build.restype = ctypes.c_int

@@ -4368,6 +4368,15 @@ extern "C" {
 
 int efd_version(void) { return EFD_VERSION; }
 
+// The sources' hash this library was compiled from (_build.source_id(), passed by _build.py as
+// -DEFD_BUILD_ID), kept as a tagged string so the build can check an existing binary without
+// loading it: a shipped .so is reused only when its tag matches the sources at hand.
+#ifndef EFD_BUILD_ID
+#define EFD_BUILD_ID "unversioned"
+#endif
+__attribute__((used)) static const char efd_build_tag[] = "EFD_BUILD_ID=" EFD_BUILD_ID;
+const char* efd_build_id(void) { return efd_build_tag + 13; }
+
 #ifdef EFD_EXP
 int efd_exp_counters(unsigned long long* out) {
     HIP_TRY(hipDeviceSynchronize());

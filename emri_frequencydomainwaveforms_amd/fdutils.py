@@ -118,6 +118,17 @@ class HannConvolution:
     templates' logL without writing them."""
 
     KEEP_KERNELS = 2   # lag-kernel spectra kept (one per m)
+    KEEP_PLANS = 2     # hipFFT plans kept (one per (m, rows); the lengths outside the four-step's)
+    # The first-order form drops an O(e^2) term, ~3.5-5 / N^2 of max|S| (the test's 5 / N^2 bound:
+    # 5e-10 at N = 1e5, 5e-6 at N = 1e3). The likelihood takes this path only where that is below
+    # TOL (N >= 2,236,068: every 1-yr or longer grid at dt = 10 s); shorter grids keep the exact
+    # size-N DFT form (windowed_spectrum), as the reference's convolution is exact at every N.
+    TOL = 1e-12
+
+    @classmethod
+    def applies(cls, n):
+        """Whether the first-order form is within TOL of max|S| at grid length n."""
+        return int(n) >= 3 and 5.0 / float(n) ** 2 <= cls.TOL
 
     def __init__(self, n, device):
         require_gpu()
@@ -236,6 +247,10 @@ class HannConvolution:
                    "efd_hann_stage", lib)
         plan = self._plans.get((m, rows))
         if plan is None:
+            # bounded like the lag kernels: m follows each batch's support and rows the last,
+            # partial group, so unbounded plans (each with its work buffer) would pile up
+            while len(self._plans) >= self.KEEP_PLANS:
+                self._plans.pop(next(iter(self._plans))).destroy()
             plan = self._plans[(m, rows)] = _hipfft.C2CPlan(m, rows)
         plan(yp, _hipfft.FORWARD, st)
         Y.mul_(self.kernel_spectrum(m))
@@ -342,8 +357,11 @@ class get_fd_waveform_fromFD:
         self.dt = dt
         self._mult = None if window is None else window_multiplier(window, window_in_fd)
         # the reference's own window (hann(N), emri_pe.py:261) takes HannConvolution
+        # when the first-order form is within HannConvolution.TOL at this length (applies(N));
+        # shorter grids keep the exact transform pair (windowed_spectrum)
         self._hann = (HannConvolution(len(window), dev)
-                      if window is not None and not window_in_fd and HannConvolution.matches(window)
+                      if window is not None and not window_in_fd
+                      and HannConvolution.applies(len(window)) and HannConvolution.matches(window)
                       else None)
         # contiguous-suffix mask (f >= 0 of a sorted grid): the fused fill path applies
         pm = self.positive_frequency_mask

@@ -9,10 +9,15 @@ the launcher's `OMP_NUM_THREADS=1` (torchrun sets it) nor a whole node's cores p
 them:
 
   - the process's affinity set is split into `LOCAL_WORLD_SIZE` contiguous, disjoint shares and
-    rank `LOCAL_RANK` takes its own (a single process keeps the whole set);
-  - `pin()` restricts the process to that share (os.sched_setaffinity), so ranks on one node do
-    not oversubscribe each other's cores;
-  - `threads()` is the share's size, capped at `MAX_THREADS`; `EFD_HOST_THREADS` overrides it.
+    rank `LOCAL_RANK` takes its own (a single process keeps the whole set). A set that already
+    looks per-rank (at most the node's cores / LOCAL_WORLD_SIZE: the launcher or scheduler
+    bound each rank) is kept as it is, and `EFD_HOST_SPLIT=0` turns the split off;
+  - `pin()` restricts every thread of the process to that share (os.sched_setaffinity on each
+    task of /proc/self/task: the call is per thread on Linux, so threads torch or HIP started
+    earlier would otherwise keep the whole node; threads started later inherit it), so ranks
+    on one node do not oversubscribe each other's cores;
+  - `threads()` is the share's size, capped at `MAX_THREADS`; `EFD_HOST_THREADS` overrides the
+    count (the process is pinned either way).
 """
 
 import os
@@ -25,18 +30,23 @@ def local_rank_world(env=None):
     return int(env.get("LOCAL_RANK", "0")), int(env.get("LOCAL_WORLD_SIZE", "1"))
 
 
-def rank_cores(affinity=None, local_rank=None, local_world=None):
+def rank_cores(affinity=None, local_rank=None, local_world=None, node_cores=None):
     """This rank's disjoint share of `affinity` (default: the process's affinity set), split
     into `local_world` contiguous chunks of equal size (the remainder goes to the first ranks).
-    With fewer cores than ranks every rank keeps one core (round-robin)."""
+    With fewer cores than ranks every rank keeps one core (round-robin). A set of at most
+    node_cores // local_world cores (default node: os.cpu_count()) is already per-rank and is
+    returned whole."""
     cores = sorted(os.sched_getaffinity(0) if affinity is None else affinity)
     lr, lw = local_rank_world()
     lr = lr if local_rank is None else int(local_rank)
     lw = lw if local_world is None else int(local_world)
-    if lw <= 1 or not cores:
-        return cores
-    if not 0 <= lr < lw:
+    if lw > 1 and not 0 <= lr < lw:
         raise ValueError(f"local rank {lr} outside a local world of {lw}")
+    if lw <= 1 or not cores or os.environ.get("EFD_HOST_SPLIT", "1") == "0":
+        return cores
+    node = node_cores if node_cores is not None else (os.cpu_count() or len(cores))
+    if len(cores) <= node // lw:
+        return cores   # already a per-rank set (bound by the launcher): not split again
     if len(cores) < lw:
         return [cores[lr % len(cores)]]
     base, extra = divmod(len(cores), lw)
@@ -48,23 +58,37 @@ _PINNED = None
 
 
 def pin():
-    """Restrict this process to its rank's share (once; a no-op for a single local process).
-    Returns the share."""
+    """Restrict every thread of this process to its rank's share (once; a no-op for a single
+    local process). Returns the share."""
     global _PINNED
     if _PINNED is None:
         share = rank_cores()
         _, lw = local_rank_world()
         if lw > 1 and set(share) != os.sched_getaffinity(0):
-            os.sched_setaffinity(0, share)
+            _pin_all_threads(share)
         _PINNED = share
     return _PINNED
+
+
+def _pin_all_threads(share):
+    """sched_setaffinity for every thread of the process (Linux: the call takes a thread id)."""
+    try:
+        tids = [int(t) for t in os.listdir("/proc/self/task")]
+    except OSError:
+        tids = [0]
+    for tid in tids:
+        try:
+            os.sched_setaffinity(tid, share)
+        except (OSError, ProcessLookupError):
+            pass   # a thread that ended meanwhile
+    os.sched_setaffinity(0, share)
 
 
 def threads(share=None):
     """Host threads for this rank's upstream: its share's size (at most MAX_THREADS), or
     EFD_HOST_THREADS when set. OMP_NUM_THREADS is deliberately not consulted."""
+    share = pin() if share is None else share
     env = os.environ.get("EFD_HOST_THREADS")
     if env:
         return max(1, int(env))
-    share = pin() if share is None else share
     return max(1, min(len(share), MAX_THREADS))

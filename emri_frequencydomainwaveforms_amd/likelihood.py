@@ -212,11 +212,13 @@ class Likelihood:
                     self._preds[slot].loglike(self._pbufs[slot], self._d, self._w_templ,
                                               out=out[i:i + 1])
             P.wait()
-        elif getattr(tm, "can_fill_batch", False):
+        elif getattr(tm, "can_fill_batch", False) and not args:
             # windowed templates (the drivers' Hann window): groups of WINDOW_GROUP walkers,
             # their spectra in one buffer and the window's transforms batched over them
-            # and the windowed templates' logL reduced in place (efd_hann_loglike)
-            G = max(1, int(getattr(tm, "WINDOW_GROUP", 8)))
+            # and the windowed templates' logL reduced in place (efd_hann_loglike, at most
+            # EFD_HANN_ROWS_MAX rows a call). The batch takes keyword waveform arguments only;
+            # extra positional ones go to the per-walker fill below, which forwards them
+            G = min(max(1, int(getattr(tm, "WINDOW_GROUP", 8))), _lib.EFD_HANN_ROWS_MAX)
             scr = getattr(self, "_wscratch", None)
             if scr is None or scr.numel() < G * _lib.EFD_LOGLIKE_SCRATCH:
                 scr = self._wscratch = torch.empty(G * _lib.EFD_LOGLIKE_SCRATCH,
@@ -360,13 +362,18 @@ class Likelihood:
             B._pending = []
             # `out` belongs to the current stream: nothing may still write it when it is
             # returned, or freed after an exception
-            if not own:
+            if sys.exc_info()[0] is not None:
+                # a failure inside B.flush() (staging, workspace growth, preparation) may leave
+                # a group's upload or preparation queued before that group reached `used`: wait
+                # for every group stream (and the sum stream), not only the recorded ones
+                for g in B.groups:
+                    g["stream"].synchronize()
+                if not own:
+                    s_sum.synchronize()
+            elif not own:
                 s_sum.synchronize()
             elif used:
                 B.groups[used[-1]]["stream"].synchronize()
-                if len(set(used)) > 1 and sys.exc_info()[0] is not None:
-                    for gj in set(used):
-                        B.groups[gj]["stream"].synchronize()
         host = pin[:n].numpy().copy()
         if np.isnan(host).any():
             B.wait()   # device-side errors of the groups' workspaces (sticky across reuse)

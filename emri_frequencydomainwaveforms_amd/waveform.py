@@ -439,6 +439,10 @@ class GenerateEMRIWaveform:
         return self._run_batch(params, out, lambda j: dict(out=torch.view_as_real(out[j])),
                                T, dt, eps, f_arr, kwargs, lanes=lanes)
 
+    def positive_bins(self, T=1.0, dt=10.0, f_arr=None):
+        """N_pos, the f >= 0 bins of the grid generate_batch writes (its out's last dimension)."""
+        return self._batch_grid(T, dt, f_arr)[1]
+
     def _batch_grid(self, T, dt, f_arr):
         gen = self.waveform_generator
         if gen.output_type != "fd":

@@ -48,6 +48,10 @@ extern "C" {
 /* Library version (major*10000 + minor*100 + patch). */
 int efd_version(void);
 
+/* The source hash the library was built from (16 hex digits of the SHA-256 over its sources,
+ * emri_frequencydomainwaveforms_amd/_build.py source_id), or "unversioned". Static storage. */
+const char* efd_build_id(void);
+
 /* Copies the last error message of the calling thread into buf (NUL-terminated). */
 int efd_last_error(char* buf, int len);
 

@@ -31,6 +31,10 @@ def test_library_exports_every_symbol():
     for name in declared_functions():
         assert hasattr(lib, name), name
     assert lib.efd_version() == 100
+    # the library that loads was compiled from exactly these sources (a library that travelled
+    # with the tree is reused only when its tagged build id matches, _build.build)
+    from emri_frequencydomainwaveforms_amd import _build
+    assert lib.efd_build_id().decode() == _build.source_id() == _build.built_id()
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
                         text=True, check=True).stdout
     for name in declared_functions():

@@ -277,3 +277,34 @@ def test_extent_from_lane_ranges():
         lo, hi = int(ln[r, 0]), int(ln[r, 1])
         k = np.nonzero(nz[r])[0]
         assert len(k) and k.min() >= min(lo, n - hi) and k.max() < max(hi, n - lo)
+
+
+def test_windowed_likelihood_short_grid_exact_path():
+    """A short grid (Tobs = 0.02 yr, N = 63,115 bins): the first-order Hann form would be off by
+    ~3.5-5 / N^2 ~ 1e-9 of max|S| here, so the likelihood must take the exact size-N transform
+    pair (windowed_spectrum) instead (HannConvolution.applies). Checked: the path taken, and
+    each walker's logL against the CPU loglike of the GPU's own spectrum windowed by the
+    reference's convolution (likelihood_oracle.windowed_polarizations) at 1e-10 relative; the
+    injection's logL is 0 exactly."""
+    from emri_frequencydomainwaveforms_amd.fdutils import HannConvolution
+    s = pe.setup(Tobs=0.02, dt=10.0, eps=1e-2, M=1e5, mu=10.0, nwalkers=8, ntemps=1,
+                 window_flag=True)
+    n = s.info["N_f"]
+    assert n == 63115 and not HannConvolution.applies(n) and HannConvolution.applies(12623261)
+    gen = s.gen
+    assert gen._hann is None and not gen.can_fill_batch     # the exact transform pair
+    like = s.like
+    batch = s.half_steps()[0]
+    ll = like(batch, **s.kwargs)
+    assert like(s.truth6[None, :], **s.kwargs)[0] == 0.0
+    f = s.f_like
+    w = lo.noise_factor(f, [get_sensitivity(f)] * 2)
+    window = gen.window
+    grid = s.few.waveform_generator.create_waveform.frequency
+    grid = grid.cpu().numpy() if hasattr(grid, "detach") else np.asarray(grid)
+    S0 = s.few._spectrum(*s.truth14, **s.kwargs).cpu().numpy()
+    d_gpu = _windowed_channels(S0, window, grid) * w
+    for i, p in enumerate(s.transform.both_transforms(batch)):
+        S = s.few._spectrum(*p, **s.kwargs).cpu().numpy()
+        ll_self = lo.loglike(_windowed_channels(S, window, grid), d_gpu, w)
+        assert abs(ll[i] - ll_self) <= 1e-10 * abs(ll_self), (i, ll[i], ll_self)

@@ -107,3 +107,53 @@ def test_two_ranks_pin_disjoint_shares():
         assert g["threads"] == g["pool"] == min(len(g["share"]), hostcpu.MAX_THREADS)
     assert set(a["fake"]).isdisjoint(b["fake"]) and len(a["fake"]) == len(b["fake"]) == 64
     assert np.array_equal(res[1][0]["share"], a["share"])   # both ranks saw the same gather
+
+
+def test_per_rank_set_not_split_again(monkeypatch):
+    """A launcher that already bound each rank to its own cores (a set of at most node / LW
+    cores) keeps that set whole; EFD_HOST_SPLIT=0 turns the split off."""
+    own = set(range(32, 48))                  # 16 cores of a 128-core node, 8 ranks
+    assert hostcpu.rank_cores(own, 3, 8, node_cores=128) == sorted(own)
+    whole = set(range(128))
+    assert hostcpu.rank_cores(whole, 3, 8, node_cores=128) == list(range(48, 64))
+    monkeypatch.setenv("EFD_HOST_SPLIT", "0")
+    assert hostcpu.rank_cores(whole, 3, 8, node_cores=128) == sorted(whole)
+
+
+_PIN_CHILD = r"""
+import os, sys, threading, time, json
+os.environ.update(LOCAL_RANK="1", LOCAL_WORLD_SIZE="2", EFD_HOST_THREADS="5")
+sys.path.insert(0, sys.argv[1])
+stop = threading.Event()
+t = threading.Thread(target=stop.wait, daemon=True)
+t.start()
+time.sleep(0.05)
+from emri_frequencydomainwaveforms_amd import hostcpu
+n = hostcpu.threads()        # EFD_HOST_THREADS set: the count is 5, the process still pinned
+share = sorted(hostcpu.pin())
+tids = [int(x) for x in os.listdir("/proc/self/task")]
+aff = {tid: sorted(os.sched_getaffinity(tid)) for tid in tids}
+stop.set()
+print(json.dumps(dict(n=n, share=share, aff=list(aff.values()))))
+"""
+
+
+def test_pin_every_thread_and_override():
+    """pin() restricts every thread of the process (a thread started before it included), and
+    setting EFD_HOST_THREADS still pins."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if len(os.sched_getaffinity(0)) < 2:
+        pytest.skip("needs 2 cores to split")
+    env = dict(os.environ)
+    env.pop("EFD_HOST_SPLIT", None)
+    r = subprocess.run([sys.executable, "-c", _PIN_CHILD, root], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n"] == 5
+    full = sorted(os.sched_getaffinity(0))
+    assert out["share"] == hostcpu.rank_cores(set(full), 1, 2)
+    assert len(out["aff"]) >= 2 and all(a == out["share"] for a in out["aff"])

@@ -64,6 +64,7 @@ def main(tag):
                                + pmc["SQ_INSTS_VALU_ADD_F64"] + pmc["SQ_INSTS_VALU_TRANS_F64"])
         gpu_cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
         fp64 = {"flops_per_launch": flops, "lane_utilisation": util,
+                "gpu_cycles_per_launch": gpu_cycles,
                 "valu_busy": pmc["SQ_ACTIVE_INST_VALU"] / 256.0 / gpu_cycles,
                 "fp64_share_of_valu_insts": (pmc["SQ_INSTS_VALU_FMA_F64"]
                                              + pmc["SQ_INSTS_VALU_MUL_F64"]
@@ -97,8 +98,15 @@ def main(tag):
     import hashlib
     src_sha = hashlib.sha256(open(os.path.join(ROOT, "emri_frequencydomainwaveforms_amd", "csrc",
                                                "emrifd.hip"), "rb").read()).hexdigest()[:16]
+    # effective clock of the launch: GPU cycles (GRBM_GUI_ACTIVE over the 8 XCDs) / rocprof time
+    clock = (fp64["gpu_cycles_per_launch"] / (stats["avg_ns"] * 1e-9) / 1e9
+             if fp64 and stats.get("avg_ns") else None)
+    summary["clock_ghz"] = clock
+    summary["write_bytes_per_launch"] = pmc["WRITE_SIZE"] * 1024.0
+    json.dump(summary, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"workload": "config2", "caustic": "uniform", "kernel": kernel, "batch": batch,
-               "sources": sources,
+               "sources": sources, "clock_ghz": clock,
+               "write_bytes_per_launch": pmc["WRITE_SIZE"] * 1024.0,
                "hbm_bytes_per_launch": hbm, "fp64": fp64, "evaluations_per_launch": evals,
                "src_sha16": src_sha, "source": f"profiles/{tag}_pmc.json"},
               open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
