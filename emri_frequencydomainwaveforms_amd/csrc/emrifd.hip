@@ -65,13 +65,34 @@ constexpr int NWAVE = TILE / 64;    // waves per workgroup
 // (paired A/B, 3 rounds on two boxes, profiles/r04_ab_bpl3.jsonl); 4 spilled (-4%)
 constexpr int BPL = 3;
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
+// k_modesum's packed chunk record header (one word per record, read by v_readlane): the
+// sub-branch's lane range relative to the tile (HDR_HB bits each), s, the series length J (3
+// bits) and Item::fdneg (2 bits)
+constexpr int HDR_HB = TILE_LANES < 1024 ? 10 : 11;
+constexpr int HDR_S = 2 * HDR_HB, HDR_J = 2 * HDR_HB + 1, HDR_FD = 2 * HDR_HB + 4;
 constexpr int XCD_GROUP = 1024 / TILE;  // consecutive tiles per XCD in the dispatch order
 constexpr int MAXRUNS = 8;          // monotonic runs per harmonic
+// k_segments_one: one 1024-thread workgroup per waveform when its 2 MAXRUNS K segment slots fit
+constexpr int SEG1_NT = 1024;
+constexpr int SEG1_MAX_K = SEG1_NT / (2 * MAXRUNS);
 constexpr int MAX_NT = 1024;        // knots (FEW max_init_len is 1000); bounds LDS staging
 constexpr int KEYCAP = 2048;        // record keys per tile pass held in LDS
 constexpr int SEGWIN = TILE;        // segments examined per window (tile list build): 4 KB of LDS
                                     // instead of 16 at 4 x TILE, so 4 workgroups fit a CU
 constexpr int MAX_K = 8192;         // harmonics per call
+// Split tiles of the sparse fused likelihood (K <= SEG1_MAX_K: k_segments_one plans them). A
+// tile whose estimated cost (wave-records: records x the 192-lane wave chunks each reaches)
+// exceeds the waveform's fair share of the chip is evaluated by S workgroups, each taking every
+// S-th chunk of the tile's record list and writing its bins' partial sums; the last of the S
+// (agent-scope release / acquire, counter per tile) adds them in split order and runs the tile's
+// epilogue. Items: the work units of the sparse launch, (tile, split j, S, partial slot).
+constexpr int SPLIT_ITEM_CAP = 8192;   // items per waveform (union tiles + extra splits)
+constexpr int SPLIT_TILE_CAP = 128;    // split tiles per waveform
+constexpr int SPLIT_SLOT_CAP = 128;    // partial slots (sum of S over split tiles)
+constexpr int SPLIT_MAX = 16;          // workgroups per split tile
+constexpr int SPLIT_UNION_CAP = 4096;  // union tiles k_segments_one can cost (else no plan)
+constexpr int SPLIT_MIN_COST = 48;     // wave-records: tiles below this are never split
+constexpr int SPLIT_SLOTS_PER_WF = 64; // the fair share: a waveform's cost / this many workgroups
 constexpr double PI = 3.141592653589793238462643383279502884;
 constexpr double TWO_PI = 6.283185307179586476925286766559005768;
 constexpr double SQRT_3_2PI = 0.69098829894267095480;   // sqrt(3 / (2 pi))
@@ -118,11 +139,15 @@ int fail(int code, const std::string& msg) {
 //   Bp(t) = sum_l y0_l A_l(t),  Bm(t) = sum_l y1_l A_l(t)   (y0 = -scale Y+, y1 = conj(-scale Y-))
 // and one SPA evaluation serves every l. 288 B (18 pieces of 16 B), staged through LDS.
 struct __attribute__((aligned(16))) Item {
+    // Field order = the fast path's LDS reads: its first reads are 16-B pairs (ds_read_b128, 4
+    // LDS cycles; a misaligned pair takes ds_read2_b64, 8): [gx, ic0] [ic1, ic2] [ic3, tj]
+    // [ph0, ph1] [ph2, ph3] [fd0, fd1] [fd2, dtj]; dtj (uncertified records only) rides with fd2
     double gx;        // left end of the inverse-spline interval (ascending F)
     double ic[4];     // t(g) = ((ic0 u + ic1) u + ic2) u + ic3, u = g - gx
-    double tj, dtj;   // forward interval [tj, tj + dtj)
+    double tj;        // forward interval [tj, tj + dtj)
     double ph[4];     // Phi_mn(t) = m Phi_phi + n Phi_r, w = t - tj (scipy PPoly order)
     double fd[3];     // F'(t)
+    double dtj;
     double fdd[3];    // sqrt(3/(2 pi)) F''(t); F'' = derivative of the spline of F'(t_i) (:583)
     int32_t jser;     // K_{1/3} series terms the fast path needs on this interval (1..FAST_J)
     int32_t fdneg;    // F' < 0 at the interval's midpoint: the sign the fast path assumes for
@@ -134,6 +159,8 @@ struct __attribute__((aligned(16))) Item {
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
 };
 static_assert(sizeof(Item) == 288, "Item must be 288 B");
+static_assert(offsetof(Item, ph) % 16 == 0 && offsetof(Item, fd) % 16 == 0 &&
+              offsetof(Item, fdd) % 16 == 0, "the fast path's coefficient pairs are 16-B aligned");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
 constexpr int B_PIECE = (int)offsetof(Item, b) / 16;   // first piece of b (b[0]: 4, b[1]: 4)
 static_assert(offsetof(Item, b) % 16 == 0 && sizeof(Item::b) == 8 * 16, "b: 8 whole pieces");
@@ -155,7 +182,9 @@ struct Header {
     int32_t bad_tile;           // set by k_modesum when a dispatch-order entry is out of range
     int64_t magic;              // HDR_MAGIC once k_group has initialised the header
     int32_t lane_lo, lane_hi;   // union [lo, hi) of the segments' lane ranges (k_segment_compact)
-    int64_t pad[2];             // 64 B
+    int32_t nitems;             // sparse sum's work items (k_segments_one's split plan), -1: none
+    int32_t nsplit;             // split tiles of the plan
+    int64_t pad;                // 64 B
 };
 static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
@@ -164,7 +193,7 @@ struct Layout {
     size_t header, coefA, coefT, kslope, tscratch, invcp, invdp, runs, items, ranges, seglh,
         seginfo, nseg, slotlh, slotinfo, slotcnt, slottiles, segbase, stb0, stb1, gm, gn, gstart,
         gkeys,
-        gmem, gamp, sctab, tkeys, tcnt, tperm, llpart, total;
+        gmem, gamp, sctab, tkeys, tcnt, tperm, llpart, sitem, scnt, spart, total;
     int64_t stbcap;
     int64_t ntiles, nlanes;
 };
@@ -214,6 +243,12 @@ __host__ __device__ inline Layout make_layout(int32_t nt, int32_t K, int64_t nf,
     L.tcnt = take(sizeof(int32_t) * (size_t)L.ntiles);
     L.tperm = take(sizeof(int32_t) * (size_t)L.ntiles);   // cost-ordered dispatch (k_tile_order)
     L.llpart = take(sizeof(double) * (size_t)L.ntiles);   // fused likelihood: per-tile partials
+    // the sparse sum's split plan (k_segments_one, K <= SEG1_MAX_K only): items, one arrival
+    // counter per split tile, the partial sums of the splits ([slot][lane][4] doubles)
+    const bool plan = K <= SEG1_MAX_K && paired;
+    L.sitem = take(plan ? sizeof(int4) * SPLIT_ITEM_CAP : 0);
+    L.scnt = take(plan ? sizeof(int32_t) * SPLIT_TILE_CAP : 0);
+    L.spart = take(plan ? sizeof(double) * 4 * (size_t)SPLIT_SLOT_CAP * TILE_LANES : 0);
     L.total = off;
     return L;
 }
@@ -518,11 +553,13 @@ __device__ __forceinline__ void header_init(Header* hdr) {
     hdr->groups = 0;
     hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
     hdr->lane_hi = INT32_MIN;
+    hdr->nitems = -1;           // no split plan unless k_segments_one makes one
+    hdr->nsplit = 0;
     if (!init) {
         hdr->runs_overflow = 0;
         hdr->bad_mn = 0;
         hdr->bad_tile = 0;
-        hdr->pad[0] = hdr->pad[1] = 0;
+        hdr->pad = 0;
         hdr->magic = HDR_MAGIC;
     }
 }
@@ -1933,8 +1970,6 @@ __global__ __launch_bounds__(256) void k_seg_tiles(const PrepBatch B) {
 // (segment, record) (k_seg_tiles' work flattened over the workgroup: a record's segment found by
 // bisection of the segments' record offsets in LDS). The same tables as the three kernels, in
 // one launch instead of three.
-constexpr int SEG1_NT = 1024;
-constexpr int SEG1_MAX_K = SEG1_NT / (2 * MAXRUNS);
 constexpr int64_t SEG1_LDS_CAP = 40 * 1024;   // bytes of staged ranges (+ 33 KB static LDS)
 __device__ __forceinline__ int seg1_excl_scan(int v, int* wsum, int& total) {
     constexpr int NW = SEG1_NT / 64;
@@ -2022,13 +2057,98 @@ __global__ __launch_bounds__(SEG1_NT) void k_segments_one(const PrepBatch B) {
     }
     int32_t* stb0 = ws_at<int32_t>(W, L.stb0);
     int32_t* stb1 = ws_at<int32_t>(W, L.stb1);
+    // the sparse sum's split plan (paired grids, i.e. the fused likelihood): every union tile's
+    // cost in wave-records, from the same (segment, record) pairs. Possible when the union fits
+    // SPLIT_UNION_CAP tiles and every segment has its tile pairs (else nitems stays -1)
+    __shared__ int s_cost[SPLIT_UNION_CAP];
+    __syncthreads();   // wr[] (the union) is complete
+    int ulo = INT32_MAX, uhi = INT32_MIN;
+    for (int w = 0; w < NW; ++w) { ulo = min(ulo, wr[w].x); uhi = max(uhi, wr[w].y); }
+    const int ut0 = ulo < uhi ? ulo / TILE_LANES : 0;
+    const int nut = ulo < uhi ? (uhi - 1) / TILE_LANES - ut0 + 1 : 0;
+    const bool plan = B.paired && nut > 0 && nut <= SPLIT_UNION_CAP &&
+                      !__syncthreads_or(valid && sbase == SEG_NO_STB);
+    if (plan)
+        for (int i = tid; i < nut; i += SEG1_NT) s_cost[i] = 0;
+    __syncthreads();
     for (int f = tid; f < nrec_all; f += SEG1_NT) {
         int a = 0, b = nseg - 1;   // the last segment q with s_roff[q] <= f
         while (a < b) {
             const int mid = (a + b + 1) >> 1;
             if (s_roff[mid] <= f) a = mid; else b = mid - 1;
         }
-        seg_tiles_record(ranges, s_lh[a], s_info[a], s_base[a], f - s_roff[a], stb0, stb1);
+        const int p = f - s_roff[a];
+        seg_tiles_record(ranges, s_lh[a], s_info[a], s_base[a], p, stb0, stb1);
+        if (plan && p < s_info[a].y) {
+            // record p's cost per tile it reaches: the 64 BPL-lane wave chunks it touches there
+            // (modesum_tile evaluates a record on every wave whose bins it reaches)
+            const int4 in = s_info[a];
+            const int4 rg = ranges[in.x + (in.z > 0 ? p : in.y - 1 - p)];
+            const int klo = in.w ? rg.z : rg.x, khi = in.w ? rg.w : rg.y;
+            if (khi > klo) {
+                constexpr int WL = 64 * BPL;
+                for (int t = klo / TILE_LANES; t <= (khi - 1) / TILE_LANES; ++t) {
+                    const int a0 = max(klo, t * TILE_LANES), b0 = min(khi, (t + 1) * TILE_LANES);
+                    atomicAdd(&s_cost[t - ut0], (b0 - 1) / WL - a0 / WL + 1);
+                }
+            }
+        }
+    }
+    if (!plan) return;
+    __syncthreads();
+    // each thread takes SPLIT_UNION_CAP / SEG1_NT consecutive union tiles
+    constexpr int PER = SPLIT_UNION_CAP / SEG1_NT;
+    int64_t csum = 0;
+    for (int i = 0; i < PER; ++i) {
+        const int u = tid * PER + i;
+        csum += u < nut ? s_cost[u] : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
+    __shared__ int64_t s_csum[NW];
+    if (lane == 0) s_csum[wave] = csum;
+    __syncthreads();
+    int64_t total = 0;
+    for (int w = 0; w < NW; ++w) total += s_csum[w];
+    // the fair share of one workgroup: the waveform's cost over SPLIT_SLOTS_PER_WF workgroups
+    // (a walker group of 16 then fills the chip's ~1,024 resident slots); a tile above it is
+    // split into ceil(cost / share) (<= SPLIT_MAX) workgroups
+    const int64_t share = max((int64_t)SPLIT_MIN_COST, total / SPLIT_SLOTS_PER_WF);
+    int nS[PER];
+    int my_items = 0, my_slots = 0, my_split = 0;
+    for (int i = 0; i < PER; ++i) {
+        const int u = tid * PER + i;
+        int S = 1;
+        if (u < nut && s_cost[u] > share)
+            S = (int)min((int64_t)SPLIT_MAX, (s_cost[u] + share - 1) / share);
+        nS[i] = u < nut ? S : 0;
+        my_items += nS[i];
+        my_slots += S > 1 ? S : 0;
+        my_split += S > 1 ? 1 : 0;
+    }
+    int n_items, n_slots, n_split;
+    const int io = seg1_excl_scan(my_items, wsum, n_items);
+    const int so = seg1_excl_scan(my_slots, wsum, n_slots);
+    const int po = seg1_excl_scan(my_split, wsum, n_split);
+    if (n_split == 0 || n_items > SPLIT_ITEM_CAP || n_slots > SPLIT_SLOT_CAP ||
+        n_split > SPLIT_TILE_CAP)
+        return;   // nothing to split, or past the plan's capacity: the plain tile loop
+    int4* items = ws_at<int4>(W, L.sitem);
+    int32_t* cnt = ws_at<int32_t>(W, L.scnt);
+    int ii = io, sl = so, sp = po;
+    for (int i = 0; i < PER; ++i) {
+        const int u = tid * PER + i, S = nS[i];
+        for (int j = 0; j < S; ++j)
+            items[ii + j] = make_int4(ut0 + u, (j << 16) | S, S > 1 ? sl : -1, S > 1 ? sp : -1);
+        if (S > 1) {
+            cnt[sp] = 0;
+            sl += S;
+            ++sp;
+        }
+        ii += S;
+    }
+    if (tid == 0) {
+        hdr->nitems = n_items;
+        hdr->nsplit = n_split;
     }
 }
 
@@ -2288,6 +2408,13 @@ __device__ __noinline__ FwdEval forward_generic(double tt, const double* __restr
 }
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// the thread index made opaque at a use site: values derived from it are recomputed there instead
+// of being hoisted to the kernel's prologue as loop invariants (which, live across the record
+// loop's cold call, were spilled to scratch by every wave)
+__device__ __forceinline__ int opq(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 __device__ __forceinline__ double cubic(const double* __restrict__ c, double w) {
     return fma(fma(fma(c[0], w, c[1]), w, c[2]), w, c[3]);
@@ -2362,9 +2489,22 @@ __device__ __forceinline__ uint64_t class_mask(double x, int32_t cls) {
 __device__ __forceinline__ double ftz_select(bool ok, double v) {
     return __hiloint2double(ok ? __double2hiint(v) : 0, __double2loint(v));
 }
+// A wave-uniform test of the record header, re-derived in SALU at each use: the empty asm
+// makes the header word "new" to the compiler, so the test is an s_and + s_cmp on the SGPR
+// instead of a boolean kept alive across the bins' blocks, which the compiler turned into a
+// VGPR and back (v_cndmask + v_cmp, 2 VALU) for every bin after the first.
+__device__ __forceinline__ bool hdr_test(uint32_t ha, uint32_t mask) {
+    asm volatile("" : "+s"(ha));
+    return (ha & mask) != 0;
+}
+__device__ __forceinline__ bool hdr_j3(uint32_t ha) {   // the record's series length J >= 3
+    asm volatile("" : "+s"(ha));
+    return ((ha >> HDR_J) & 7u) >= 3u;
+}
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
-                                           int J, uint64_t actm, const double2* __restrict__ sct,
+                                           uint32_t ha, uint64_t actm,
+                                           const double2* __restrict__ sct,
                                            const RecSign& rs, double& wr, double& wi, double& w,
                                            uint64_t& needm) {
     const double u = sfk - it->gx;
@@ -2374,7 +2514,7 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
     const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
     const double afd = fabs(fd);
     uint64_t goodm = ~0ull;
-    if (!rs.safe) {   // wave-uniform: a record k_items could not certify tests every lane
+    if (!hdr_test(ha, 2u << HDR_FD)) {   // wave-uniform: a record k_items could not certify tests every lane
         asm volatile("");
         goodm = __builtin_amdgcn_ballot_w64((unsigned long long)__double_as_longlong(w) <
                                             (unsigned long long)__double_as_longlong(it->dtj)) &
@@ -2400,7 +2540,7 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         const double t3 = fdds * a3;
         double ww = t3 * t3;   // 1/|y|
         double am, c0, thn;
-        if (J >= 3) {   // wave-uniform; a real branch (see KTH0's notes)
+        if (hdr_j3(ha)) {   // J >= 3: wave-uniform; a real branch (see KTH0's notes)
             asm volatile("");
             // the |y| >= FAST_Y test only matters for J = 4 (J = 3 lanes pass it by their
             // record's bound), but a nested J test's condition crossed the join as a per-lane
@@ -2607,7 +2747,13 @@ __device__ __forceinline__ void modesum_tile(
     // every walker (efd_loglike_tile_constants); NULL: such tiles compute it
     const double* __restrict__ llconst,
     int64_t b,     // b: this workgroup's place in the waveform's dispatch order
-    bool direct = false) {   // b is the tile itself (k_modesum_batch's sparse form)
+    bool direct = false,     // b is the tile itself (k_modesum_batch's sparse form)
+    // a split tile (k_segments_one's plan; sparse form): this workgroup evaluates the chunks g of
+    // the tile's record list with g mod split_S = split_j, writes its bins' partial sums to slot
+    // spart + split_j, and the last of the split_S workgroups (arrival counter *scnt) adds the
+    // slots in order and runs the epilogue. split_S = 1: the whole tile
+    int split_j = 0, int split_S = 1, double* __restrict__ spart = nullptr,
+    int32_t* __restrict__ scnt = nullptr) {
     __shared__ uint32_t keys[KEYCAP];
     __shared__ Item stage[2][NC];
     __shared__ int part[TILE];
@@ -2655,8 +2801,12 @@ __device__ __forceinline__ void modesum_tile(
     // MODE.IEEE = 0 (rsqrt_pos_sum's output modifier). Nothing here depends on IEEE mode's NaN
     // rules: the one min (fmin(|thn|, 1)) sees quiet NaNs at most and returns 1 in either mode.
     __builtin_amdgcn_s_setreg(1 | (9 << 6), 0);               // hwreg(HW_REG_MODE, 9, 1)
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
+    // tid / lane are re-derived from tid0 through opq at the top of each loop and of the
+    // epilogue, so nothing derived from them is live across the record loop's cold call (the
+    // prologue's scratch stores of such values, 7 KB per wave, are gone)
+    const int tid0 = threadIdx.x;
+    int tid = tid0;
+    int lane = tid & 63;
     const int ni = nt - 1;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     // Prebuilt record list: k_tile_keys, launched in the preparation phase, stored this tile's
@@ -2746,6 +2896,7 @@ __device__ __forceinline__ void modesum_tile(
         }                                                                                     \
     } while (0)
 
+    int gch = 0;        // chunks of the record list in earlier passes (the split's chunk order)
     int win = 0;        // next segment window
     int nhit = 0;       // overlapping segments of the current window
     int wtotal = 0;     // keys of the current window
@@ -2754,6 +2905,8 @@ __device__ __forceinline__ void modesum_tile(
     while (true) {
         // ---- fill keys[] (block-uniform control flow)
         while (pre < 0 && nkeys < KEYCAP) {
+            tid = opq(tid0);
+            lane = tid & 63;
             if (wdone == wtotal) {                 // need a new window of segments
                 if (win >= nseg) break;
                 // (1) overlap test + ordered compaction: every thread tests its SEGWIN/TILE
@@ -2875,16 +3028,24 @@ __device__ __forceinline__ void modesum_tile(
         const int cnt = nkeys;
         const int nchunk = (cnt + NC - 1) / NC;
         seen = true;
-        EFD_GLDS(0, 0);
+        tid = opq(tid0);
+        lane = tid & 63;
+        // this workgroup's chunks: every one (split_S = 1), or those with (gch + c) mod split_S
+        // = split_j; `it` counts them (the stage buffer of the it-th is it & 1)
+        const int c0 = ((split_j - gch) % split_S + split_S) % split_S;
+        gch += nchunk;
+        if (c0 < nchunk) EFD_GLDS(c0, 0);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's LDS-DMA pieces landed
         __syncthreads();
 
-        for (int c = 0; c < nchunk; ++c) {
-            // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
-            // barrier that closed it: its pieces for chunk c+1 stream in during the chunk
-            if (c + 1 < nchunk) EFD_GLDS(c + 1, (c + 1) & 1);
+        for (int c = c0, it_ = 0; c < nchunk; c += split_S, ++it_) {
+            tid = opq(tid0);
+            lane = tid & 63;
+            // buffer (it_+1)&1 was last read in the previous chunk, which every wave finished
+            // before the barrier that closed it: the next chunk's pieces stream in meanwhile
+            if (c + split_S < nchunk) EFD_GLDS(c + split_S, (it_ + 1) & 1);
             const int nin = (int)rfl((uint32_t)min(NC, cnt - c * NC));   // loop bound in an SGPR
-            const Item* stg = stage[c & 1];
+            const Item* stg = stage[it_ & 1];
             // the chunk's record headers, one lane per record, read from LDS once per chunk and
             // packed into one word: the sub-branch's lane range clamped to the tile, relative
             // to its first lane (HB bits each), s and the series length: hdr = lo | hi << HB |
@@ -2907,9 +3068,9 @@ __device__ __forceinline__ void modesum_tile(
             }
 #ifdef EFD_EXP
             int nev = 0;
-            if (c > 0 && tid == 0) {
+            if (it_ > 0 && tid == 0) {
                 int mx = 0, sm = 0;
-                for (int w = 0; w < NWAVE; ++w) { mx = max(mx, wimb[(c - 1) & 1][w]); sm += wimb[(c - 1) & 1][w]; }
+                for (int w = 0; w < NWAVE; ++w) { mx = max(mx, wimb[(it_ - 1) & 1][w]); sm += wimb[(it_ - 1) & 1][w]; }
                 atomicAdd(&g_exp_count[24], (unsigned long long)mx);
                 atomicAdd(&g_exp_count[25], (unsigned long long)sm);
                 atomicAdd(&g_exp_count[26], 1ull);
@@ -2968,7 +3129,7 @@ __device__ __forceinline__ void modesum_tile(
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t base = w_lo + 64 * i;
-                        spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], J,
+                        spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], ha,
                                             lane_range_mask(klo - base, khi - base), sctab, rs,
                                             wr[i], wi[i], w[i], needm[i]);
                         need[i] = __builtin_amdgcn_inverse_ballot_w64(needm[i]);
@@ -3011,14 +3172,29 @@ __device__ __forceinline__ void modesum_tile(
                         const uint32_t key = rfl(keys[c * NC + ii]);
                         const int hg = (int)((key >> 1) / (uint32_t)ni);
                         const int jr = (int)((key >> 1) - (uint32_t)hg * (uint32_t)ni);
+                        // the bins' g = -+f are reloaded from the grid around the calls (and
+                        // fk, tfk after them), so they are not live across the calls: the
+                        // caller-saved copies the kernel's prologue stored for every wave go
+                        const int ln = opq(tid0) & 63;
 #pragma unroll
                         for (int i = 0; i < BPL; ++i) {
                             if (need[i]) {
+                                const double f = freq[w_lo + 64 * i + ln];   // k < nlanes here
                                 const ColdEval ce = spa_general<CAUSTIC>(
-                                    it, fk[i], s, hg, jr, t, nt, K, gm, gn, coefA, coefT);
+                                    it, s_cur ? f : -f, s, hg, jr, t, nt, K, gm, gn, coefA, coefT);
                                 accumulate<0, PAIRED>(ce.wr, ce.wi, ce.b[0], ce.b[1], ce.b[2],
                                                       ce.b[3], own_r[i], own_i[i], mir_r[i],
                                                       mir_i[i]);
+                            }
+                        }
+                        {
+                            const int ln2 = opq(tid0) & 63;
+#pragma unroll
+                            for (int i = 0; i < BPL; ++i) {
+                                const int32_t k = w_lo + 64 * i + ln2;
+                                const double f = k < nlanes ? freq[k] : 0.0;
+                                fk[i] = s_cur ? f : -f;
+                                tfk[i] = TWO_PI * fk[i];
                             }
                         }
                         // the cold block's reloads retired here, so the loop head needs no
@@ -3028,7 +3204,7 @@ __device__ __forceinline__ void modesum_tile(
                 }
             }
 #ifdef EFD_EXP
-            if (lane == 0) wimb[c & 1][wave] = nev;
+            if (lane == 0) wimb[it_ & 1][wave] = nev;
 #endif
             // retire this wave's LDS-DMA pieces, then the barrier publishes chunk c+1's stage
             __builtin_amdgcn_s_waitcnt(0x0f70);
@@ -3038,6 +3214,59 @@ __device__ __forceinline__ void modesum_tile(
         if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
+    if (split_S > 1) {
+        // a split tile: this workgroup's partial sums of its bins (true signs) to its slot, then
+        // the arrival count (cdna_hip_programming.md's in-launch split-K reduction: plain stores
+        // -> every wave's vmcnt(0) -> barrier -> lane 0 agent release -> vmcnt(0) -> relaxed
+        // agent fetch_add; the last arriver: agent acquire -> vmcnt(0) -> barrier -> plain loads;
+        // correct for any placement of the splits over XCDs and CUs)
+        if (s_cur)
+#pragma unroll
+            for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
+        s_cur = 0;
+        const int lt = opq(tid0);
+        const int lw = lt >> 6, ll = lt & 63;
+        double2* slot = reinterpret_cast<double2*>(spart) + (size_t)split_j * TILE_LANES * 2;
+#pragma unroll
+        for (int i = 0; i < BPL; ++i) {
+            const int li = lw * 64 * BPL + 64 * i + ll;
+            slot[2 * li] = make_double2(own_r[i], own_i[i]);
+            slot[2 * li + 1] = make_double2(mir_r[i], mir_i[i]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lt == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int arrived = __hip_atomic_fetch_add(scnt, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            const int last = arrived == split_S - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // re-armed for a later sum on the same preparation (k_segments_one zeroes it too)
+                __hip_atomic_store(scnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            part[0] = last;   // "I am last", through an LDS array the tile already has
+        }
+        __syncthreads();
+        if (!part[0]) return;
+        // the last arriver: the split_S slots added in split order (deterministic whichever
+        // workgroup arrives last), then the tile's own epilogue below
+        const double2* s0 = reinterpret_cast<const double2*>(spart);
+#pragma unroll
+        for (int i = 0; i < BPL; ++i) {
+            const int li = lw * 64 * BPL + 64 * i + ll;
+            double2 a = s0[2 * li], m = s0[2 * li + 1];
+            for (int j = 1; j < split_S; ++j) {
+                const double2 a2 = s0[(size_t)j * TILE_LANES * 2 + 2 * li];
+                const double2 m2 = s0[(size_t)j * TILE_LANES * 2 + 2 * li + 1];
+                a.x += a2.x; a.y += a2.y; m.x += m2.x; m.y += m2.y;
+            }
+            own_r[i] = a.x; own_i[i] = a.y; mir_r[i] = m.x; mir_i[i] = m.y;
+        }
+        seen = true;
+    }
     if (PAIRED && llconst != nullptr && !seen && out == nullptr && hp == nullptr) {
         // no record reached this tile: h = 0 on its bins, whose likelihood partial is the
         // walker-independent one k_ll_tile_const computed with this epilogue's arithmetic
@@ -3051,6 +3280,8 @@ __device__ __forceinline__ void modesum_tile(
     // S is written when out != NULL; on a symmetric grid h+ and hx of bins [k0, nf) are written
     // straight from the registers when hp != NULL (the lane holds S(k) and S(nf-1-k), the two
     // halves of efd_polarizations' flip), so the likelihood path never stores S
+    tid = opq(tid0);
+    lane = tid & 63;
     double2* o = reinterpret_cast<double2*>(out);
     double2* php = reinterpret_cast<double2*>(hp);
     double2* phc = reinterpret_cast<double2*>(hc);
@@ -3265,6 +3496,26 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
     }
     const BatchDesc& d = batch.d[w];
     if constexpr (SPARSE) {
+        const int32_t nit = d.hdr->nitems;
+        if (nit > 0) {
+            // k_segments_one's split plan: items (tile, split j, S, partial slot, counter)
+            const Layout L = make_layout(d.nt, d.K, nf, 1);
+            char* W = reinterpret_cast<char*>(d.hdr);
+            const int4* items = ws_at<const int4>(W, L.sitem);
+            for (int64_t it = pos; it < nit; it += nper) {
+                const int4 e = items[it];
+                const int S = e.y & 0xffff, j = e.y >> 16;
+                modesum_tile<PAIRED, CAUSTIC, BPL>(
+                    d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles,
+                    d.nt, d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt,
+                    d.tperm, d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc,
+                    d.k0, lld, llw, d.llpart, llconst, e.x, true, j, S,
+                    S > 1 ? ws_at<double>(W, L.spart) + (size_t)e.z * TILE_LANES * 4 : nullptr,
+                    S > 1 ? ws_at<int32_t>(W, L.scnt) + e.w : nullptr);
+                __syncthreads();   // the next tile's LDS writes after every wave's last reads
+            }
+            return;
+        }
         const int32_t lo = d.hdr->lane_lo, hi = d.hdr->lane_hi;
         if (lo < hi) {
             const int64_t t1 = min((int64_t)(hi - 1) / TILE_LANES, ntiles - 1);
@@ -4786,9 +5037,14 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
     const int64_t gq = 8 * XCD_GROUP;
     int64_t nper = 0;
     if (sparse) {
-        // workgroups per waveform: a multiple of 8 (one XCD place each), ~SPARSE_WG in all
+        // workgroups per waveform: a multiple of 8 (one XCD place each), ~SPARSE_WG in all. With
+        // a possible split plan (K <= SEG1_MAX_K: k_segments_one; its item count is on the
+        // device) the whole share, so every item of a plan gets its own workgroup (those past
+        // the items exit at once)
         const int64_t cap = std::max<int64_t>(64, (SPARSE_WG / count + 7) / 8 * 8);
-        nper = std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
+        bool planned = true;
+        for (int i = 0; i < count; ++i) planned = planned && a[i]->K <= SEG1_MAX_K;
+        nper = planned ? cap : std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
     }
     const int64_t nblk = sparse ? nper * count : (L0.ntiles + gq - 1) / gq * gq * count;
     if (nblk > (int64_t)UINT32_MAX) return fail(EFD_ERR_ARG, F + ": grid too large");

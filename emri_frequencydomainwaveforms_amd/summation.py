@@ -185,6 +185,17 @@ class ModeSumEngine:
         self._ws_ptr = self._ws.data_ptr()
         return self._ws
 
+    def split_plan(self):
+        """(items, split tiles) of the sparse fused likelihood's split plan in this workspace's
+        header (k_segments_one; items = -1: no plan, the sum visits each union tile once).
+        Synchronises the device; for tests and tools."""
+        if self._ws is None:
+            return (-1, 0)
+        torch = _torch()
+        torch.cuda.synchronize(self._ws.device)
+        v = self._ws[48:56].cpu().numpy().view(np.int32)
+        return int(v[0]), int(v[1])
+
     def launch(self, inp, freq, out, grid_symmetric, scale=1.0 + 0.0j, accumulate=False,
                stream=None, prof_events=(None, None), hp=None, hc=None, k0=0, phase="all"):
         """Asynchronous launch; returns the workspace (check with `status`).

@@ -55,7 +55,7 @@ def ulp_perturbation(seed, ulps=PERTURB_ULPS):
     return lambda x: x * (1.0 + rng.choice([-1.0, 1.0], len(x)) * ulps * 2.0 ** -52)
 
 
-def split_check(S, R, Rps, rel=1e-9, dilate=8, E=None):
+def split_check(S, R, Rps, rel=1e-9, dilate=8, E=None, Rps1=None):
     """Per-bin parity of a spectrum S against the oracle's R.
 
     D_k = max over the perturbed oracle runs Rps (PERTURB_ULPS ulps of the trajectory arrays) of
@@ -69,7 +69,12 @@ def split_check(S, R, Rps, rel=1e-9, dilate=8, E=None):
     whose t(g) the splines extrapolate outside the trajectory (the inverse spline of a nearly
     flat run overshoots its times; scipy's CubicSpline, which the notebook uses, extrapolates).
     Their phase comes from cubics evaluated far outside their intervals, so two faithful
-    evaluations agree in magnitude only: those bins get + 2 E_k. Returns (ok, stats, tol[k])."""
+    evaluations agree in magnitude only: those bins get + 2 E_k. Returns (ok, stats, tol[k]).
+
+    Rps1 (optional): the oracle perturbed by ONE ulp instead. Not part of the pass rule; it adds
+    D1 (the same dilated response at 1 ulp) and err / D1 at the bins where D1 > rel max|R| to the
+    stats: how the kernel's fold error compares with the reference construction's own rounding
+    sensitivity."""
     from scipy.ndimage import maximum_filter1d
     mx = float(np.abs(R).max())
     D = np.zeros(len(R))
@@ -99,6 +104,22 @@ def split_check(S, R, Rps, rel=1e-9, dilate=8, E=None):
                           f"+-{dilate}-bin running max), + 2 E_k at the {int(ext.sum())} bins "
                           f"with extrapolated terms",
              "ok": ok}
+    # the tolerance a user can rely on, per bin class, relative to max|R|: off the folds the
+    # 1e-9 rule; at the folds the measured worst error (the bound there is 2 D_k)
+    stats["tol_rel_by_class"] = {"off_fold": rel,
+                                 "fold_measured_max": float(err[fold].max() / mx)
+                                 if fold.any() and mx > 0 else 0.0,
+                                 "fold_bound_max": float(2.0 * D.max() / mx) if mx > 0 else 0.0}
+    if Rps1:
+        D1 = np.zeros(len(R))
+        for Rp in Rps1:
+            D1 = np.maximum(D1, np.abs(Rp - R))
+        if dilate:
+            D1 = maximum_filter1d(D1, size=2 * dilate + 1, mode="nearest")
+        f1 = (D1 > rel * mx) & ~ext
+        stats["D1_fold_bins"] = int(f1.sum())
+        stats["max_err_over_D1_at_folds"] = float((err[f1] / D1[f1]).max()) if f1.any() else 0.0
+        stats["D1_max_rel"] = float(D1.max() / mx) if mx > 0 else 0.0
     if not ok:
         k = int(np.argmax(err - tol))
         stats["worst_bin"] = {"k": k, "err_rel": float(err[k] / mx), "tol_rel": float(tol[k] / mx),

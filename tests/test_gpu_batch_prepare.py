@@ -250,7 +250,12 @@ def test_fused_loglike_tile_constants_bitwise(sources, dt):
     torch.cuda.synchronize()
     B.wait()
     assert torch.all(torch.isfinite(ref)) and torch.all(ref < 0)
-    assert torch.equal(got, ref) and torch.equal(got2, ref)
+    # bitwise, except for a walker whose heavy tiles the sparse form splits (k_segments_one's
+    # plan: the split tiles add their partial sums in split order, another rounding)
+    split = torch.tensor([eng.split_plan()[1] > 0 for eng, _ in jobs], device="cuda")
+    for g in (got, got2):
+        assert torch.equal(g[~split], ref[~split])
+        assert torch.allclose(g[split], ref[split], rtol=1e-13, atol=0.0)
     # the constants alone sum to a zero template's sum |d - 0 w|^2 over every bin (to rounding:
     # another summation order)
     h0 = float((torch.abs(d) ** 2).sum())
@@ -292,3 +297,47 @@ def test_fused_loglike_tile_constants_no_segment(sources):
     assert torch.equal(got, ref)
     h0 = -2.0 * float((torch.abs(d) ** 2).sum())
     assert np.allclose(ref.cpu().numpy(), h0, rtol=1e-12, atol=0.0)
+
+
+def test_fused_loglike_split_tiles():
+    """The sparse fused likelihood's split plan (k_segments_one: a tile above the waveform's fair
+    share of the chip is evaluated by S workgroups, each writing its bins' partial sums; the last
+    arriver adds them in split order and runs the tile's epilogue) on config 5's shape: a coarse
+    downsampled grid where a few low-frequency tiles hold most records. The plan must be made
+    (split tiles > 0), the logL must equal the unsplit dense launch's to 1e-13 (summation order
+    only), repeat bitwise, and a second sum on the same preparation (the arrival counters re-armed
+    by the last arrivers) must give bitwise the same values."""
+    from emri_frequencydomainwaveforms_amd.summation import loglike_tile_constants
+    srcs = [source_inputs(M=M, e0=e0, T=0.5, dt=10.0, eps=1e-2)
+            for M, e0 in ((1e6, 0.35), (8e5, 0.3), (1.2e6, 0.4), (9e5, 0.25))]
+    fmax = max(float(np.abs(s["m"] * s["f_phi"][:, None] + s["n"] * s["f_r"][:, None]).max())
+               for s in srcs)
+    p = np.linspace(0.0, 1.01 * fmax, 4001)          # emri_pe.py's downsampled grid shape
+    freq_h = np.concatenate([-p[::-1][:-1], p])
+    freq = torch.as_tensor(freq_h, device="cuda")
+    nf = int(freq.numel())
+    k0 = nf // 2
+    nb = nf - k0
+    rng = np.random.default_rng(3)
+    d = torch.as_tensor(rng.standard_normal((2, nb)) + 1j * rng.standard_normal((2, nb)),
+                        device="cuda") * 1e-21
+    w = torch.as_tensor(rng.uniform(0.5, 2.0, (2, nb)) * 1e20, device="cuda")
+    tc = loglike_tile_constants(d, w, nf, k0)
+    B = BatchPreparer(group=len(srcs), depth=1)
+    for src in srcs:
+        B.submit(_host(src), freq, True, src["prefactor"], k0=k0, prepare_only=True)
+    gi, jobs = B.flush()
+    cur = torch.cuda.current_stream()
+    cur.wait_stream(B.stream(gi))
+    ref = torch.empty(len(srcs), dtype=torch.float64, device="cuda")
+    got = [torch.empty_like(ref) for _ in range(3)]
+    B.sum_loglike(gi, d, w, ref, cur.cuda_stream)                       # dense: no plan used
+    for g in got:
+        B.sum_loglike(gi, d, w, g, cur.cuda_stream, tile_const=tc)     # sparse, split tiles
+    torch.cuda.synchronize()
+    B.wait()
+    plans = [eng.split_plan() for eng, _ in jobs]
+    assert any(ns > 0 for _, ns in plans), plans
+    assert torch.all(torch.isfinite(ref))
+    assert torch.allclose(got[0], ref, rtol=1e-13, atol=0.0), (got[0] - ref) / ref
+    assert torch.equal(got[1], got[0]) and torch.equal(got[2], got[0])

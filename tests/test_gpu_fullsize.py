@@ -75,7 +75,16 @@ def test_config2_full_spectrum_vs_c_oracle(cfg2, oracle2):
                                        w["m"], w["n"], w["ylm_p"],
                                        w["ylm_m"], w["freq"], w["prefactor"], caustic="uniform",
                                        nthreads=threads))
-    ok, stats, _ = split_check(S, R, Rps, E=E)
+    # the same oracle at ONE ulp (two seeds): reported beside the 4-ulp rule, not part of it
+    Rps1 = []
+    for seed in (17, 18):
+        pert = ulp_perturbation(seed, ulps=1)
+        Rps1.append(fd_oracle_c.modesum(pert(w["t"]), w["amp"].T, pert(w["phi_phi"]),
+                                        pert(w["phi_r"]), pert(w["f_phi"]), pert(w["f_r"]),
+                                        w["m"], w["n"], w["ylm_p"],
+                                        w["ylm_m"], w["freq"], w["prefactor"], caustic="uniform",
+                                        nthreads=threads))
+    ok, stats, _ = split_check(S, R, Rps, E=E, Rps1=Rps1)
     record_parity("config2", dict(stats, contributions=C, evaluations=n_eval, groups=groups))
     if not ok and os.environ.get("EFD_PARITY_OUT"):   # the neighbourhood of the worst bin
         k = stats["worst_bin"]["k"]

@@ -1,6 +1,6 @@
 """Kernel experiments: build libemrifd.so variants here (CPU), time them on the GPU box.
 
-    python tools/exp_variants.py build NAME[:-DFLAG[=V][,-DFLAG2...]] ...   # here, hipcc only
+    python tools/exp_variants.py build NAME[=SRC][:-DFLAG[=V][,-DFLAG2...]] ...   # here, hipcc only
     python tools/exp_variants.py run NAME ...                              # on the GPU box
 
 `build` writes exp/libemrifd_<NAME>.so (git-ignored, travels with gpurun). `run` loads each
@@ -40,8 +40,10 @@ def build(specs):
     procs = []
     for spec in specs:
         name, _, flags = spec.partition(":")
+        # NAME=SOURCE: another kernel source (e.g. an earlier revision saved under exp/)
+        name, _, src = name.partition("=")
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               *[f for f in flags.split(",") if f], "-o", lib_path(name), *objs, SRC,
+               *[f for f in flags.split(",") if f], "-o", lib_path(name), *objs, src or SRC,
                "-lgomp", "-lmvec"]
         print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
