@@ -245,7 +245,9 @@ __host__ __device__ inline Layout make_layout(int32_t nt, int32_t K, int64_t nf,
     L.llpart = take(sizeof(double) * (size_t)L.ntiles);   // fused likelihood: per-tile partials
     // the sparse sum's split plan (k_segments_one, K <= SEG1_MAX_K only): items, one arrival
     // counter per split tile, the partial sums of the splits ([slot][lane][4] doubles)
-    const bool plan = K <= SEG1_MAX_K && paired;
+    // (in both layouts: efd_modesum_workspace_bytes sizes by the unpaired one, which must stay
+    // the larger)
+    const bool plan = K <= SEG1_MAX_K;
     L.sitem = take(plan ? sizeof(int4) * SPLIT_ITEM_CAP : 0);
     L.scnt = take(plan ? sizeof(int32_t) * SPLIT_TILE_CAP : 0);
     L.spart = take(plan ? sizeof(double) * 4 * (size_t)SPLIT_SLOT_CAP * TILE_LANES : 0);
@@ -2501,6 +2503,10 @@ __device__ __forceinline__ bool hdr_j3(uint32_t ha) {   // the record's series l
     asm volatile("" : "+s"(ha));
     return ((ha >> HDR_J) & 7u) >= 3u;
 }
+__device__ __forceinline__ bool hdr_j4(uint32_t ha) {   // J >= 4
+    asm volatile("" : "+s"(ha));
+    return ((ha >> HDR_J) & 7u) >= 4u;
+}
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            uint32_t ha, uint64_t actm,
@@ -2540,6 +2546,19 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         const double t3 = fdds * a3;
         double ww = t3 * t3;   // 1/|y|
         double am, c0, thn;
+#ifdef EFD_EXP_J3
+        if (hdr_j3(ha) && !hdr_j4(ha)) {   // J = 3 (16% of records): every in-interval lane
+            // is inside the series' range (|y| >= 555: v <= VS / 555 = 3.4e-4), so no range test
+            // or second mask; rho = 1 - v^2 (its 45.7 v^4 term < 5.8e-13) multiplies the
+            // amplitude (folded into the cosine's constant, as for J <= 2, it would leave
+            // |rho - 1| |sr| <= 7e-10 of a term), theta's KTHN_1 term stays (2e-10 rad)
+            asm volatile("");
+            const double uu = ww * ww;
+            thn = ww * fma(-14.733333333333333333, uu, 1.0);
+            am = ampm * (1.0 - uu);
+            c0 = COS_A;
+        } else
+#endif
         if (hdr_j3(ha)) {   // J >= 3: wave-uniform; a real branch (see KTH0's notes)
             asm volatile("");
             // the |y| >= FAST_Y test only matters for J = 4 (J = 3 lanes pass it by their
@@ -3129,8 +3148,16 @@ __device__ __forceinline__ void modesum_tile(
 #pragma unroll
                     for (int i = 0; i < BPL; ++i) {
                         const int32_t base = w_lo + 64 * i;
-                        spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], ha,
-                                            lane_range_mask(klo - base, khi - base), sctab, rs,
+#ifdef EFD_EXP_FULLMASK
+                        // a record covering the wave's whole 64 BPL-lane chunk needs no lane
+                        // masks (a wave-uniform branch around their SALU work)
+                        uint64_t am = ~0ull;
+                        if (hdr_test((uint32_t)((w_lo - klo) | (khi - w_hi)), 0x80000000u))
+                            am = lane_range_mask(klo - base, khi - base);
+#else
+                        const uint64_t am = lane_range_mask(klo - base, khi - base);
+#endif
+                        spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], ha, am, sctab, rs,
                                             wr[i], wi[i], w[i], needm[i]);
                         need[i] = __builtin_amdgcn_inverse_ballot_w64(needm[i]);
                         needany |= needm[i];
