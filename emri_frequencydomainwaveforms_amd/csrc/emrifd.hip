@@ -4993,6 +4993,15 @@ int efd_modesum_sum(const efd_modesum_args* a, void* workspace, size_t workspace
 // efd_modesum_sum_batch, and efd_modesum_sum_loglike when d != NULL (paired grids: the tiles
 // write their likelihood partials, k_ll_final turns each waveform's into out[i])
 constexpr int64_t SPARSE_WG = 4096;   // workgroups of a sparse launch, all waveforms
+// (EFD_SPARSE_WG overrides it: an experiment switch for paired A/B runs, read once)
+static int64_t sparse_wg() {
+    static const int64_t v = [] {
+        const char* e = getenv("EFD_SPARSE_WG");
+        const long long x = e ? atoll(e) : 0;
+        return x >= 64 && x <= (1 << 20) ? (int64_t)x : SPARSE_WG;
+    }();
+    return v;
+}
 int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const* workspace,
                    const size_t* workspace_bytes, int32_t count, const double* d, const double* w,
                    double* llout, void* stream, const double* llconst = nullptr) {
@@ -5068,7 +5077,7 @@ int sum_batch_impl(const char* fn, const efd_modesum_args* const* a, void* const
         // a possible split plan (K <= SEG1_MAX_K: k_segments_one; its item count is on the
         // device) the whole share, so every item of a plan gets its own workgroup (those past
         // the items exit at once)
-        const int64_t cap = std::max<int64_t>(64, (SPARSE_WG / count + 7) / 8 * 8);
+        const int64_t cap = std::max<int64_t>(64, (sparse_wg() / count + 7) / 8 * 8);
         bool planned = true;
         for (int i = 0; i < count; ++i) planned = planned && a[i]->K <= SEG1_MAX_K;
         nper = planned ? cap : std::min<int64_t>((L0.ntiles + 7) / 8 * 8, cap);
