@@ -82,14 +82,15 @@ constexpr int SEGWIN = TILE;        // segments examined per window (tile list b
 constexpr int MAX_K = 8192;         // harmonics per call
 // Split tiles of the sparse fused likelihood (K <= SEG1_MAX_K: k_segments_one plans them). A
 // tile whose estimated cost (wave-records: records x the 192-lane wave chunks each reaches)
-// exceeds the waveform's fair share of the chip is evaluated by S workgroups, each taking every
-// S-th chunk of the tile's record list and writing its bins' partial sums; the last of the S
-// (agent-scope release / acquire, counter per tile) adds them in split order and runs the tile's
-// epilogue. Items: the work units of the sparse launch, (tile, split j, S, partial slot).
+// exceeds the waveform's fair share of the chip is evaluated by BPL workgroups, workgroup j
+// taking bin j of every lane over the tile's whole record list (the sub-bin form of
+// modesum_tile: each bin's sum in the whole tile's order, so the result is bitwise unsplit);
+// the last of them (agent-scope release / acquire, counter per tile) runs the tile's epilogue
+// from the bins they stored. A split across the record list instead (every S-th chunk, partial
+// sums added by the last) reordered each bin's sum: the injection's logL became -6e-33, not 0.
+// Items: the work units of the sparse launch, (tile, bin j, S, slot).
 constexpr int SPLIT_ITEM_CAP = 8192;   // items per waveform (union tiles + extra splits)
-constexpr int SPLIT_TILE_CAP = 128;    // split tiles per waveform
-constexpr int SPLIT_SLOT_CAP = 128;    // partial slots (sum of S over split tiles)
-constexpr int SPLIT_MAX = 16;          // workgroups per split tile
+constexpr int SPLIT_TILE_CAP = 128;    // split tiles per waveform (one slot and counter each)
 constexpr int SPLIT_UNION_CAP = 4096;  // union tiles k_segments_one can cost (else no plan)
 constexpr int SPLIT_MIN_COST = 48;     // wave-records: tiles below this are never split
 constexpr int SPLIT_SLOTS_PER_WF = 64; // the fair share: a waveform's cost / this many workgroups
@@ -250,7 +251,7 @@ __host__ __device__ inline Layout make_layout(int32_t nt, int32_t K, int64_t nf,
     const bool plan = K <= SEG1_MAX_K;
     L.sitem = take(plan ? sizeof(int4) * SPLIT_ITEM_CAP : 0);
     L.scnt = take(plan ? sizeof(int32_t) * SPLIT_TILE_CAP : 0);
-    L.spart = take(plan ? sizeof(double) * 4 * (size_t)SPLIT_SLOT_CAP * TILE_LANES : 0);
+    L.spart = take(plan ? sizeof(double) * 4 * (size_t)SPLIT_TILE_CAP * TILE_LANES : 0);
     L.total = off;
     return L;
 }
@@ -276,6 +277,7 @@ struct PrepBatch {
     int32_t paired, n;
     int32_t pcr_groups;   // k_prep_pcr_b groups the harmonics itself (k_group_b not launched)
     int32_t seg_lds;      // k_segments_one's dynamic LDS bytes for the ranges table (0: none)
+    int32_t split_min;    // k_segments_one: tiles costing at most this (wave-records) stay whole
 };
 static_assert(sizeof(PrepBatch) <= 3072, "kernel arguments stay well inside 4 KB");
 
@@ -2112,38 +2114,32 @@ __global__ __launch_bounds__(SEG1_NT) void k_segments_one(const PrepBatch B) {
     int64_t total = 0;
     for (int w = 0; w < NW; ++w) total += s_csum[w];
     // the fair share of one workgroup: the waveform's cost over SPLIT_SLOTS_PER_WF workgroups
-    // (a walker group of 16 then fills the chip's ~1,024 resident slots); a tile above it is
-    // split into ceil(cost / share) (<= SPLIT_MAX) workgroups
-    const int64_t share = max((int64_t)SPLIT_MIN_COST, total / SPLIT_SLOTS_PER_WF);
+    // (a walker group of 16 then fills the chip's ~1,024 resident slots); a tile above it (and
+    // above B.split_min) is split into its BPL bins
+    const int64_t share = max((int64_t)B.split_min, total / SPLIT_SLOTS_PER_WF);
     int nS[PER];
-    int my_items = 0, my_slots = 0, my_split = 0;
+    int my_items = 0, my_split = 0;
     for (int i = 0; i < PER; ++i) {
         const int u = tid * PER + i;
-        int S = 1;
-        if (u < nut && s_cost[u] > share)
-            S = (int)min((int64_t)SPLIT_MAX, (s_cost[u] + share - 1) / share);
+        const int S = (u < nut && s_cost[u] > share) ? BPL : 1;
         nS[i] = u < nut ? S : 0;
         my_items += nS[i];
-        my_slots += S > 1 ? S : 0;
         my_split += S > 1 ? 1 : 0;
     }
-    int n_items, n_slots, n_split;
+    int n_items, n_split;
     const int io = seg1_excl_scan(my_items, wsum, n_items);
-    const int so = seg1_excl_scan(my_slots, wsum, n_slots);
     const int po = seg1_excl_scan(my_split, wsum, n_split);
-    if (n_split == 0 || n_items > SPLIT_ITEM_CAP || n_slots > SPLIT_SLOT_CAP ||
-        n_split > SPLIT_TILE_CAP)
+    if (n_split == 0 || n_items > SPLIT_ITEM_CAP || n_split > SPLIT_TILE_CAP)
         return;   // nothing to split, or past the plan's capacity: the plain tile loop
     int4* items = ws_at<int4>(W, L.sitem);
     int32_t* cnt = ws_at<int32_t>(W, L.scnt);
-    int ii = io, sl = so, sp = po;
+    int ii = io, sp = po;
     for (int i = 0; i < PER; ++i) {
         const int u = tid * PER + i, S = nS[i];
         for (int j = 0; j < S; ++j)
-            items[ii + j] = make_int4(ut0 + u, (j << 16) | S, S > 1 ? sl : -1, S > 1 ? sp : -1);
+            items[ii + j] = make_int4(ut0 + u, (j << 16) | S, S > 1 ? sp : -1, S > 1 ? sp : -1);
         if (S > 1) {
             cnt[sp] = 0;
-            sl += S;
             ++sp;
         }
         ii += S;
@@ -2507,6 +2503,31 @@ __device__ __forceinline__ bool hdr_j4(uint32_t ha) {   // J >= 4
     asm volatile("" : "+s"(ha));
     return ((ha >> HDR_J) & 7u) >= 4u;
 }
+#ifdef EFD_EXP_FASTPATH
+// The common record class on its own straight-line body (EFD_EXP_FASTPATH): certified safe,
+// series length J <= 2 and covering the wave's whole 64 BPL-lane chunk (every lane evaluates,
+// every lane passes the interval and sign tests), so no lane mask, no amplitude select and no
+// series branch: spa_fast_m's J <= 2 arithmetic, bitwise the same values.
+__device__ __forceinline__ void spa_simple(const Item* __restrict__ it, double sfk, double stfk,
+                                           const double2* __restrict__ sct, const RecSign& rs,
+                                           double& wr, double& wi, double& w) {
+    const double u = sfk - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    w = tt - it->tj;
+    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+    const double amp = rsqrt_pos_sum(fabs(fd));
+    const double psi0 = fma(stfk, tt, -ph);
+    const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+    const double a3 = amp * amp * amp;
+    const double t3 = fdds * a3;
+    const double ww = t3 * t3;
+    double sn, cs;
+    sincos_tab(psi0, rs.shift, sct, sn, cs, ww, true, rs.kth, fma(-ww, ww, COS_A));
+    wr = amp * cs;
+    wi = amp * sn;
+}
+#endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            uint32_t ha, uint64_t actm,
@@ -2736,7 +2757,33 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst) {
 // term in a cold block. The sub-branch S of a record is wave-uniform: each S has its own copy of
 // the evaluation (compile-time signs and LDS offsets).
 // ----------------------------------------------------------------------------------------
-template <bool PAIRED, int CAUSTIC, int BPL>
+// The tile's LDS, one object for every instantiation a kernel inlines (a kernel holding both the
+// whole-tile and the sub-bin form of modesum_tile allocates it once, not twice)
+struct TileLds {
+    uint32_t keys[KEYCAP];
+    Item stage[2][NC];
+    int part[TILE];
+    int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
+    int wcnt[(SEGWIN / TILE) * NWAVE];
+    double2 sctab[SCTAB];   // (sin, cos)(k pi/128) for sincos_tab
+#ifdef EFD_EXP
+    int wimb[2][NWAVE];     // records each wave evaluated in a chunk (barrier balance)
+#endif
+};
+__device__ __forceinline__ TileLds& tile_lds() {
+    __shared__ TileLds lds;
+    return lds;
+}
+
+template <bool PAIRED>
+__device__ __forceinline__ void tile_epilogue(
+    double (&own_r)[BPL], double (&own_i)[BPL], double (&mir_r)[BPL], double (&mir_i)[BPL],
+    int32_t w_lo, int lane, int wave, int tid, int64_t nlanes, int64_t nf, int64_t k0,
+    int accumulate_out, double* __restrict__ out, double* __restrict__ hp,
+    double* __restrict__ hc, const double* __restrict__ lld, const double* __restrict__ llw,
+    double* __restrict__ llpart, int64_t tile);
+
+template <bool PAIRED, int CAUSTIC, int NB = BPL>
 // 4 waves per SIMD (<= 128 VGPRs, 19 spilled, all outside the fast path's FMA chains): with
 // 37.6 KB of LDS per workgroup 4 workgroups fit a CU, and the fourth wave hides more FP64
 // latency than the spills cost (config 2: 1.00 ms against 1.09 ms at 3 waves / 147 VGPRs;
@@ -2767,21 +2814,27 @@ __device__ __forceinline__ void modesum_tile(
     const double* __restrict__ llconst,
     int64_t b,     // b: this workgroup's place in the waveform's dispatch order
     bool direct = false,     // b is the tile itself (k_modesum_batch's sparse form)
-    // a split tile (k_segments_one's plan; sparse form): this workgroup evaluates the chunks g of
-    // the tile's record list with g mod split_S = split_j, writes its bins' partial sums to slot
-    // spart + split_j, and the last of the split_S workgroups (arrival counter *scnt) adds the
-    // slots in order and runs the epilogue. split_S = 1: the whole tile
-    int split_j = 0, int split_S = 1, double* __restrict__ spart = nullptr,
-    int32_t* __restrict__ scnt = nullptr) {
-    __shared__ uint32_t keys[KEYCAP];
-    __shared__ Item stage[2][NC];
-    __shared__ int part[TILE];
-    __shared__ int hits[SEGWIN], hp0[SEGWIN], hcnt[SEGWIN], hoff[SEGWIN];
-    __shared__ int wcnt[(SEGWIN / TILE) * NWAVE];
-    __shared__ double2 sctab[SCTAB];   // (sin, cos)(k pi/128) for sincos_tab
+    // NB < BPL: a split tile (k_segments_one's plan; sparse form), the sub-bin form. This
+    // workgroup evaluates bins ioff .. ioff + NB - 1 of every lane (all of the tile's records, in
+    // the whole tile's order, so each bin's sum is bitwise the whole tile's), stores them in the
+    // tile's slot spart, and the last of the BPL / NB workgroups (arrival counter *scnt) loads
+    // the slot and runs the epilogue
+    int ioff = 0, double* __restrict__ spart = nullptr, int32_t* __restrict__ scnt = nullptr) {
+    static_assert(NB == BPL || NB == 1, "sub-bin form: one bin per lane");
+    TileLds& L_ = tile_lds();
+    uint32_t* const keys = L_.keys;
+    Item (*const stage)[NC] = L_.stage;
+    int* const part = L_.part;
+    int* const hits = L_.hits;
+    int* const hp0 = L_.hp0;
+    int* const hcnt = L_.hcnt;
+    int* const hoff = L_.hoff;
+    int* const wcnt = L_.wcnt;
+    double2* const sctab = L_.sctab;
 #ifdef EFD_EXP
-    __shared__ int wimb[2][NWAVE];     // records each wave evaluated in a chunk (barrier balance)
+    int (*const wimb)[NWAVE] = L_.wimb;
 #endif
+    if (NB == BPL) ioff = 0;
     // Tile order. Blocks are dealt round-robin over the 8 XCDs; XCD x = b % 8 here gets groups
     // of XCD_GROUP consecutive tiles (neighbouring tiles share interval records, which then hit
     // in that XCD's L2) interleaved with the other XCDs' groups, so every XCD sees the same mix
@@ -2871,12 +2924,14 @@ __device__ __forceinline__ void modesum_tile(
     // keys[] until KEYCAP, then the chunked evaluation below drains them. The summation order
     // (segment, then lane order) is fixed, so the result is bitwise reproducible.
     const int32_t w_lo = (int32_t)(tile * TILE_LANES + wave * 64 * BPL);
-    const int32_t w_hi = w_lo + 64 * BPL;
-    double fk[BPL], tfk[BPL];
-    double own_r[BPL], own_i[BPL], mir_r[BPL], mir_i[BPL];
+    // the bins this workgroup evaluates in the wave's chunk: [e_lo, e_hi), NB per lane
+    const int32_t e_lo = w_lo + 64 * ioff;
+    const int32_t e_hi = e_lo + 64 * NB;
+    double fk[NB], tfk[NB];
+    double own_r[NB], own_i[NB], mir_r[NB], mir_i[NB];
 #pragma unroll
-    for (int i = 0; i < BPL; ++i) {
-        const int32_t k = w_lo + 64 * i + lane;
+    for (int i = 0; i < NB; ++i) {
+        const int32_t k = e_lo + 64 * i + lane;
         fk[i] = (anyrec && k < nlanes) ? freq[k] : 0.0;
         tfk[i] = TWO_PI * fk[i];
         own_r[i] = own_i[i] = mir_r[i] = mir_i[i] = 0.0;
@@ -2888,7 +2943,7 @@ __device__ __forceinline__ void modesum_tile(
     // round-to-nearest, so the sums are bitwise those of the signed-copy form.
     int s_cur = 0;
 #pragma unroll
-    for (int i = 0; i < BPL; ++i) { fk[i] = -fk[i]; tfk[i] = -tfk[i]; }   // s = 0: g = -f
+    for (int i = 0; i < NB; ++i) { fk[i] = -fk[i]; tfk[i] = -tfk[i]; }   // s = 0: g = -f
 
     // staging: a record is PIECES pieces of 16 B; NC records take at most ROUNDS pieces per thread.
     // The pieces go global -> LDS directly (gfx950 global_load_lds_dwordx4: no VGPR staging,
@@ -2915,7 +2970,6 @@ __device__ __forceinline__ void modesum_tile(
         }                                                                                     \
     } while (0)
 
-    int gch = 0;        // chunks of the record list in earlier passes (the split's chunk order)
     int win = 0;        // next segment window
     int nhit = 0;       // overlapping segments of the current window
     int wtotal = 0;     // keys of the current window
@@ -3049,22 +3103,18 @@ __device__ __forceinline__ void modesum_tile(
         seen = true;
         tid = opq(tid0);
         lane = tid & 63;
-        // this workgroup's chunks: every one (split_S = 1), or those with (gch + c) mod split_S
-        // = split_j; `it` counts them (the stage buffer of the it-th is it & 1)
-        const int c0 = ((split_j - gch) % split_S + split_S) % split_S;
-        gch += nchunk;
-        if (c0 < nchunk) EFD_GLDS(c0, 0);
+        EFD_GLDS(0, 0);
         __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): this wave's LDS-DMA pieces landed
         __syncthreads();
 
-        for (int c = c0, it_ = 0; c < nchunk; c += split_S, ++it_) {
+        for (int c = 0; c < nchunk; ++c) {
             tid = opq(tid0);
             lane = tid & 63;
-            // buffer (it_+1)&1 was last read in the previous chunk, which every wave finished
-            // before the barrier that closed it: the next chunk's pieces stream in meanwhile
-            if (c + split_S < nchunk) EFD_GLDS(c + split_S, (it_ + 1) & 1);
+            // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the
+            // barrier that closed it: chunk c+1's pieces stream in meanwhile
+            if (c + 1 < nchunk) EFD_GLDS(c + 1, (c + 1) & 1);
             const int nin = (int)rfl((uint32_t)min(NC, cnt - c * NC));   // loop bound in an SGPR
-            const Item* stg = stage[it_ & 1];
+            const Item* stg = stage[c & 1];
             // the chunk's record headers, one lane per record, read from LDS once per chunk and
             // packed into one word: the sub-branch's lane range clamped to the tile, relative
             // to its first lane (HB bits each), s and the series length: hdr = lo | hi << HB |
@@ -3087,9 +3137,9 @@ __device__ __forceinline__ void modesum_tile(
             }
 #ifdef EFD_EXP
             int nev = 0;
-            if (it_ > 0 && tid == 0) {
+            if (c > 0 && tid == 0) {
                 int mx = 0, sm = 0;
-                for (int w = 0; w < NWAVE; ++w) { mx = max(mx, wimb[(it_ - 1) & 1][w]); sm += wimb[(it_ - 1) & 1][w]; }
+                for (int w = 0; w < NWAVE; ++w) { mx = max(mx, wimb[(c - 1) & 1][w]); sm += wimb[(c - 1) & 1][w]; }
                 atomicAdd(&g_exp_count[24], (unsigned long long)mx);
                 atomicAdd(&g_exp_count[25], (unsigned long long)sm);
                 atomicAdd(&g_exp_count[26], 1ull);
@@ -3101,7 +3151,7 @@ __device__ __forceinline__ void modesum_tile(
                 const int32_t klo = tlo + (int32_t)(ha & HM);
                 const int32_t khi = tlo + (int32_t)((ha >> HB) & HM);
                 const Item* it = stg + ii;
-                if (khi <= w_lo || klo >= w_hi) {              // misses this wave's chunk
+                if (khi <= e_lo || klo >= e_hi) {              // misses this wave's bins
 #ifdef EFD_EXP
                     if (lane == 0) atomicAdd(&g_exp_count[3], 1ull);
 #endif
@@ -3115,7 +3165,7 @@ __device__ __forceinline__ void modesum_tile(
                 }
 #endif
                 bool anyneed = false;
-                bool need[BPL];
+                bool need[NB];
                 {
                     // one body: sub-branch sign (the register state above) and series length as
                     // wave-uniform values
@@ -3127,7 +3177,7 @@ __device__ __forceinline__ void modesum_tile(
 #endif
                     if (s != s_cur) {
 #pragma unroll
-                        for (int i = 0; i < BPL; ++i) {
+                        for (int i = 0; i < NB; ++i) {
                             fk[i] = -fk[i];
                             tfk[i] = -tfk[i];
                             own_i[i] = -own_i[i];
@@ -3139,20 +3189,35 @@ __device__ __forceinline__ void modesum_tile(
                     // the stage holds b[s] at b[0] (EFD_GLDS swaps the halves for s = 1)
                     const double* xo = &it->b[0][0][0];
                     const double* xm = &it->b[1][0][0];
-                    double wr[BPL], wi[BPL], w[BPL];
-                    uint64_t needm[BPL], needany = 0;
+                    double wr[NB], wi[NB], w[NB];
+                    uint64_t needm[NB], needany = 0;
                     const RecSign rs = rec_sign((ha >> (2 * HB + 4)) & 3u);
 #ifdef EFD_EXP   // [29]: wave-records of certified-safe records
                     if (lane == 0 && rs.safe) atomicAdd(&g_exp_count[29], 1ull);
 #endif
+#ifdef EFD_EXP_FASTPATH
+                    // certified safe, J <= 2 and covering the whole chunk: the straight-line
+                    // evaluation (no lane masks, amplitude selects or series branch); the
+                    // amplitude cubics and accumulation below are shared
+                    if (CAUSTIC == EFD_CAUSTIC_UNIFORM &&
+                        !hdr_test(((uint32_t)((e_lo - klo) | (khi - e_hi)) >> 31) |
+                                  ((((ha >> HDR_J) & 7u) + 5u) >> 3) |
+                                  (((ha >> (HDR_FD + 1)) & 1u) ^ 1u), 1u)) {
 #pragma unroll
-                    for (int i = 0; i < BPL; ++i) {
-                        const int32_t base = w_lo + 64 * i;
+                        for (int i = 0; i < NB; ++i) {
+                            spa_simple(it, fk[i], tfk[i], sctab, rs, wr[i], wi[i], w[i]);
+                            need[i] = false;
+                        }
+                    } else
+#endif
+#pragma unroll
+                    for (int i = 0; i < NB; ++i) {
+                        const int32_t base = e_lo + 64 * i;
 #ifdef EFD_EXP_FULLMASK
                         // a record covering the wave's whole 64 BPL-lane chunk needs no lane
                         // masks (a wave-uniform branch around their SALU work)
                         uint64_t am = ~0ull;
-                        if (hdr_test((uint32_t)((w_lo - klo) | (khi - w_hi)), 0x80000000u))
+                        if (hdr_test((uint32_t)((e_lo - klo) | (khi - e_hi)), 0x80000000u))
                             am = lane_range_mask(klo - base, khi - base);
 #else
                         const uint64_t am = lane_range_mask(klo - base, khi - base);
@@ -3166,7 +3231,7 @@ __device__ __forceinline__ void modesum_tile(
                     // the own bins' amplitude cubics (b[0], 16 VGPRs) first, then the mirrors'
                     // (b[1], read after a compiler fence so they can reuse the registers)
 #pragma unroll
-                    for (int i = 0; i < BPL; ++i) {
+                    for (int i = 0; i < NB; ++i) {
                         const double xr = cubic(xo, w[i]), xi = cubic(xo + 4, w[i]);
                         own_r[i] = fma(xr, wr[i], own_r[i]);
                         own_r[i] = fma(-xi, wi[i], own_r[i]);
@@ -3176,7 +3241,7 @@ __device__ __forceinline__ void modesum_tile(
                     if (PAIRED) {
                         asm volatile("" ::: "memory");
 #pragma unroll
-                        for (int i = 0; i < BPL; ++i) {
+                        for (int i = 0; i < NB; ++i) {
                             const double zr = cubic(xm, w[i]), zi = cubic(xm + 4, w[i]);
                             mir_r[i] = fma(zr, wr[i], mir_r[i]);
                             mir_r[i] = fma(-zi, wi[i], mir_r[i]);
@@ -3189,7 +3254,7 @@ __device__ __forceinline__ void modesum_tile(
                         {
                             unsigned long long nl_ = 0;
 #pragma unroll
-                            for (int i = 0; i < BPL; ++i) nl_ += __popcll(__ballot(need[i]));
+                            for (int i = 0; i < NB; ++i) nl_ += __popcll(__ballot(need[i]));
                             if (lane == 0) {
                                 atomicAdd(&g_exp_count[16], 1ull);
                                 atomicAdd(&g_exp_count[17], nl_);
@@ -3204,9 +3269,9 @@ __device__ __forceinline__ void modesum_tile(
                         // caller-saved copies the kernel's prologue stored for every wave go
                         const int ln = opq(tid0) & 63;
 #pragma unroll
-                        for (int i = 0; i < BPL; ++i) {
+                        for (int i = 0; i < NB; ++i) {
                             if (need[i]) {
-                                const double f = freq[w_lo + 64 * i + ln];   // k < nlanes here
+                                const double f = freq[e_lo + 64 * i + ln];   // k < nlanes here
                                 const ColdEval ce = spa_general<CAUSTIC>(
                                     it, s_cur ? f : -f, s, hg, jr, t, nt, K, gm, gn, coefA, coefT);
                                 accumulate<0, PAIRED>(ce.wr, ce.wi, ce.b[0], ce.b[1], ce.b[2],
@@ -3217,8 +3282,8 @@ __device__ __forceinline__ void modesum_tile(
                         {
                             const int ln2 = opq(tid0) & 63;
 #pragma unroll
-                            for (int i = 0; i < BPL; ++i) {
-                                const int32_t k = w_lo + 64 * i + ln2;
+                            for (int i = 0; i < NB; ++i) {
+                                const int32_t k = e_lo + 64 * i + ln2;
                                 const double f = k < nlanes ? freq[k] : 0.0;
                                 fk[i] = s_cur ? f : -f;
                                 tfk[i] = TWO_PI * fk[i];
@@ -3231,7 +3296,7 @@ __device__ __forceinline__ void modesum_tile(
                 }
             }
 #ifdef EFD_EXP
-            if (lane == 0) wimb[it_ & 1][wave] = nev;
+            if (lane == 0) wimb[c & 1][wave] = nev;
 #endif
             // retire this wave's LDS-DMA pieces, then the barrier publishes chunk c+1's stage
             __builtin_amdgcn_s_waitcnt(0x0f70);
@@ -3241,22 +3306,23 @@ __device__ __forceinline__ void modesum_tile(
         if (pre >= 0) break;   // a prebuilt list is the whole list
     }
 #undef EFD_GLDS
-    if (split_S > 1) {
-        // a split tile: this workgroup's partial sums of its bins (true signs) to its slot, then
-        // the arrival count (cdna_hip_programming.md's in-launch split-K reduction: plain stores
-        // -> every wave's vmcnt(0) -> barrier -> lane 0 agent release -> vmcnt(0) -> relaxed
-        // agent fetch_add; the last arriver: agent acquire -> vmcnt(0) -> barrier -> plain loads;
-        // correct for any placement of the splits over XCDs and CUs)
+    if constexpr (NB < BPL) {
+        // the sub-bin form: this workgroup's bins (true signs) to the tile's slot, then the
+        // arrival count (cdna_hip_programming.md's in-launch split-K reduction: plain stores ->
+        // every wave's vmcnt(0) -> barrier -> lane 0 agent release -> vmcnt(0) -> relaxed agent
+        // fetch_add; the last arriver: agent acquire -> vmcnt(0) -> barrier -> plain loads;
+        // correct for any placement of the workgroups over XCDs and CUs). Each bin's sum is
+        // complete here (all the tile's records, in its order): the slot is a handover, not a
+        // reduction, so the spectrum is bitwise the whole tile's
         if (s_cur)
 #pragma unroll
-            for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
-        s_cur = 0;
+            for (int i = 0; i < NB; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
         const int lt = opq(tid0);
         const int lw = lt >> 6, ll = lt & 63;
-        double2* slot = reinterpret_cast<double2*>(spart) + (size_t)split_j * TILE_LANES * 2;
+        double2* slot = reinterpret_cast<double2*>(spart);
 #pragma unroll
-        for (int i = 0; i < BPL; ++i) {
-            const int li = lw * 64 * BPL + 64 * i + ll;
+        for (int i = 0; i < NB; ++i) {
+            const int li = lw * 64 * BPL + 64 * (ioff + i) + ll;
             slot[2 * li] = make_double2(own_r[i], own_i[i]);
             slot[2 * li + 1] = make_double2(mir_r[i], mir_i[i]);
         }
@@ -3267,7 +3333,7 @@ __device__ __forceinline__ void modesum_tile(
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int arrived = __hip_atomic_fetch_add(scnt, 1, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
-            const int last = arrived == split_S - 1;
+            const int last = arrived == BPL / NB - 1;
             if (last) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3278,37 +3344,48 @@ __device__ __forceinline__ void modesum_tile(
         }
         __syncthreads();
         if (!part[0]) return;
-        // the last arriver: the split_S slots added in split order (deterministic whichever
-        // workgroup arrives last), then the tile's own epilogue below
         const double2* s0 = reinterpret_cast<const double2*>(spart);
+        double a_r[BPL], a_i[BPL], m_r[BPL], m_i[BPL];
 #pragma unroll
         for (int i = 0; i < BPL; ++i) {
             const int li = lw * 64 * BPL + 64 * i + ll;
-            double2 a = s0[2 * li], m = s0[2 * li + 1];
-            for (int j = 1; j < split_S; ++j) {
-                const double2 a2 = s0[(size_t)j * TILE_LANES * 2 + 2 * li];
-                const double2 m2 = s0[(size_t)j * TILE_LANES * 2 + 2 * li + 1];
-                a.x += a2.x; a.y += a2.y; m.x += m2.x; m.y += m2.y;
-            }
-            own_r[i] = a.x; own_i[i] = a.y; mir_r[i] = m.x; mir_i[i] = m.y;
+            const double2 a = s0[2 * li], m = s0[2 * li + 1];
+            a_r[i] = a.x; a_i[i] = a.y; m_r[i] = m.x; m_i[i] = m.y;
         }
-        seen = true;
-    }
-    if (PAIRED && llconst != nullptr && !seen && out == nullptr && hp == nullptr) {
-        // no record reached this tile: h = 0 on its bins, whose likelihood partial is the
-        // walker-independent one k_ll_tile_const computed with this epilogue's arithmetic
-        if (tid == 0) llpart[tile] = llconst[tile];
-        return;
-    }
-    if (s_cur)
+        tile_epilogue<PAIRED>(a_r, a_i, m_r, m_i, w_lo, ll, lw, lt, nlanes, nf, k0,
+                              accumulate_out, out, hp, hc, lld, llw, llpart, tile);
+    } else {
+        if (PAIRED && llconst != nullptr && !seen && out == nullptr && hp == nullptr) {
+            // no record reached this tile: h = 0 on its bins, whose likelihood partial is the
+            // walker-independent one k_ll_tile_const computed with this epilogue's arithmetic
+            if (tid == 0) llpart[tile] = llconst[tile];
+            return;
+        }
+        if (s_cur)
 #pragma unroll
-        for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
+            for (int i = 0; i < BPL; ++i) { own_i[i] = -own_i[i]; mir_i[i] = -mir_i[i]; }
+        tid = opq(tid0);
+        tile_epilogue<PAIRED>(own_r, own_i, mir_r, mir_i, w_lo, tid & 63, wave, tid, nlanes, nf,
+                              k0, accumulate_out, out, hp, hc, lld, llw, llpart, tile);
+    }
+#ifdef EFD_EXP
+    if (threadIdx.x == 0 && tile < 16384)
+        g_exp_tclk[tile] = ((t_start & 0xffffffffull) << 32) | ((wall_clock64() - t_start) & 0xffffffffull);
+#endif
+}
 
+// The tile's epilogue (whole tile, or the last arriver of a sub-bin split): the spectrum S,
+// the symmetric grid's h+ / hx, and the fused likelihood's partial of the tile
+template <bool PAIRED>
+__device__ __forceinline__ void tile_epilogue(
+    double (&own_r)[BPL], double (&own_i)[BPL], double (&mir_r)[BPL], double (&mir_i)[BPL],
+    int32_t w_lo, int lane, int wave, int tid, int64_t nlanes, int64_t nf, int64_t k0,
+    int accumulate_out, double* __restrict__ out, double* __restrict__ hp,
+    double* __restrict__ hc, const double* __restrict__ lld, const double* __restrict__ llw,
+    double* __restrict__ llpart, int64_t tile) {
     // S is written when out != NULL; on a symmetric grid h+ and hx of bins [k0, nf) are written
     // straight from the registers when hp != NULL (the lane holds S(k) and S(nf-1-k), the two
     // halves of efd_polarizations' flip), so the likelihood path never stores S
-    tid = opq(tid0);
-    lane = tid & 63;
     double2* o = reinterpret_cast<double2*>(out);
     double2* php = reinterpret_cast<double2*>(hp);
     double2* phc = reinterpret_cast<double2*>(hc);
@@ -3380,10 +3457,6 @@ __device__ __forceinline__ void modesum_tile(
             llpart[tile] = t;
         }
     }
-#ifdef EFD_EXP
-    if (threadIdx.x == 0 && tile < 16384)
-        g_exp_tclk[tile] = ((t_start & 0xffffffffull) << 32) | ((wall_clock64() - t_start) & 0xffffffffull);
-#endif
 }
 
 #define EFD_MODESUM_PARAMS                                                                    \
@@ -3407,7 +3480,7 @@ __device__ __forceinline__ void modesum_tile(
 template <bool PAIRED, int CAUSTIC, int BPL>
 __global__ __launch_bounds__(TILE) __attribute__((amdgpu_waves_per_eu(EFD_WAVES_PER_EU, 8)))
 void k_modesum(EFD_MODESUM_PARAMS) {
-    modesum_tile<PAIRED, CAUSTIC, BPL>(EFD_MODESUM_ARGS, nullptr, nullptr, nullptr, nullptr,
+    modesum_tile<PAIRED, CAUSTIC>(EFD_MODESUM_ARGS, nullptr, nullptr, nullptr, nullptr,
                                        (int64_t)blockIdx.x);
 }
 
@@ -3525,20 +3598,28 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
     if constexpr (SPARSE) {
         const int32_t nit = d.hdr->nitems;
         if (nit > 0) {
-            // k_segments_one's split plan: items (tile, split j, S, partial slot, counter)
+            // k_segments_one's split plan: items (tile, bin j, S, slot = counter); S = BPL: the
+            // sub-bin form, one bin of every lane per workgroup
             const Layout L = make_layout(d.nt, d.K, nf, 1);
             char* W = reinterpret_cast<char*>(d.hdr);
             const int4* items = ws_at<const int4>(W, L.sitem);
             for (int64_t it = pos; it < nit; it += nper) {
                 const int4 e = items[it];
                 const int S = e.y & 0xffff, j = e.y >> 16;
-                modesum_tile<PAIRED, CAUSTIC, BPL>(
-                    d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles,
-                    d.nt, d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt,
-                    d.tperm, d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc,
-                    d.k0, lld, llw, d.llpart, llconst, e.x, true, j, S,
-                    S > 1 ? ws_at<double>(W, L.spart) + (size_t)e.z * TILE_LANES * 4 : nullptr,
-                    S > 1 ? ws_at<int32_t>(W, L.scnt) + e.w : nullptr);
+                if (S > 1)
+                    modesum_tile<PAIRED, CAUSTIC, 1>(
+                        d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles,
+                        d.nt, d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt,
+                        d.tperm, d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp,
+                        d.hc, d.k0, lld, llw, d.llpart, llconst, e.x, true, j,
+                        ws_at<double>(W, L.spart) + (size_t)e.z * TILE_LANES * 4,
+                        ws_at<int32_t>(W, L.scnt) + e.w);
+                else
+                    modesum_tile<PAIRED, CAUSTIC>(
+                        d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles,
+                        d.nt, d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt,
+                        d.tperm, d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp,
+                        d.hc, d.k0, lld, llw, d.llpart, llconst, e.x, true);
                 __syncthreads();   // the next tile's LDS writes after every wave's last reads
             }
             return;
@@ -3547,7 +3628,7 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
         if (lo < hi) {
             const int64_t t1 = min((int64_t)(hi - 1) / TILE_LANES, ntiles - 1);
             for (int64_t tile = lo / TILE_LANES + pos; tile <= t1; tile += nper) {
-                modesum_tile<PAIRED, CAUSTIC, BPL>(
+                modesum_tile<PAIRED, CAUSTIC>(
                     d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles,
                     d.nt, d.K, d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt,
                     d.tperm, d.segbase, d.stb0, d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc,
@@ -3557,7 +3638,7 @@ void k_modesum_batch(const SumBatch batch, int64_t nf, int64_t nlanes, int64_t n
         }
         return;
     }
-    modesum_tile<PAIRED, CAUSTIC, BPL>(
+    modesum_tile<PAIRED, CAUSTIC>(
         d.items, d.ranges, d.seglh, d.seginfo, d.nseg, d.freq, nf, nlanes, ntiles, d.nt, d.K,
         d.gm, d.gn, d.t, d.coefA, d.coefT, d.sctab, d.tkeys, d.tcnt, d.tperm, d.segbase, d.stb0,
         d.stb1, d.hdr, accumulate_out, d.out, d.hp, d.hc, d.k0, lld, llw, d.llpart, llconst, pos);
@@ -4675,6 +4756,17 @@ int efd_last_error(char* buf, int len) {
     return EFD_OK;
 }
 
+
+// the split plan's cost floor (k_segments_one): SPLIT_MIN_COST, or EFD_SPLIT_MIN_COST when set
+// (read per preparation; -1 splits every tile of the union: the tests' bitwise check of the
+// sub-bin form)
+static int32_t split_min_cost() {
+    const char* e = getenv("EFD_SPLIT_MIN_COST");
+    if (!e || !*e) return SPLIT_MIN_COST;
+    const long long x = atoll(e);
+    return x >= -1 && x <= (1 << 30) ? (int32_t)x : SPLIT_MIN_COST;
+}
+
 int efd_spline_build(const double* x, int n, const double* y, int ninterp, double* coef,
                      void* stream) {
     if (!x || !y || !coef || n < 2 || ninterp <= 0 || n > MAX_NT)
@@ -4874,6 +4966,7 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
             if (b <= SEG1_LDS_CAP) need = std::max(need, b);
         }
         B.seg_lds = (int32_t)need;
+        B.split_min = split_min_cost();
         hipLaunchKernelGGL(k_segments_one, dim3(1, 1, nz), dim3(SEG1_NT), (size_t)B.seg_lds, st,
                            B);
         HIP_TRY(hipGetLastError());

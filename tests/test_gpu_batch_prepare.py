@@ -250,12 +250,9 @@ def test_fused_loglike_tile_constants_bitwise(sources, dt):
     torch.cuda.synchronize()
     B.wait()
     assert torch.all(torch.isfinite(ref)) and torch.all(ref < 0)
-    # bitwise, except for a walker whose heavy tiles the sparse form splits (k_segments_one's
-    # plan: the split tiles add their partial sums in split order, another rounding)
-    split = torch.tensor([eng.split_plan()[1] > 0 for eng, _ in jobs], device="cuda")
-    for g in (got, got2):
-        assert torch.equal(g[~split], ref[~split])
-        assert torch.allclose(g[split], ref[split], rtol=1e-13, atol=0.0)
+    # bitwise, split tiles included (k_segments_one's plan evaluates a heavy tile's bins on
+    # several workgroups, each bin's sum in the whole tile's order)
+    assert torch.equal(got, ref) and torch.equal(got2, ref)
     # the constants alone sum to a zero template's sum |d - 0 w|^2 over every bin (to rounding:
     # another summation order)
     h0 = float((torch.abs(d) ** 2).sum())
@@ -299,16 +296,21 @@ def test_fused_loglike_tile_constants_no_segment(sources):
     assert np.allclose(ref.cpu().numpy(), h0, rtol=1e-12, atol=0.0)
 
 
-def test_fused_loglike_split_tiles():
+@pytest.mark.parametrize("split_min", ["", "-1"])
+def test_fused_loglike_split_tiles(split_min, monkeypatch):
     """The sparse fused likelihood's split plan (k_segments_one: a tile above the waveform's fair
-    share of the chip is evaluated by S workgroups, each writing its bins' partial sums; the last
-    arriver adds them in split order and runs the tile's epilogue) on config 5's shape: a coarse
+    share of the chip is evaluated by BPL workgroups, one bin of every lane each; the last
+    arriver runs the tile's epilogue from the bins they stored) on config 5's shape: a coarse
     downsampled grid where a few low-frequency tiles hold most records. The plan must be made
-    (split tiles > 0), the logL must equal the unsplit dense launch's to 1e-13 (summation order
-    only), repeat bitwise, and a second sum on the same preparation (the arrival counters re-armed
-    by the last arrivers) must give bitwise the same values."""
+    (split tiles > 0), the logL must equal the unsplit dense launch's bitwise, and repeated sums
+    on the same preparation (the arrival counters re-armed by the last arrivers) must give
+    bitwise the same values. split_min = -1 (EFD_SPLIT_MIN_COST) splits every tile of the union,
+    empty ones included."""
     from emri_frequencydomainwaveforms_amd.summation import loglike_tile_constants
-    srcs = [source_inputs(M=M, e0=e0, T=0.5, dt=10.0, eps=1e-2)
+    if split_min:
+        monkeypatch.setenv("EFD_SPLIT_MIN_COST", split_min)
+    # eps = 3e-2: 24-30 modes, inside k_segments_one's K <= SEG1_MAX_K (the plan's condition)
+    srcs = [source_inputs(M=M, e0=e0, T=0.5, dt=10.0, eps=3e-2)
             for M, e0 in ((1e6, 0.35), (8e5, 0.3), (1.2e6, 0.4), (9e5, 0.25))]
     fmax = max(float(np.abs(s["m"] * s["f_phi"][:, None] + s["n"] * s["f_r"][:, None]).max())
                for s in srcs)
@@ -339,5 +341,5 @@ def test_fused_loglike_split_tiles():
     plans = [eng.split_plan() for eng, _ in jobs]
     assert any(ns > 0 for _, ns in plans), plans
     assert torch.all(torch.isfinite(ref))
-    assert torch.allclose(got[0], ref, rtol=1e-13, atol=0.0), (got[0] - ref) / ref
+    assert torch.equal(got[0], ref), (got[0] - ref) / ref
     assert torch.equal(got[1], got[0]) and torch.equal(got[2], got[0])

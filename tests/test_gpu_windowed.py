@@ -290,7 +290,7 @@ def test_windowed_likelihood_short_grid_exact_path():
     s = pe.setup(Tobs=0.02, dt=10.0, eps=1e-2, M=1e5, mu=10.0, nwalkers=8, ntemps=1,
                  window_flag=True)
     n = s.info["N_f"]
-    assert n == 63115 and not HannConvolution.applies(n) and HannConvolution.applies(12623261)
+    assert n == 63117 and not HannConvolution.applies(n) and HannConvolution.applies(12623261)
     gen = s.gen
     assert gen._hann is None and not gen.can_fill_batch     # the exact transform pair
     like = s.like
