@@ -2503,11 +2503,11 @@ __device__ __forceinline__ bool hdr_j4(uint32_t ha) {   // J >= 4
     asm volatile("" : "+s"(ha));
     return ((ha >> HDR_J) & 7u) >= 4u;
 }
-#ifdef EFD_EXP_FASTPATH
-// The common record class on its own straight-line body (EFD_EXP_FASTPATH): certified safe,
-// series length J <= 2 and covering the wave's whole 64 BPL-lane chunk (every lane evaluates,
-// every lane passes the interval and sign tests), so no lane mask, no amplitude select and no
-// series branch: spa_fast_m's J <= 2 arithmetic, bitwise the same values.
+// The common record class on its own straight-line body: certified safe, series length J <= 2
+// and covering the wave's whole 64 BPL-lane chunk (every lane evaluates, every lane passes the
+// interval and sign tests), so no lane mask, no amplitude select and no series branch:
+// spa_fast_m's J <= 2 arithmetic, bitwise the same values (config 2: kernel 5.128 -> 4.978 ms
+// per launch of 8, +3.2% waveforms/s, 3 paired rounds, profiles/r05d_ab_fastpath.jsonl)
 __device__ __forceinline__ void spa_simple(const Item* __restrict__ it, double sfk, double stfk,
                                            const double2* __restrict__ sct, const RecSign& rs,
                                            double& wr, double& wi, double& w) {
@@ -2527,7 +2527,6 @@ __device__ __forceinline__ void spa_simple(const Item* __restrict__ it, double s
     wr = amp * cs;
     wi = amp * sn;
 }
-#endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            uint32_t ha, uint64_t actm,
@@ -2567,19 +2566,6 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
         const double t3 = fdds * a3;
         double ww = t3 * t3;   // 1/|y|
         double am, c0, thn;
-#ifdef EFD_EXP_J3
-        if (hdr_j3(ha) && !hdr_j4(ha)) {   // J = 3 (16% of records): every in-interval lane
-            // is inside the series' range (|y| >= 555: v <= VS / 555 = 3.4e-4), so no range test
-            // or second mask; rho = 1 - v^2 (its 45.7 v^4 term < 5.8e-13) multiplies the
-            // amplitude (folded into the cosine's constant, as for J <= 2, it would leave
-            // |rho - 1| |sr| <= 7e-10 of a term), theta's KTHN_1 term stays (2e-10 rad)
-            asm volatile("");
-            const double uu = ww * ww;
-            thn = ww * fma(-14.733333333333333333, uu, 1.0);
-            am = ampm * (1.0 - uu);
-            c0 = COS_A;
-        } else
-#endif
         if (hdr_j3(ha)) {   // J >= 3: wave-uniform; a real branch (see KTH0's notes)
             asm volatile("");
             // the |y| >= FAST_Y test only matters for J = 4 (J = 3 lanes pass it by their
@@ -3195,7 +3181,6 @@ __device__ __forceinline__ void modesum_tile(
 #ifdef EFD_EXP   // [29]: wave-records of certified-safe records
                     if (lane == 0 && rs.safe) atomicAdd(&g_exp_count[29], 1ull);
 #endif
-#ifdef EFD_EXP_FASTPATH
                     // certified safe, J <= 2 and covering the whole chunk: the straight-line
                     // evaluation (no lane masks, amplitude selects or series branch); the
                     // amplitude cubics and accumulation below are shared
@@ -3209,19 +3194,10 @@ __device__ __forceinline__ void modesum_tile(
                             need[i] = false;
                         }
                     } else
-#endif
 #pragma unroll
                     for (int i = 0; i < NB; ++i) {
                         const int32_t base = e_lo + 64 * i;
-#ifdef EFD_EXP_FULLMASK
-                        // a record covering the wave's whole 64 BPL-lane chunk needs no lane
-                        // masks (a wave-uniform branch around their SALU work)
-                        uint64_t am = ~0ull;
-                        if (hdr_test((uint32_t)((e_lo - klo) | (khi - e_hi)), 0x80000000u))
-                            am = lane_range_mask(klo - base, khi - base);
-#else
                         const uint64_t am = lane_range_mask(klo - base, khi - base);
-#endif
                         spa_fast_m<CAUSTIC>(it, fk[i], tfk[i], ha, am, sctab, rs,
                                             wr[i], wi[i], w[i], needm[i]);
                         need[i] = __builtin_amdgcn_inverse_ballot_w64(needm[i]);

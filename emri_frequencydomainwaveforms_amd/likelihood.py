@@ -203,8 +203,7 @@ class Likelihood:
             # stream, the batch costs one host synchronisation
             P = self._pipeline_for(tm)
             P.order_after_current()
-            if hasattr(tm, "prefetch"):
-                tm.prefetch(params, *args, **kwargs)
+            _prefetch(tm, params, args, kwargs)
             for i, params_i in enumerate(params):
                 j = P.next_slot()
                 slot = tm.submit(P, self._pbufs[j], *params_i, *args, order=False, **kwargs)
@@ -223,8 +222,7 @@ class Likelihood:
             if scr is None or scr.numel() < G * _lib.EFD_LOGLIKE_SCRATCH:
                 scr = self._wscratch = torch.empty(G * _lib.EFD_LOGLIKE_SCRATCH,
                                                    dtype=torch.float64, device=self.device)
-            if hasattr(tm, "prefetch"):
-                tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
+            _prefetch(tm, params, args, kwargs)
             for g0 in range(0, num_likes, G):
                 rows = params[g0:g0 + G]
                 tm.loglike_batch(out[g0:g0 + len(rows)], rows, self._d, self._w_templ, scr,
@@ -232,8 +230,7 @@ class Likelihood:
         elif getattr(tm, "can_fill", False):
             if self._buf is None or tuple(self._buf.shape) != (nch, nb):
                 self._buf = torch.empty((nch, nb), dtype=torch.complex128, device=self.device)
-            if hasattr(tm, "prefetch"):
-                tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
+            _prefetch(tm, params, args, kwargs)
             for i, params_i in enumerate(params):
                 tm.fill(self._buf, *params_i, *args, **kwargs)
                 self._red.loglike(self._buf, self._d, self._w_templ, out=out[i:i + 1])
@@ -247,12 +244,12 @@ class Likelihood:
             return out
         return out.cpu().numpy()
 
-    # walkers per fused group: one efd_modesum_prepare_batch and one efd_modesum_sum_loglike
-    # each; FUSED_DEPTH groups rotate so group i+1's preparation runs beside group i's sum.
+    # walkers per fused group (EFD_FUSED_GROUP overrides it: an experiment switch): one
+    # efd_modesum_prepare_batch and one efd_modesum_sum_loglike each; FUSED_DEPTH groups rotate so group i+1's preparation runs beside group i's sum.
     # Balanced groups of at most 16 (EFD_BATCH_MAX): config 5's 64-walker half-steps (host-bound,
     # 43-tile grids) ran 54-60 k logL/s in 4 groups against 40-51 k in 8 (5 interleaved rounds);
     # config 4's 8 walkers are one group either way (groups of 4 or 3: -5 to -10%)
-    FUSED_GROUP = 16
+    FUSED_GROUP = min(max(1, int(os.environ.get("EFD_FUSED_GROUP", "16"))), 16)
     FUSED_DEPTH = 2
     # each group's sum on the group's own stream, right behind its preparation: no
     # cross-stream wait between the two (~12 us of idle device per group on config 4's chain,
@@ -276,8 +273,7 @@ class Likelihood:
         from .summation import BatchPreparer
         if not self._fused_grid_ok(tm, kwargs):
             return None
-        if hasattr(tm, "prefetch"):
-            tm.prefetch(params, *args, **kwargs)   # the batch's host upstream, in parallel
+        _prefetch(tm, params, args, kwargs)
         n = len(params)
         if n == 0:
             return np.empty(0, dtype=np.float64)
@@ -472,6 +468,18 @@ class Likelihood:
                 args_in += (self.injection_channels, self.noise_factor)
             out_ll.append(_to_numpy(self.get_ll(*args_in, **kwargs)))
         return np.concatenate(out_ll, axis=0)
+
+
+def _prefetch(tm, params, args, kwargs):
+    """The batch's host upstream on the pool. Without waiting when the template supports it
+    (PREFETCH_ASYNC): each walker's template then waits for its own upstream only, so the first
+    groups' device work runs while the pool computes the later walkers'."""
+    if not hasattr(tm, "prefetch"):
+        return
+    if getattr(tm, "PREFETCH_ASYNC", False) and os.environ.get("EFD_PREFETCH_ASYNC", "1") != "0":
+        tm.prefetch(params, *args, wait=False, **kwargs)
+    else:
+        tm.prefetch(params, *args, **kwargs)
 
 
 def _to_numpy(x):

@@ -76,6 +76,7 @@ class FastSchwarzschildEccentricFlux:
         self._ylm_cache = {}
         self._prefetched = {}
         self._prefetched_bytes = 0
+        self._inflight = {}   # prefetch(wait=False): parameters -> the pool's Future
         self._lock = threading.Lock()
 
     # -- host-side upstream ------------------------------------------------------------------
@@ -106,6 +107,11 @@ class FastSchwarzschildEccentricFlux:
             key = (float(M), float(mu), float(p0), float(e0), float(theta), float(phi),
                    float(dist), float(Phi_phi0), float(Phi_r0), float(T), float(eps),
                    bool(include_minus_m))
+            if self._inflight:
+                with self._lock:
+                    fut = self._inflight.pop(key, None)
+                if fut is not None:
+                    return fut.result()   # (a worker's exception is raised here)
             if self._prefetched:
                 with self._lock:
                     hit = self._prefetched.pop(key, None)
@@ -113,6 +119,12 @@ class FastSchwarzschildEccentricFlux:
                         self._prefetched_bytes -= _nbytes(hit)
                 if hit is not None:
                     return hit
+        return self._upstream(M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
+                              mode_selection, include_minus_m)
+
+    def _upstream(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps,
+                  mode_selection, include_minus_m):
+        """prepare()'s computation, no cache (the prefetch workers call it directly)."""
         amp = self.amplitude_generator
         lib = getattr(self.inspiral_generator, "lib", None)
         if lib is not None and mode_selection is None and hasattr(lib, "efd_host_modes"):
@@ -170,11 +182,17 @@ class FastSchwarzschildEccentricFlux:
                     f_phi=om_phi / (2.0 * np.pi * M * MTSUN_SI),
                     f_r=om_r / (2.0 * np.pi * M * MTSUN_SI))
 
-    def prefetch(self, calls):
+    def prefetch(self, calls, wait=True):
         """Run the host upstream of several sources at once: `calls` are prepare() argument
         tuples (M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps). The native parts
         release the GIL, so a thread pool works a walker batch in parallel; the results are held
-        for the prepare() calls that follow (each taken once)."""
+        for the prepare() calls that follow (each taken once).
+
+        wait=False returns at once: each call's upstream runs on the pool (in `calls` order) and
+        the prepare() call with its parameters waits for that one result only, so a caller
+        working through the batch in groups starts a group's device work as soon as the
+        group's own walkers are done, while the pool works on the next groups (the fused
+        likelihood's half-step)."""
         calls = [tuple(c) for c in calls]
         for c in calls:                       # Ylm per viewing angle before the threads start
             self._ylms(c[4], c[5])
@@ -188,8 +206,15 @@ class FastSchwarzschildEccentricFlux:
 
         def run(c):
             lib.efd_host_set_threads(per)
-            return self.prepare(*c)
+            return self._upstream(*c, None, True)
 
+        if not wait:
+            with self._lock:
+                if len(self._inflight) > self.INFLIGHT_MAX:
+                    self._inflight.clear()   # results nobody took: dropped when they finish
+                for c in calls:
+                    self._inflight[tuple(float(v) for v in c[:11]) + (True,)] = pool.submit(run, c)
+            return len(calls)
         res = list(pool.map(run, calls))
         with self._lock:
             # results nobody took (a batch interrupted by an exception, parameters the caller
@@ -209,6 +234,7 @@ class FastSchwarzschildEccentricFlux:
         return len(res)
 
     PREFETCH_MAX_BYTES = 1 << 30
+    INFLIGHT_MAX = 4096
 
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
@@ -495,8 +521,11 @@ class GenerateEMRIWaveform:
         prep.wait()   # device-side errors of the groups' workspaces raise here
         return out
 
+    # prefetch(wait=False) is supported (the likelihood's groups then overlap the upstream)
+    PREFETCH_ASYNC = True
+
     def prefetch(self, params, T=1.0, dt=10.0, eps=1e-5, mode_selection=None,
-                 include_minus_m=True, **kwargs):
+                 include_minus_m=True, wait=True, **kwargs):
         """The host upstream of a batch of 14-parameter sets at once (thread pool; see
         FastSchwarzschildEccentricFlux.prefetch); later calls with the same parameters and
         kwargs take the results. Only for the FD generator without an explicit mode list."""
@@ -508,7 +537,7 @@ class GenerateEMRIWaveform:
             M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
             theta, phi, _ = self._angles(qS, phiS, qK, phiK)
             calls.append((M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps))
-        return gen.prefetch(calls)
+        return gen.prefetch(calls, wait=wait)
 
     def fill_channels(self, out, *params, k0=None, **kwargs):
         """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).

@@ -173,6 +173,28 @@ def test_fused_likelihood_many_walkers(setup):
     bad = [(jobs[0][0], dict(jobs[0][1], _args=bad_args)), jobs[1]]
     with pytest.raises(_lib.EFDError):
         sum_batch_loglike(bad, like._d, like._w_templ, out)
+    # a failure inside the second group's flush, after its upload and preparation are queued:
+    # get_ll raises only once every group stream is idle, and the next call is unaffected
+    like.fused_likelihood = True
+    Bp = like._fused["prep"]
+    orig, seen = Bp.flush, []
+
+    def flaky():
+        r = orig()
+        seen.append(r[0])
+        if len(seen) == 2:
+            raise RuntimeError("injected flush failure")
+        return r
+
+    Bp.flush = flaky
+    try:
+        with pytest.raises(RuntimeError, match="injected"):
+            like.get_ll(walkers, **kw)
+        assert len(seen) == 2 and seen[0] != seen[1]
+        assert all(g["stream"].query() for g in Bp.groups)
+    finally:
+        del Bp.flush
+    np.testing.assert_array_equal(like.get_ll(walkers, **kw), llf)
 
 
 def test_spectrum_matches_oracle_through_api(setup):

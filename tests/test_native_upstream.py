@@ -93,7 +93,7 @@ def _bare_generator(backend):
     wg.mode_selector = ModeSelector(wg.amplitude_generator.m0mask)
     wg.output_type, wg.last_modes = "fd", None
     wg._ylm_cache, wg._prefetched, wg._lock = {}, {}, threading.Lock()
-    wg._prefetched_bytes = 0
+    wg._prefetched_bytes, wg._inflight = 0, {}
     return wg
 
 
@@ -120,6 +120,21 @@ def test_prepare_native_vs_numpy_and_prefetch():
     wn.prefetch(calls[:2])
     wn.prefetch(calls[2:4])                        # 4 results would pass 3: the first 2 go
     assert len(wn._prefetched) == 2 and wn._prefetched_bytes <= wn.PREFETCH_MAX_BYTES
+    # wait=False: each prepare() takes its own walker's Future (the likelihood's groups), the
+    # same arrays; a worker's exception is raised by the prepare() that takes it
+    wn._prefetched.clear()
+    wn._prefetched_bytes = 0
+    assert wn.prefetch(calls, wait=False) == len(calls) and len(wn._inflight) == len(calls)
+    for c, ref in zip(calls, serial):
+        got = wn.prepare(*c)
+        for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
+            np.testing.assert_array_equal(got[k], ref[k])
+    assert not wn._inflight and not wn._prefetched
+    bad = calls[0][:2] + (3.0,) + calls[0][3:]     # p0 inside the separatrix buffer
+    wn.prefetch([bad], wait=False)
+    with pytest.raises(ValueError):
+        wn.prepare(*bad)
+    assert not wn._inflight
 
 
 def test_host_modes_threads_bitwise():
