@@ -2615,7 +2615,8 @@ __device__ unsigned long long g_exp_count[EXP_NCOUNT];  // [8..15]: |y| bands of
 // balance: sum over chunks of the busiest wave's record evaluations, of all waves' evaluations,
 // and the number of chunks; [27, 28]: segment table size, hits per tile summed (k_tile_keys);
 // [29]: wave-records of certified-safe records; [32..35]: wave-records by series length J = 1..4,
-// [36]: sub-branch flips
+// [36]: sub-branch flips; [37..39]: wave-records off the straight-line path by cause (partial
+// coverage, J >= 3, not certified; a record may count in several)
 __device__ unsigned int g_exp_tile[16384];       // record evaluations per tile (first 16384)
 __device__ unsigned long long g_exp_tclk[16384];  // wall clock (s_memrealtime) per tile
 #endif
@@ -3180,6 +3181,13 @@ __device__ __forceinline__ void modesum_tile(
                     const RecSign rs = rec_sign((ha >> (2 * HB + 4)) & 3u);
 #ifdef EFD_EXP   // [29]: wave-records of certified-safe records
                     if (lane == 0 && rs.safe) atomicAdd(&g_exp_count[29], 1ull);
+#endif
+#ifdef EFD_EXP   // [37]: partial coverage of the wave's bins, [38]: J >= 3, [39]: not certified
+                    if (lane == 0) {
+                        if ((e_lo - klo) < 0 || (khi - e_hi) < 0) atomicAdd(&g_exp_count[37], 1ull);
+                        if (((ha >> HDR_J) & 7u) >= 3u) atomicAdd(&g_exp_count[38], 1ull);
+                        if (!((ha >> (HDR_FD + 1)) & 1u)) atomicAdd(&g_exp_count[39], 1ull);
+                    }
 #endif
                     // certified safe, J <= 2 and covering the whole chunk: the straight-line
                     // evaluation (no lane masks, amplitude selects or series branch); the

@@ -135,7 +135,8 @@ def child(name, ref_path):
              "ov_lt1e-12", "ov_lt1e-9", "ov_lt1e-6", "ov_lt1e-3", "ov_lt1e-1", "ov_ge1e-1",
              "chunk_max_wave_evals", "chunk_wave_evals", "chunks", "segments",
              "tile_hits", "safe_wave_evals", "unused30", "unused31", "records_j1", "records_j2",
-             "records_j3", "records_j4", "subbranch_flips"))}
+             "records_j3", "records_j4", "subbranch_flips", "off_fast_partial", "off_fast_j3",
+             "off_fast_uncertified"))}
         c = out["counters_per_launch"]
         if c["chunk_wave_evals"] > 0:
             # wave-time lost at the chunk barriers if every record evaluation cost the same
