@@ -297,6 +297,9 @@ constexpr int SPLINE_PF = 8;   // 16: same, 32: slower (k_prep 110 -> 177 us)
 // fixup steps) on the serial Thomas chains, whose latency sets the preparation's length; the
 // coefficients stay within 1e-11 of scipy's (tests/test_gpu_modesum.py), their rounding level
 __device__ __forceinline__ double spl_rcp(double x) {
+#ifdef EFD_EXP_EXACT_RCP   // experiment: IEEE division (the host twin's), for the HIP = twin study
+    return 1.0 / x;
+#endif
     double y = __builtin_amdgcn_rcp(x);
     double e = fma(-x, y, 1.0);
     y = fma(y, e, y);
@@ -2527,6 +2530,33 @@ __device__ __forceinline__ void spa_simple(const Item* __restrict__ it, double s
     wr = amp * cs;
     wi = amp * sn;
 }
+#ifdef EFD_EXP_FAST3
+// (EFD_EXP_FAST3) the same for series length J = 3: spa_fast_m's J >= 3 branch with every lane
+// in range (a J = 3 record's lanes pass |y| >= FAST_Y by its bound) and active
+__device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double sfk, double stfk,
+                                            const double2* __restrict__ sct, const RecSign& rs,
+                                            double& wr, double& wi, double& w) {
+    const double u = sfk - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    w = tt - it->tj;
+    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+    const double fd = fma(fma(it->fd[0], w, it->fd[1]), w, it->fd[2]);
+    const double amp = rsqrt_pos_sum(fabs(fd));
+    const double psi0 = fma(stfk, tt, -ph);
+    const double fdds = fma(fma(it->fdd[0], w, it->fdd[1]), w, it->fdd[2]);
+    const double a3 = amp * amp * amp;
+    const double t3 = fdds * a3;
+    const double ww = t3 * t3;
+    const double uu = ww * ww;
+    const double r = fma(45.7, uu * uu, 1.0 - uu);
+    const double thn = ww * fma(-14.733333333333333333, uu, 1.0);
+    const double am = amp * r;
+    double sn, cs;
+    sincos_tab(psi0, rs.shift, sct, sn, cs, thn, true, rs.kth, COS_A);
+    wr = am * cs;
+    wi = am * sn;
+}
+#endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            uint32_t ha, uint64_t actm,
@@ -3202,6 +3232,18 @@ __device__ __forceinline__ void modesum_tile(
                             need[i] = false;
                         }
                     } else
+#ifdef EFD_EXP_FAST3
+                    if (CAUSTIC == EFD_CAUSTIC_UNIFORM &&
+                        !hdr_test(((uint32_t)((e_lo - klo) | (khi - e_hi)) >> 31) |
+                                  (((((ha >> HDR_J) & 7u) ^ 3u) + 7u) >> 3) |
+                                  (((ha >> (HDR_FD + 1)) & 1u) ^ 1u), 1u)) {
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) {
+                            spa_simple3(it, fk[i], tfk[i], sctab, rs, wr[i], wi[i], w[i]);
+                            need[i] = false;
+                        }
+                    } else
+#endif
 #pragma unroll
                     for (int i = 0; i < NB; ++i) {
                         const int32_t base = e_lo + 64 * i;
@@ -4882,7 +4924,11 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         d.lists = use_prebuilt(ai->K) ? (use_cost_order(L, ai->K) ? 3 : 1) : 0;
         any_lists |= d.lists != 0;
         any_order |= d.lists == 3;
+#ifdef EFD_EXP_NO_PCR   // experiment: every waveform on the Thomas kernels (the twin's solve order)
+        const bool pcr = false;
+#else
         const bool pcr = ai->nt >= 4 && ai->nt <= PCR_NMAX;
+#endif
         d.pcr = pcr ? (ai->K < PCR_MAX_K ? 3 : 1) : 0;
         if (pcr) {
             any_pcr = true;

@@ -429,9 +429,14 @@ class get_fd_waveform_fromFD:
 
     def prefetch(self, params, *args, **kwargs):
         """The host upstream of a walker batch in parallel (GenerateEMRIWaveform.prefetch),
-        ahead of the per-walker submit/fill calls; a no-op for other generators."""
+        ahead of the per-walker submit/fill calls; a no-op for other generators. wait=False
+        (PREFETCH_ASYNC generators) returns before the upstream is done."""
         fn = getattr(self.waveform_generator, "prefetch", None)
         return fn(params, **kwargs) if fn is not None and not args else 0
+
+    @property
+    def PREFETCH_ASYNC(self):
+        return bool(getattr(self.waveform_generator, "PREFETCH_ASYNC", False))
 
     # walkers per windowed group (fill_batch): their spectra share one batched transform pair
     WINDOW_GROUP = 8

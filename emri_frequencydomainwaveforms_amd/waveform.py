@@ -537,7 +537,7 @@ class GenerateEMRIWaveform:
             M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
             theta, phi, _ = self._angles(qS, phiS, qK, phiK)
             calls.append((M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps))
-        return gen.prefetch(calls, wait=wait)
+        return gen.prefetch(calls) if wait else gen.prefetch(calls, wait=False)
 
     def fill_channels(self, out, *params, k0=None, **kwargs):
         """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).
