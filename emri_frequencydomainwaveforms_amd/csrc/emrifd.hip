@@ -2530,9 +2530,10 @@ __device__ __forceinline__ void spa_simple(const Item* __restrict__ it, double s
     wr = amp * cs;
     wi = amp * sn;
 }
-#ifdef EFD_EXP_FAST3
-// (EFD_EXP_FAST3) the same for series length J = 3: spa_fast_m's J >= 3 branch with every lane
-// in range (a J = 3 record's lanes pass |y| >= FAST_Y by its bound) and active
+// The same for series length J = 3 (16% of config 2's records): spa_fast_m's J >= 3 branch with
+// every lane active and in range (k_items gives J = 3 only when |y| >= 555 / 1.1 on the whole
+// interval, far inside FAST_Y = 153), bitwise its values (+1.8% config 2, CI 1.006-1.023, 3
+// paired rounds, profiles/r05g_ab_fast3.jsonl)
 __device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double sfk, double stfk,
                                             const double2* __restrict__ sct, const RecSign& rs,
                                             double& wr, double& wi, double& w) {
@@ -2556,7 +2557,6 @@ __device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double 
     wr = am * cs;
     wi = am * sn;
 }
-#endif
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
                                            uint32_t ha, uint64_t actm,
@@ -3232,7 +3232,6 @@ __device__ __forceinline__ void modesum_tile(
                             need[i] = false;
                         }
                     } else
-#ifdef EFD_EXP_FAST3
                     if (CAUSTIC == EFD_CAUSTIC_UNIFORM &&
                         !hdr_test(((uint32_t)((e_lo - klo) | (khi - e_hi)) >> 31) |
                                   (((((ha >> HDR_J) & 7u) ^ 3u) + 7u) >> 3) |
@@ -3243,7 +3242,6 @@ __device__ __forceinline__ void modesum_tile(
                             need[i] = false;
                         }
                     } else
-#endif
 #pragma unroll
                     for (int i = 0; i < NB; ++i) {
                         const int32_t base = e_lo + 64 * i;

@@ -77,7 +77,7 @@ def test_config3_full_grid_vs_twin():
     upstream builds the inputs). Each point's HIP spectrum is held to the host twin
     efd_modesum_cpu, which runs the same algorithm and is itself pinned to the oracle
     (tests/test_cpu_twin.py; the oracle checks the grid's corners above). The bound is the
-    config-2 twin test's per-bin rule: 1e-10 max|S| wherever the twin's response to two 4-ulp
+    config-2 twin test's per-bin rule: 1e-10 max|S| wherever the twin's response to four 4-ulp
     input perturbations stays below that, 2x that response elsewhere. Supports, contribution
     and evaluation counts must be identical."""
     from emri_frequencydomainwaveforms_amd import cputwin
@@ -112,14 +112,19 @@ def test_config3_full_grid_vs_twin():
                                        p(d["f_phi"]), p(d["f_r"]), m, n, yp, ym, freq_h, scale)
             T = twin()
             assert eng.stats() == cputwin.stats(), (M, e0)
-            Tps = [twin(ulp_perturbation(s)) for s in (41, 42)]
+            # four 4-ulp draws for D (as the config-2 twin test; two recorded beside)
+            Tps = [twin(ulp_perturbation(s)) for s in (41, 42, 43, 44)]
             ok, stats, _ = split_check(S, T, Tps, rel=1e-10)
             assert ok, (M, e0, stats)
+            _, stats2, _ = split_check(S, T, Tps[:2], rel=1e-10)
+            stats["max_err_over_D_at_folds_2draws"] = stats2["max_err_over_D_at_folds"]
             np.testing.assert_array_equal(S != 0, T != 0)
-            for k in ("max_err_off_fold_rel", "max_err_over_D_at_folds", "fold_bins"):
-                worst[k] = max(worst[k], stats[k])
+            for k in ("max_err_off_fold_rel", "max_err_over_D_at_folds", "fold_bins",
+                      "max_err_over_D_at_folds_2draws"):
+                worst[k] = max(worst.get(k, 0.0), stats[k])
     record_parity("config3_grid_vs_twin", dict(worst, points=len(Ks), harmonics_min=min(Ks),
-                                               harmonics_max=max(Ks), ok=True))
+                                               harmonics_max=max(Ks), perturbation_draws=4,
+                                               ok=True))
 
 
 def test_config5_downsampled_grid():

@@ -6,7 +6,7 @@ only by rounding (reciprocal / rsqrt estimates with Newton steps and FMA contrac
 the records' order within a tile):
 - small sources, both caustic modes, symmetric / asymmetric / downsampled grids, the fused
   h+/hx: max|S_hip - S_twin| <= 1e-10 max|S_twin|;
-- config 2 at full size: per bin, 1e-10 max|S_twin| wherever the twin's own response to two
+- config 2 at full size: per bin, 1e-10 max|S_twin| wherever the twin's own response to six
   random 4-ulp perturbations of the trajectory inputs stays below that, 2 x that response on
   the remaining (fold / extrapolated-term) bins (tests/helpers.split_check), identical support,
   contribution and evaluation counts.
@@ -70,8 +70,14 @@ def test_hip_equals_twin_config2_full_size():
     tstats = cputwin.stats()
     S, st = _hip(w, w["freq"], amp_nt_k=w["amp"])
     assert st == tstats
-    Tps = [twin(ulp_perturbation(s)) for s in (31, 32)]
+    # D from six 4-ulp perturbations (the twin is cheap): with two, D is the larger of two draws
+    # of the response and the GPU's own rounding differences, one more draw, reach ~1.0 D at
+    # the worst of the 1.26 M fold bins; the two-draw figure is recorded beside it
+    Tps = [twin(ulp_perturbation(s)) for s in (31, 32, 33, 34, 35, 36)]
     ok, stats, _ = split_check(S, T, Tps, rel=1e-10)
+    _, stats2, _ = split_check(S, T, Tps[:2], rel=1e-10)
+    stats["max_err_over_D_at_folds_2draws"] = stats2["max_err_over_D_at_folds"]
+    stats["perturbation_draws"] = len(Tps)
     record_parity("config2_hip_vs_twin", stats)
     assert ok, stats
     np.testing.assert_array_equal(S != 0, T != 0)
