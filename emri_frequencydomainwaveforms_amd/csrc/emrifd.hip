@@ -4515,13 +4515,105 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
     }
 }
 
-// (B): one row f_r per workgroup: forward FFT, times the kernel's spectrum, inverse FFT
-__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+// (B): one row f_r per workgroup: forward FFT, times the kernel's spectrum, inverse FFT, as
+// three register stages per direction with two LDS exchanges between them (8192 = 32 x 16 x 16):
+//   forward  (A) thread t = n2 (n = n2 + 256 n1): DFT-32 over n1, times w_8192^(n2 k1)
+//            (B) task (k1, n2a) (n2 = n2a + 16 n2b): DFT-16 over n2b, times w_256^(n2a k2a)
+//            (C) task (k1, k2a): DFT-16 over n2a -> X[k1 + 32 k2a + 512 k2b], natural index k
+//   times the kernel's spectrum at k, then the transpose of the same steps: the inverse of (C) on
+//   the same task's registers (no exchange), of (B), of (A) -> x[n2 + 256 n1], natural order.
+// Four exchanges of 64 KB per row instead of the Stockham passes' ten (five radix-8/2 passes per
+// direction, each a 64-KB LDS read and write) and the multiply's own pass; every exchange is
+// bank-conflict free (exchange 1: rows of 257 elements, lanes along k1 at stride 514 words;
+// exchange 2: [k2a][n2a][k1], lanes along k1). Twiddle powers from two __sincosf (w, w^8).
+constexpr int FR_NT = 256;     // threads of the row workgroup (32 elements each)
+constexpr int FR_S1 = 257;     // exchange 1: LDS row stride of [k1][n2] (elements)
+// cos and sin of 2 pi j / 32
+constexpr float FC_COS32[32] = {
+    1.000000000e+00f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f, 7.071067812e-01f,
+    5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f, 0.0f, -1.950903220e-01f,
+    -3.826834324e-01f, -5.555702330e-01f, -7.071067812e-01f, -8.314696123e-01f,
+    -9.238795325e-01f, -9.807852804e-01f, -1.000000000e+00f, -9.807852804e-01f,
+    -9.238795325e-01f, -8.314696123e-01f, -7.071067812e-01f, -5.555702330e-01f,
+    -3.826834324e-01f, -1.950903220e-01f, 0.0f, 1.950903220e-01f, 3.826834324e-01f,
+    5.555702330e-01f, 7.071067812e-01f, 8.314696123e-01f, 9.238795325e-01f, 9.807852804e-01f};
+// w_N^j = exp(SIGN 2 pi i j / N) for N = 16, 32 (compile-time j: constant-folded)
+template <int SIGN, int N>
+__device__ __forceinline__ fcv fc_w(int j) {
+    const int q = (j * (32 / N)) & 31;
+    return (fcv){FC_COS32[q], (float)SIGN * FC_COS32[(q + 24) & 31]};
+}
+// natural-order DFT-16 (4 x 4) and DFT-32 (4 x 8) in registers, exp(SIGN 2 pi i n k / N)
+template <int SIGN>
+__device__ __forceinline__ void fc_dft16(fcv* v) {
+    fcv t[4][4];
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) {   // DFT-4 over n2 of x[n1 + 4 n2]
+        fcv a0 = v[n1], a1 = v[n1 + 4], a2 = v[n1 + 8], a3 = v[n1 + 12];
+        fc_dft4<SIGN>(a0, a1, a2, a3);
+        t[n1][0] = a0; t[n1][1] = a1; t[n1][2] = a2; t[n1][3] = a3;
+    }
+#pragma unroll
+    for (int n1 = 1; n1 < 4; ++n1)
+#pragma unroll
+        for (int k1 = 1; k1 < 4; ++k1) t[n1][k1] = cmulf(t[n1][k1], fc_w<SIGN, 16>(n1 * k1));
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {   // DFT-4 over n1 -> X[k1 + 4 k2]
+        fcv a0 = t[0][k1], a1 = t[1][k1], a2 = t[2][k1], a3 = t[3][k1];
+        fc_dft4<SIGN>(a0, a1, a2, a3);
+        v[k1] = a0; v[k1 + 4] = a1; v[k1 + 8] = a2; v[k1 + 12] = a3;
+    }
+}
+template <int SIGN>
+__device__ __forceinline__ void fc_dft32(fcv* v) {
+    fcv t[8][4];
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {   // DFT-4 over n2 of x[n1 + 8 n2]
+        fcv a0 = v[n1], a1 = v[n1 + 8], a2 = v[n1 + 16], a3 = v[n1 + 24];
+        fc_dft4<SIGN>(a0, a1, a2, a3);
+        t[n1][0] = a0; t[n1][1] = a1; t[n1][2] = a2; t[n1][3] = a3;
+    }
+#pragma unroll
+    for (int n1 = 1; n1 < 8; ++n1)
+#pragma unroll
+        for (int k1 = 1; k1 < 4; ++k1) t[n1][k1] = cmulf(t[n1][k1], fc_w<SIGN, 32>(n1 * k1));
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {   // DFT-8 over n1 -> X[k1 + 4 k2]
+        fcv e[8];
+#pragma unroll
+        for (int n1 = 0; n1 < 8; ++n1) e[n1] = t[n1][k1];
+        fc_dft8<SIGN>(e);
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) v[k1 + 4 * k2] = e[k2];
+    }
+}
+// v[j] *= w^j, j = 0 .. N-1, w = exp(i theta): powers from w and w^8 (at most 3 + 7 products)
+template <int N>
+__device__ __forceinline__ void fc_twiddle_pow(fcv* v, float theta) {
+    float s1, c1, s8, c8;
+    __sincosf(theta, &s1, &c1);
+    __sincosf(8.0f * theta, &s8, &c8);
+    const fcv w1 = {c1, s1}, w8 = {c8, s8};
+    fcv p[8];
+    p[0] = (fcv){1.0f, 0.0f};
+    p[1] = w1;
+#pragma unroll
+    for (int j = 2; j < 8; ++j) p[j] = cmulf(p[j - 1], w1);
+    fcv b = (fcv){1.0f, 0.0f};
+#pragma unroll
+    for (int a = 0; a < N / 8; ++a) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (a + j > 0) v[8 * a + j] = cmulf(v[8 * a + j], a == 0 ? p[j] : (j == 0 ? b : cmulf(b, p[j])));
+        b = a == 0 ? w8 : cmulf(b, w8);
+    }
+}
+__global__ __launch_bounds__(FR_NT)
 void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
-    __shared__ fcv sm[FC_C + FC_C / 16];
+    static_assert(FC_C == 32 * 16 * 16 && FR_NT == 256, "row transform: 8192 = 32 x 16 x 16");
+    __shared__ fcv sm[32 * FR_S1];   // exchange 1 [k1][n2] (stride 257); exchange 2 [k2a][n2a][k1]
     const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
     fcv* Y = reinterpret_cast<fcv*>(Yv);
-    const FcRowIdx idx;
     // (row f_r, walker) pairs: XCD x = b mod 8 takes the contiguous eighth of them in f_r-major
     // order, so a kernel-spectrum row is read from HBM once per XCD and from its L2 for the
     // group's other walkers (gridDim.x = R * rows, a multiple of 8)
@@ -4529,26 +4621,85 @@ void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __r
     const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
     const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
     fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C;
-    const fcv* k = kfp + (int64_t)fr * FC_C;
-    constexpr int NQ = FC_C / FC_NT;
+    const fcv* kr = kfp + (int64_t)fr * FC_C;
+    const int t = threadIdx.x;
+    constexpr float W8192 = FC_2PI / 8192.0f, W256 = FC_2PI / 256.0f;
+    {   // forward (A): n2 = t
+        fcv v[32];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = threadIdx.x + q * FC_NT;
-        sm[idx(0, e)] = y[e];
+        for (int n1 = 0; n1 < 32; ++n1) v[n1] = y[t + 256 * n1];
+        fc_dft32<-1>(v);
+        fc_twiddle_pow<32>(v, -W8192 * (float)t);
+#pragma unroll
+        for (int k1 = 0; k1 < 32; ++k1) sm[k1 * FR_S1 + t] = v[k1];
     }
     __syncthreads();
-    fc_fft<-1, FC_C, 0>(sm, idx);
+    fcv u[2][16];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = threadIdx.x + q * FC_NT;
-        sm[idx(0, e)] = cmulf(sm[idx(0, e)], k[e]);
+    for (int h = 0; h < 2; ++h) {   // forward (B): task (k1, n2a)
+        const int q = t + 256 * h, k1 = q & 31, n2a = q >> 5;
+#pragma unroll
+        for (int n2b = 0; n2b < 16; ++n2b) u[h][n2b] = sm[k1 * FR_S1 + n2a + 16 * n2b];
     }
     __syncthreads();
-    fc_fft<1, FC_C, 0>(sm, idx);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = threadIdx.x + q * FC_NT;
-        y[e] = sm[idx(0, e)];
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h, k1 = q & 31, n2a = q >> 5;
+        fc_dft16<-1>(u[h]);
+        fc_twiddle_pow<16>(u[h], -W256 * (float)n2a);
+#pragma unroll
+        for (int k2a = 0; k2a < 16; ++k2a) sm[(k2a * 16 + n2a) * 32 + k1] = u[h][k2a];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // forward (C), the kernel's spectrum, inverse (C): (k1, k2a)
+        const int q = t + 256 * h, k1 = q & 31, k2a = q >> 5;
+#pragma unroll
+        for (int n2a = 0; n2a < 16; ++n2a) u[h][n2a] = sm[(k2a * 16 + n2a) * 32 + k1];
+        fc_dft16<-1>(u[h]);
+#pragma unroll
+        for (int k2b = 0; k2b < 16; ++k2b)
+            u[h][k2b] = cmulf(u[h][k2b], kr[k1 + 32 * k2a + 512 * k2b]);
+        fc_dft16<1>(u[h]);
+        fc_twiddle_pow<16>(u[h], W256 * (float)k2a);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h, k1 = q & 31, k2a = q >> 5;
+#pragma unroll
+        for (int n2a = 0; n2a < 16; ++n2a) sm[(k2a * 16 + n2a) * 32 + k1] = u[h][n2a];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // inverse (B): task (k1, n2a)
+        const int q = t + 256 * h, k1 = q & 31, n2a = q >> 5;
+#pragma unroll
+        for (int k2a = 0; k2a < 16; ++k2a) u[h][k2a] = sm[(k2a * 16 + n2a) * 32 + k1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h, k1 = q & 31, n2a = q >> 5;
+        fc_dft16<1>(u[h]);   // -> n2b
+        // times w_8192^(-n2 k1), n2 = n2a + 16 n2b: w^(n2a k1) (w^(16 k1))^n2b
+        float s0, c0;
+        __sincosf(W8192 * (float)(n2a * k1), &s0, &c0);
+        const fcv w0 = {c0, s0};
+#pragma unroll
+        for (int n2b = 0; n2b < 16; ++n2b) u[h][n2b] = cmulf(u[h][n2b], w0);
+        fc_twiddle_pow<16>(u[h], W8192 * 16.0f * (float)k1);
+#pragma unroll
+        for (int n2b = 0; n2b < 16; ++n2b) sm[k1 * FR_S1 + n2a + 16 * n2b] = u[h][n2b];
+    }
+    __syncthreads();
+    {   // inverse (A): n2 = t -> x[n2 + 256 n1]
+        fcv v[32];
+#pragma unroll
+        for (int k1 = 0; k1 < 32; ++k1) v[k1] = sm[k1 * FR_S1 + t];
+        fc_dft32<1>(v);
+#pragma unroll
+        for (int n1 = 0; n1 < 32; ++n1) y[t + 256 * n1] = v[n1];
     }
 }
 
@@ -5571,7 +5722,7 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         hipLaunchKernelGGL((k_fc_cols<true, RR>), dim3(FC_C / NC, (unsigned)rows), dim3(FC_NT), \
                            0, st, (const double2*)S, stride, info, y);                        \
         HIP_TRY(hipGetLastError());                                                           \
-        hipLaunchKernelGGL(k_fc_rows, dim3(RR * (unsigned)rows), dim3(FC_NT), 0, st,          \
+        hipLaunchKernelGGL(k_fc_rows, dim3(RR * (unsigned)rows), dim3(FR_NT), 0, st,          \
                            (const float2*)kfp, m, (int)rows, y);                              \
         HIP_TRY(hipGetLastError());                                                           \
         hipLaunchKernelGGL((k_fc_cols<false, RR>), dim3(FC_C / NC, (unsigned)rows),          \

@@ -2,7 +2,7 @@
 # GPU box, round 5.   bash tools/gpu/r05_measure.sh TAG PART
 #   PART pmc:     the bench line + kernel trace + PMC passes (pmc_refresh.sh) and an LDS pass of
 #                 the mode sum
-#   PART configs: the windowed path's trace and HBM passes, configs 1/3/4/5 (API and device
+#   PART configs (configs_only: without the windowed passes): the windowed path's trace and HBM passes, configs 1/3/4/5 (API and device
 #                 rates), the API path's upstream overlap A/B (EFD_PREFETCH_ASYNC, EFD_FUSED_GROUP),
 #                 the walker half-step host phases and the upstream pool's scaling
 set -o pipefail
@@ -17,7 +17,7 @@ if [ "$PART" = pmc ]; then
   echo pmc done
   exit 0
 fi
-bash tools/gpu/windowed_prof.sh $TAG || exit $?
+[ "$PART" = configs_only ] || bash tools/gpu/windowed_prof.sh $TAG || exit $?
 timeout -k 10 600 python tools/configs.py --only 1,3,4,5 --reps 5 > $O/configs.jsonl 2> $O/configs.err || { tail -20 $O/configs.err; exit 9; }
 timeout -k 10 300 env EFD_PREFETCH_ASYNC=0 python tools/configs.py --only 4,5 --reps 5 > $O/configs_sync.jsonl 2> $O/configs_sync.err || { tail -20 $O/configs_sync.err; exit 9; }
 timeout -k 10 300 env EFD_FUSED_GROUP=4 python tools/configs.py --only 4 --reps 5 > $O/configs_g4.jsonl 2> $O/configs_g4.err || { tail -20 $O/configs_g4.err; exit 9; }
