@@ -4741,62 +4741,45 @@ __global__ void k_hann_polarizations(const double2* __restrict__ S, const float2
     hc[i] = vc;
 }
 // the windowed templates' log-likelihood partials of every row: efd_loglike's terms (d - h w,
-// product rounded then difference) for both channels of every bin [k0, nf). A thread takes a bin
-// for all rows, so d and w (48 B per bin, the same for every walker) are read once per group
-// instead of once per row.
+// product rounded then difference) for both channels of every bin [k0, nf). One workgroup per
+// (bin chunk, row): a thread holds one row's sum (70 VGPRs, 7 waves per SIMD: the loads of many
+// waves in flight; the earlier form kept all rows' sums and loads in one thread, 233 VGPRs and
+// 2 waves per SIMD, 0.53 of HBM). The rows of a chunk are consecutive workgroups of one XCD
+// (workgroup b runs on XCD b mod 8), so d and w (48 B per bin, the same for every row) come from
+// HBM once and from that XCD's L2 for the other rows. part[row * nchunk + chunk].
 constexpr int HANN_ROWS_MAX = 16;
 __global__ __launch_bounds__(256) void k_hann_loglike_partial(
     const double2* __restrict__ S, int64_t stride, const float2* __restrict__ Y,
     const uint64_t* __restrict__ info, int64_t m, int64_t nf, int64_t k0,
-    const double2* __restrict__ d, const double* __restrict__ w, int rows,
+    const double2* __restrict__ d, const double* __restrict__ w, int rows, int nchunk,
     double* __restrict__ part) {
 #pragma clang fp contract(off)
-    __shared__ double sc[HANN_ROWS_MAX];
-    __shared__ int64_t sfirst[HANN_ROWS_MAX];
-    if (threadIdx.x < HANN_ROWS_MAX && (int)threadIdx.x < rows) {
-        const HannRow h = hann_row(info, threadIdx.x);
-        sc[threadIdx.x] = h.scale / (4.0 * (double)(nf - 1));
-        sfirst[threadIdx.x] = h.first;
-    }
-    __syncthreads();
+    const int j = (int)(blockIdx.x >> 3);
+    const int r = j % rows, chunk = (int)(blockIdx.x & 7) + 8 * (j / rows);
+    const HannRow h = hann_row(info, r);
+    const double c = h.scale / (4.0 * (double)(nf - 1));
+    const double2* Sr = S + (int64_t)r * stride;
+    const float2* Yr = Y + (int64_t)r * m;
     const int64_t nb = nf - k0;
-    double acc[HANN_ROWS_MAX];
-#pragma unroll
-    for (int r = 0; r < HANN_ROWS_MAX; ++r) acc[r] = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
-         i += (int64_t)gridDim.x * blockDim.x) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)chunk * 256 + threadIdx.x; i < nb; i += (int64_t)nchunk * 256) {
         const double2 d0 = d[i], d1 = d[nb + i];
         const double w0 = w[i], w1 = w[nb + i];
-#pragma unroll
-        for (int r = 0; r < HANN_ROWS_MAX; ++r) {
-            if (r < rows) {
-                double2 vp, vc;
-                hann_pol(S + (int64_t)r * stride, Y + (int64_t)r * m, nf, k0 + i, sc[r],
-                         sfirst[r], m - nf, vp, vc);
-                const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
-                const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
-                acc[r] = fma(r0, r0, fma(i0, i0, acc[r]));
-                acc[r] = fma(r1, r1, fma(i1, i1, acc[r]));
-            }
-        }
+        double2 vp, vc;
+        hann_pol(Sr, Yr, nf, k0 + i, c, h.first, m - nf, vp, vc);
+        const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
+        const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
+        acc = fma(r0, r0, fma(i0, i0, acc));
+        acc = fma(r1, r1, fma(i1, i1, acc));
     }
-    // per row: a butterfly over each wave, then the 4 waves in turn (fixed order)
-    __shared__ double red[HANN_ROWS_MAX][4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // a butterfly over each wave, then the 4 waves in turn (fixed order)
+    __shared__ double red[4];
 #pragma unroll
-    for (int r = 0; r < HANN_ROWS_MAX; ++r) {
-        if (r < rows) {
-            double v = acc[r];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (lane == 0) red[r][wv] = v;
-        }
-    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if ((int)threadIdx.x < rows)
-        part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] =
-            ((red[threadIdx.x][0] + red[threadIdx.x][1]) + red[threadIdx.x][2]) +
-            red[threadIdx.x][3];
+    if (threadIdx.x == 0 && chunk < nchunk)
+        part[(int64_t)r * nchunk + chunk] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 // fused log-likelihood partials: one workgroup per chunk, then a second pass
@@ -5762,11 +5745,14 @@ int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint
         return fail(EFD_ERR_ARG, "efd_hann_loglike: bad arguments (rows <= 16)");
     const int64_t nb = nf - k0;
     const int threads = 256;
-    const int np = (int)std::min<int64_t>(EFD_LOGLIKE_SCRATCH, (nb + threads - 1) / threads);
+    // chunks: a multiple of 8 (one per XCD in turn), at most EFD_LOGLIKE_SCRATCH per row
+    const int np = (int)std::min<int64_t>(EFD_LOGLIKE_SCRATCH,
+                                          ((nb + threads - 1) / threads + 7) / 8 * 8);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)np), dim3(threads), 0, st,
+    static_assert(EFD_LOGLIKE_SCRATCH % 8 == 0, "chunks: whole rounds of the 8 XCDs");
+    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)(np * rows)), dim3(threads), 0, st,
                        (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
-                       (const double2*)d, w, (int)rows, scratch);
+                       (const double2*)d, w, (int)rows, np, scratch);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_loglike_final, dim3((unsigned)rows), dim3(256), 0, st, scratch, np, out);
     HIP_TRY(hipGetLastError());

@@ -12,7 +12,8 @@
 //                                the -m partners, keep them while the power before them is below
 //                                (1 - eps) of the total, fold -m picks onto +m, union over knots
 //                                (few.utils.modeselector as recalled, notebook :125-127)
-// The selection bins the powers by binary exponent instead of sorting all ~7,700 per knot.
+// The selection bins the candidate powers by their top 16 bits instead of sorting all ~7,700 per
+// knot.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -72,23 +73,15 @@ extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, cons
     }
     const int np_ = nm + (int)partner_of.size();
     std::vector<unsigned char> kept(nm, 0);
-    constexpr int NB = 2048;                      // binary exponents of non-negative doubles
-    auto expo = [](double v) {
-        uint64_t u;
-        std::memcpy(&u, &v, 8);
-        return (int)((u >> 52) & 2047u);
-    };
     // the knots' selections are independent and their union is order-free: any thread count
     // gives the same kept set
     const int nth = std::max(1, std::min(t_threads, nt / 4));
 #pragma omp parallel num_threads(nth) if (nth > 1)
     {
     std::vector<unsigned char> kept_l(nm, 0);
-    std::vector<double> mag(nm), pw(np_);
-    std::vector<int32_t> idx(np_), cut(np_);
-    std::vector<int16_t> ex(np_);
-    std::vector<double> bsum(NB);
-    std::vector<int32_t> bcnt(NB);
+    std::vector<double> mag(nm), pw(np_), hs;
+    std::vector<int32_t> cand(np_), idx(np_), cut(np_), hc;
+    std::vector<uint16_t> key(np_);
 #pragma omp for schedule(static)
     for (int i = 0; i < nt; ++i) {
         magnitudes(p[i], e[i], nm, c1.data(), dn.data(), dm.data(), hl.data(), jitter, mag.data());
@@ -99,39 +92,70 @@ extern "C" int efd_host_modes(const double* p, const double* e, int32_t nt, cons
             pw[nm + j] = mag[k] * mag[k] * ym2[k];
         }
         // keep the largest while the sum before them is < (1 - eps) total: the kept set is the
-        // top-c, c = min{c : sum of the top c >= threshold}. Binned by the powers' binary
-        // exponent (one pass): every bin above the one where the running sum from the top
-        // crosses the threshold is kept whole, and only that bin is sorted.
+        // top-c, c = min{c : sum of the top c >= threshold}. The c-th largest exceeds
+        // eps total / np (the bottom np - c + 1 sum to more than eps total), so only the powers
+        // above that floor are candidates; they are binned by their top 16 bits (exponent and 4
+        // mantissa bits; 4 interleaved histograms, no store-to-load chains on equal bins), every
+        // bin above the one where the running sum from the top crosses the threshold is kept
+        // whole, and only that bin is sorted. (Round 4 binned every power by its exponent:
+        // 2.4x the time, the histogram's read-modify-write chains and the crossing bin's sort.)
         for (int k = 0; k < np_; ++k) total += pw[k];
         double need = total * (1.0 - eps);
-        std::fill(bsum.begin(), bsum.end(), 0.0);
-        std::fill(bcnt.begin(), bcnt.end(), 0);
-        for (int k = 0; k < np_; ++k) {
-            const int b = expo(pw[k]);
-            ex[k] = (int16_t)b;
-            bsum[b] += pw[k];
-            ++bcnt[b];
+        const double floor_ = eps * total / (double)np_;
+        int nc = 0;
+        for (int k = 0; k < np_; ++k) {   // branch-free compaction
+            cand[nc] = k;
+            nc += pw[k] > floor_ ? 1 : 0;
         }
-        int bcut = -1;
-        for (int b = NB - 1; b >= 0; --b) {
-            if (!bcnt[b]) continue;
-            if (bsum[b] >= need) { bcut = b; break; }
-            need -= bsum[b];
+        uint32_t kmin = 0xffffu, kmax = 0u;
+        for (int j = 0; j < nc; ++j) {
+            uint64_t u;
+            std::memcpy(&u, &pw[cand[j]], 8);
+            const uint32_t q = (uint32_t)(u >> 48);
+            key[j] = (uint16_t)q;
+            kmin = std::min(kmin, q);
+            kmax = std::max(kmax, q);
         }
         int lo = 0;
-        for (int k = 0; k < np_; ++k)
-            if (ex[k] > bcut) idx[lo++] = k;         // whole bins above the crossing
-        if (bcut >= 0) {
+        if (nc > 0) {
+            const int R = (int)(kmax - kmin) + 1;
+            hs.assign(4 * (size_t)R, 0.0);
+            hc.assign(4 * (size_t)R, 0);
+            for (int j = 0; j < nc; ++j) {
+                const int b = (int)(key[j] - kmin) * 4 + (j & 3);
+                hs[b] += pw[cand[j]];
+                ++hc[b];
+            }
+            int bcut = -1;
+            for (int b = R - 1; b >= 0; --b) {
+                const int c = hc[4 * b] + hc[4 * b + 1] + hc[4 * b + 2] + hc[4 * b + 3];
+                if (!c) continue;
+                const double sb = (hs[4 * b] + hs[4 * b + 1]) + (hs[4 * b + 2] + hs[4 * b + 3]);
+                if (sb >= need) { bcut = b; break; }
+                need -= sb;
+            }
+            const int kc = bcut + (int)kmin;
             int nb = 0;
-            for (int k = 0; k < np_; ++k)
-                if (ex[k] == bcut) cut[nb++] = k;
-            std::sort(cut.begin(), cut.begin() + nb, [&](int x, int y) { return pw[x] > pw[y]; });
-            for (int j = 0; j < nb && need > 0.0; ++j) {
-                need -= pw[cut[j]];
-                idx[lo++] = cut[j];
+            for (int j = 0; j < nc; ++j) {   // branch-free partition: above / the crossing bin
+                const int q = key[j];
+                idx[lo] = cand[j];
+                lo += q > kc ? 1 : 0;
+                cut[nb] = cand[j];
+                nb += q == kc ? 1 : 0;
+            }
+            if (bcut >= 0) {
+                std::sort(cut.begin(), cut.begin() + nb, [&](int x, int y) { return pw[x] > pw[y]; });
+                for (int j = 0; j < nb && need > 0.0; ++j) {
+                    need -= pw[cut[j]];
+                    idx[lo++] = cut[j];
+                }
             }
         }
-        if (lo == 0 && np_ > 0) lo = 1;   // the largest is always kept
+        if (lo == 0 && np_ > 0) {   // the largest is always kept
+            int best = 0;
+            for (int k = 1; k < np_; ++k) best = pw[k] > pw[best] ? k : best;
+            idx[lo++] = best;
+        }
         for (int k = 0; k < lo; ++k) {
             const int q = idx[k];
             kept_l[q < nm ? q : partner_of[q - nm]] = 1;
