@@ -2,7 +2,8 @@
 
   csrc/emrifd_cpu.cpp -> g++ -O3 -march=x86-64-v4 -fopenmp (the host twin, efd_*_cpu; AVX-512 is
                          on both this container's Sapphire Rapids and the GPU box's EPYC 9575F)
-  csrc/emrifd_host.cpp -> g++ -O3: the host upstream stand-ins (trajectory, p0 solve) in C++
+  csrc/emrifd_host.cpp -> g++ -O3 -fopenmp: the host upstream stand-ins (trajectory, p0 solve) in C++
+  and the walker batches' staging
   csrc/emrifd_modes.cpp -> g++ -O3 -ffast-math -fopenmp (libmvec; knots over threads for one-at-a-time
                           calls): amplitudes, mode selection
   csrc/emrifd.hip     -> hipcc --offload-arch=gfx950, linked with both objects and libgomp
@@ -67,8 +68,8 @@ def build(force=False, verbose=False, extra=()):
     hobj = os.path.join(OBJDIR, "emrifd_host.o")
     cpu = ["g++", "-O3", f"-march={CPU_ARCH}", "-fopenmp", "-ffp-contract=off", "-fPIC",
            "-std=c++17", "-c", CPU_SRC, "-o", obj]
-    host = ["g++", "-O3", f"-march={CPU_ARCH}", "-ffp-contract=off", "-fPIC", "-std=c++17", "-c",
-            HOST_SRC, "-o", hobj]
+    host = ["g++", "-O3", f"-march={CPU_ARCH}", "-ffp-contract=off", "-fopenmp", "-fPIC",
+            "-std=c++17", "-c", HOST_SRC, "-o", hobj]
     mobj = os.path.join(OBJDIR, "emrifd_modes.o")
     modes = ["g++", "-O3", f"-march={CPU_ARCH}", "-ffast-math", "-fopenmp", "-fPIC",
              "-std=c++17", "-c", MODES_SRC, "-o", mobj]

@@ -4703,6 +4703,140 @@ void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __r
     }
 }
 
+// (A) and (C) for R = 2048 (m = 2^24, test.sh's transform), NCOL = 4 columns per workgroup, as
+// register stages with two LDS exchanges (2048 = 16 x 16 x 8; n = n2 + 128 n1, n2 = n2a + 8 n2b;
+// k = k1 + 16 k2a + 256 k2b): forward (A) task (j, n2): DFT-16 over n1, times w_2048^(n2 k1);
+// (B) task (j, k1, n2a): DFT-16 over n2b, times w_128^(n2a k2a); (C) task (j, k1, k2a): DFT-8
+// over n2a -> f_r = k. The inverse runs the transposed steps in reverse. Exchange 1 is
+// [k1][n2][j], exchange 2 [k1][k2a][n2a (pad to 9)][j]: every LDS access of a half-wave covers
+// 64 distinct banks. Two exchanges per direction instead of the Stockham form's four passes and
+// the staging round trip (the other R keep it).
+constexpr int FCC_R = 2048, FCC_NCOL = 4, FCC_S2 = 9;
+template <bool FWD>
+__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_fc_cols2048(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
+                   float2* __restrict__ Yv) {
+    static_assert(FC_NT == 512 && FCC_R * FCC_NCOL == 16 * FC_NT, "16 elements per thread");
+    constexpr int64_t M = (int64_t)FCC_R * FC_C;
+    // exchange 1: 16 x 128 x 4 = 8192; exchange 2: 16 x 16 x 9 x 4 = 9216 elements (73.7 KB)
+    __shared__ fcv sm[16 * 16 * FCC_S2 * FCC_NCOL];
+    fcv* Y = reinterpret_cast<fcv*>(Yv);
+    const int row = blockIdx.y;
+    constexpr int G = FC_C / FCC_NCOL;
+    static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
+    const int c0 = ((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * FCC_NCOL;
+    fcv* y = Y + (int64_t)row * M;
+    const int t = threadIdx.x;
+    const int j = t & 3;
+    constexpr float W2048 = FC_2PI / 2048.0f, W128 = FC_2PI / 128.0f;
+    auto e1 = [](int k1, int n2, int jj) { return (k1 * 128 + n2) * FCC_NCOL + jj; };
+    auto e2 = [](int k1, int k2a, int n2a, int jj) {
+        return ((k1 * 16 + k2a) * FCC_S2 + n2a) * FCC_NCOL + jj;
+    };
+    if (FWD) {
+        const HannRow h = hann_row(info, row);
+        const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;
+        const double2* src = S + (int64_t)row * stride + h.first;
+        const bool bad = h.len > M;
+        {   // (A): task (j, n2)
+            const int n2 = t >> 2;
+            fcv v[16];
+#pragma unroll
+            for (int n1 = 0; n1 < 16; ++n1) {
+                const int64_t s = (int64_t)(n2 + 128 * n1) * FC_C + c0 + j;
+                fcv x = {0.f, 0.f};
+                if (bad) {
+                    x = (fcv){__int_as_float(0x7fc00000), 0.f};
+                } else if (s < h.len) {
+                    const double2 d = src[s];
+                    x = (fcv){(float)(d.x * inv), (float)(d.y * inv)};
+                }
+                v[n1] = x;
+            }
+            fc_dft16<-1>(v);
+            fc_twiddle_pow<16>(v, -W2048 * (float)n2);
+#pragma unroll
+            for (int k1 = 0; k1 < 16; ++k1) sm[e1(k1, n2, j)] = v[k1];
+        }
+        __syncthreads();
+        fcv u[16];
+        const int n2a = (t >> 2) & 7, k1b = t >> 5;
+#pragma unroll
+        for (int n2b = 0; n2b < 16; ++n2b) u[n2b] = sm[e1(k1b, n2a + 8 * n2b, j)];
+        __syncthreads();
+        fc_dft16<-1>(u);
+        fc_twiddle_pow<16>(u, -W128 * (float)n2a);
+#pragma unroll
+        for (int k2a = 0; k2a < 16; ++k2a) sm[e2(k1b, k2a, n2a, j)] = u[k2a];
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // (C): tasks (j, k2a, k1), two per thread
+            const int q = t + FC_NT * hh;
+            const int k2a = (q >> 2) & 15, k1 = q >> 6;
+            fcv w[8];
+#pragma unroll
+            for (int a = 0; a < 8; ++a) w[a] = sm[e2(k1, k2a, a, j)];
+            fc_dft8<-1>(w);
+#pragma unroll
+            for (int k2b = 0; k2b < 8; ++k2b) {
+                const int fr = k1 + 16 * k2a + 256 * k2b;
+                const int c = c0 + j;
+                const uint32_t pp = (uint32_t)c * (uint32_t)fr;   // < C R = M: no reduction
+                float sn, cs;
+                __sincosf(-FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
+                y[(int64_t)fr * FC_C + c] = cmulf(w[k2b], (fcv){cs, sn});
+            }
+        }
+    } else {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // inverse (C): tasks (j, k2a, k1)
+            const int q = t + FC_NT * hh;
+            const int k2a = (q >> 2) & 15, k1 = q >> 6;
+            fcv w[8];
+#pragma unroll
+            for (int k2b = 0; k2b < 8; ++k2b) {
+                const int fr = k1 + 16 * k2a + 256 * k2b;
+                const int c = c0 + j;
+                const uint32_t pp = (uint32_t)c * (uint32_t)fr;
+                float sn, cs;
+                __sincosf(FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
+                w[k2b] = cmulf(y[(int64_t)fr * FC_C + c], (fcv){cs, sn});
+            }
+            fc_dft8<1>(w);   // -> n2a
+            fc_twiddle_pow<8>(w, W128 * (float)k2a);
+#pragma unroll
+            for (int a = 0; a < 8; ++a) sm[e2(k1, k2a, a, j)] = w[a];
+        }
+        __syncthreads();
+        fcv u[16];
+        const int n2a = (t >> 2) & 7, k1b = t >> 5;
+#pragma unroll
+        for (int k2a = 0; k2a < 16; ++k2a) u[k2a] = sm[e2(k1b, k2a, n2a, j)];
+        __syncthreads();
+        fc_dft16<1>(u);   // -> n2b
+        {   // times w_2048^(-n2 k1), n2 = n2a + 8 n2b
+            float s0, cz;
+            __sincosf(W2048 * (float)(n2a * k1b), &s0, &cz);
+            const fcv w0 = {cz, s0};
+#pragma unroll
+            for (int n2b = 0; n2b < 16; ++n2b) u[n2b] = cmulf(u[n2b], w0);
+            fc_twiddle_pow<16>(u, W2048 * 8.0f * (float)k1b);
+        }
+#pragma unroll
+        for (int n2b = 0; n2b < 16; ++n2b) sm[e1(k1b, n2a + 8 * n2b, j)] = u[n2b];
+        __syncthreads();
+        {   // inverse (A): task (j, n2) -> r = n2 + 128 n1
+            const int n2 = t >> 2;
+            fcv v[16];
+#pragma unroll
+            for (int k1 = 0; k1 < 16; ++k1) v[k1] = sm[e1(k1, n2, j)];
+            fc_dft16<1>(v);
+#pragma unroll
+            for (int n1 = 0; n1 < 16; ++n1) y[(int64_t)(n2 + 128 * n1) * FC_C + c0 + j] = v[n1];
+        }
+    }
+}
+
 // S_w at bin k: the 3-point stencil on S and the correction's difference (neighbours mod nf)
 __device__ __forceinline__ double2 hann_sw(const double2* __restrict__ S,
                                            const float2* __restrict__ Y, int64_t nf, int64_t k,
@@ -5690,6 +5824,15 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }
+// the register-staged column kernels at R = 2048 (EFD_FC_COLS=0: the Stockham ones, an
+// experiment switch for paired A/B runs; read once)
+static bool fc_cols_staged() {
+    static const bool v = [] {
+        const char* e = getenv("EFD_FC_COLS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream) {
     if (!hann_rows_ok("efd_hann_convolve", S, stride, nf, rows) || !info || !kfp || !Y ||
@@ -5717,7 +5860,22 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         case 256: EFD_FC(256); break;
         case 512: EFD_FC(512); break;
         case 1024: EFD_FC(1024); break;
-        case 2048: EFD_FC(2048); break;
+        case 2048:
+            if (fc_cols_staged()) {
+                hipLaunchKernelGGL((k_fc_cols2048<true>), dim3(FC_C / FCC_NCOL, (unsigned)rows),
+                                   dim3(FC_NT), 0, st, (const double2*)S, stride, info, y);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_fc_rows, dim3(2048 * (unsigned)rows), dim3(FR_NT), 0, st,
+                                   (const float2*)kfp, m, (int)rows, y);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL((k_fc_cols2048<false>), dim3(FC_C / FCC_NCOL, (unsigned)rows),
+                                   dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,
+                                   (const uint64_t*)nullptr, y);
+                HIP_TRY(hipGetLastError());
+            } else {
+                EFD_FC(2048);
+            }
+            break;
         default: EFD_FC(4096); break;
     }
 #undef EFD_FC

@@ -327,18 +327,33 @@ int efd_stage_batch(void* pin, size_t pin_bytes, uint64_t dev_base, int32_t coun
     *total = off;
     if (!pin || off > pin_bytes) return EFD_ERR_WORKSPACE;
     char* dst = (char*)pin;
-    off = 0;
+    // each walker's offset (the sizes pass above, again), then the copies: walkers over OpenMP
+    // threads when the batch is large (config 5's groups of 16: ~2-4 MB, one thread's memcpy
+    // bandwidth made the copy most of the group's flush)
+    std::vector<size_t> woff((size_t)count + 1, 0);
+    for (int i = 0; i < count; ++i) {
+        const size_t nt = (size_t)shape[2 * i], K = (size_t)shape[2 * i + 1];
+        const size_t bytes[10] = {8 * nt, 8 * nt, 8 * nt, 8 * nt, 8 * nt, 16 * nt * K,
+                                  4 * K, 4 * K, 16 * K, 16 * K};
+        size_t o = woff[i];
+        for (int f = 0; f < 10; ++f) o = al(o + bytes[f]);
+        woff[i + 1] = o;
+        for (int f = 0; f < 10; ++f)
+            if (!src[10 * (size_t)i + f]) return EFD_ERR_ARG;
+    }
+    const int nth = off >= ((size_t)1 << 20) ? std::min(count, 8) : 1;
+#pragma omp parallel for num_threads(nth) schedule(static) if (nth > 1)
     for (int i = 0; i < count; ++i) {
         const size_t nt = (size_t)shape[2 * i], K = (size_t)shape[2 * i + 1];
         const size_t bytes[10] = {8 * nt, 8 * nt, 8 * nt, 8 * nt, 8 * nt, 16 * nt * K,
                                   4 * K, 4 * K, 16 * K, 16 * K};
         uint64_t dp[10];
+        size_t o = woff[i];
         for (int f = 0; f < 10; ++f) {
             const void* sp = (const void*)(uintptr_t)src[10 * (size_t)i + f];
-            if (!sp) return EFD_ERR_ARG;
-            std::memcpy(dst + off, sp, bytes[f]);
-            dp[f] = dev_base + off;
-            off = al(off + bytes[f]);
+            std::memcpy(dst + o, sp, bytes[f]);
+            dp[f] = dev_base + o;
+            o = al(o + bytes[f]);
         }
         efd_modesum_args& a = args[i];
         a = *tmpl;
