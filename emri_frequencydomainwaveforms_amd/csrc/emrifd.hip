@@ -4837,15 +4837,20 @@ void k_fc_cols2048(const double2* __restrict__ S, int64_t stride, const uint64_t
     }
 }
 
-// S_w at bin k: the 3-point stencil on S and the correction's difference (neighbours mod nf)
+// S_w at bin k: the 3-point stencil on S and the correction's difference (neighbours mod nf).
+// S is zero outside the row's support [first, first + len) (cyclic; efd_hann_extent's bounds),
+// so it is read only there: the support is ~40% of test.sh's grid, and the skipped reads were
+// half of the reduction's HBM bytes (the correction C = Y is nonzero everywhere)
 __device__ __forceinline__ double2 hann_sw(const double2* __restrict__ S,
                                            const float2* __restrict__ Y, int64_t nf, int64_t k,
-                                           double c, int64_t first, int64_t off) {
+                                           double c, int64_t first, int64_t len, int64_t off) {
     const int64_t kp = k + 1 < nf ? k + 1 : 0, km = k > 0 ? k - 1 : nf - 1;
-    int64_t qp = kp - first, qm = km - first;
+    int64_t qp = kp - first, qm = km - first, q0 = k - first;
     qp += qp < 0 ? nf : 0;
     qm += qm < 0 ? nf : 0;
-    const double2 s = S[k], sp = S[kp], sm = S[km];
+    q0 += q0 < 0 ? nf : 0;
+    const double2 z = make_double2(0.0, 0.0);
+    const double2 s = q0 < len ? S[k] : z, sp = qp < len ? S[kp] : z, sm = qm < len ? S[km] : z;
     const float2 cp = Y[qp + off], cm = Y[qm + off];
     return make_double2(0.5 * s.x - 0.25 * (sp.x + sm.x) - c * ((double)cp.x - (double)cm.x),
                         0.5 * s.y - 0.25 * (sp.y + sm.y) - c * ((double)cp.y - (double)cm.y));
@@ -4853,10 +4858,10 @@ __device__ __forceinline__ double2 hann_sw(const double2* __restrict__ S,
 // h+ = (a + conj b)/2, hx = i (a - conj b)/2 of the windowed spectrum at k (a) and nf-1-k (b)
 __device__ __forceinline__ void hann_pol(const double2* __restrict__ S,
                                          const float2* __restrict__ Y, int64_t nf, int64_t k,
-                                         double c, int64_t first, int64_t off, double2& vp,
-                                         double2& vc) {
-    const double2 a = hann_sw(S, Y, nf, k, c, first, off);
-    const double2 b = hann_sw(S, Y, nf, nf - 1 - k, c, first, off);
+                                         double c, int64_t first, int64_t len, int64_t off,
+                                         double2& vp, double2& vc) {
+    const double2 a = hann_sw(S, Y, nf, k, c, first, len, off);
+    const double2 b = hann_sw(S, Y, nf, nf - 1 - k, c, first, len, off);
     vp = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
     vc = make_double2(-0.5 * (a.y + b.y), 0.5 * (a.x - b.x));
 }
@@ -4870,7 +4875,7 @@ __global__ void k_hann_polarizations(const double2* __restrict__ S, const float2
     const HannRow h = hann_row(info, 0);
     const double c = h.scale / (4.0 * (double)(nf - 1));
     double2 vp, vc;
-    hann_pol(S, Y, nf, k, c, h.first, m - nf, vp, vc);
+    hann_pol(S, Y, nf, k, c, h.first, h.len, m - nf, vp, vc);
     hp[i] = vp;
     hc[i] = vc;
 }
@@ -4900,7 +4905,7 @@ __global__ __launch_bounds__(256) void k_hann_loglike_partial(
         const double2 d0 = d[i], d1 = d[nb + i];
         const double w0 = w[i], w1 = w[nb + i];
         double2 vp, vc;
-        hann_pol(Sr, Yr, nf, k0 + i, c, h.first, m - nf, vp, vc);
+        hann_pol(Sr, Yr, nf, k0 + i, c, h.first, h.len, m - nf, vp, vc);
         const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
         const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
         acc = fma(r0, r0, fma(i0, i0, acc));
@@ -5868,9 +5873,11 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                 hipLaunchKernelGGL(k_fc_rows, dim3(2048 * (unsigned)rows), dim3(FR_NT), 0, st,
                                    (const float2*)kfp, m, (int)rows, y);
                 HIP_TRY(hipGetLastError());
-                hipLaunchKernelGGL((k_fc_cols2048<false>), dim3(FC_C / FCC_NCOL, (unsigned)rows),
-                                   dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,
-                                   (const uint64_t*)nullptr, y);
+                // the inverse pass stays on the Stockham kernel: its staged form measured 649
+                // against 611 us (r05l; both at ~0.6 of HBM, bound by the 32-B column segments)
+                hipLaunchKernelGGL((k_fc_cols<false, 2048>), dim3(FC_C / FcCols<2048>::NCOL,
+                                   (unsigned)rows), dim3(FC_NT), 0, st, (const double2*)nullptr,
+                                   (int64_t)0, (const uint64_t*)nullptr, y);
                 HIP_TRY(hipGetLastError());
             } else {
                 EFD_FC(2048);
