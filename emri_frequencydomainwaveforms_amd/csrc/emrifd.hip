@@ -63,7 +63,10 @@ constexpr int NWAVE = TILE / 64;    // waves per workgroup
 // bins (lanes) per thread in k_modesum. Round 4: 3 with the own/mirror amplitude cubics split
 // (below) fits the 128-VGPR budget without spills in the record loop: config 2 +2.1-2.4% over 2
 // (paired A/B, 3 rounds on two boxes, profiles/r04_ab_bpl3.jsonl); 4 spilled (-4%)
-constexpr int BPL = 3;
+#ifndef EFD_BPL
+#define EFD_BPL 3   // (an experiment switch: -DEFD_BPL=4)
+#endif
+constexpr int BPL = EFD_BPL;
 constexpr int TILE_LANES = TILE * BPL;  // frequency bins (lanes) per tile
 // k_modesum's packed chunk record header (one word per record, read by v_readlane): the
 // sub-branch's lane range relative to the tile (HDR_HB bits each), s, the series length J (3
@@ -2805,7 +2808,9 @@ template <bool PAIRED, int CAUSTIC, int NB = BPL>
 // 37.6 KB of LDS per workgroup 4 workgroups fit a CU, and the fourth wave hides more FP64
 // latency than the spills cost (config 2: 1.00 ms against 1.09 ms at 3 waves / 147 VGPRs;
 // 5 waves with a one-round stage: 1.07 ms)
+#ifndef EFD_WAVES_PER_EU
 #define EFD_WAVES_PER_EU 4
+#endif
 // 1: the tiles' record lists are built by k_tile_keys in the preparation phase and DMA'd in by
 // the sum; tiles whose list needs more than one KEYCAP pass or has more than TK_HITS segments
 // (tcnt = -1) build it in the sum as before. 0: always in the sum.
