@@ -639,11 +639,17 @@ class BatchPreparer:
         return self.groups[gi]["stream"]
 
     # -- one batch -----------------------------------------------------------------------------
+    # optional section timers of flush (tools/halfstep_host.py sets a dict: seconds per section)
+    FLUSH_TIMERS = None
+
     def flush(self):
         """Upload and prepare the collected walkers; returns (group index, jobs). A job's
         argument struct lives in the group's reused array: use the jobs before the group's next
         flush (sum_batch / sum_batch_loglike copy what they need)."""
         import ctypes
+        import time
+        T = self.FLUSH_TIMERS
+        t_0 = time.perf_counter() if T is not None else 0.0
         torch = _torch()
         pend, self._pending = self._pending, []
         if not pend:
@@ -709,6 +715,9 @@ class BatchPreparer:
                 keep.append(arrays)
                 src[i] = [a.ctypes.data for a in arrays]
                 shape[i] = (nt, K)
+        if T is not None:
+            t_1 = time.perf_counter()
+            T["wait+src"] = T.get("wait+src", 0.0) + t_1 - t_0
         total = ctypes.c_size_t(0)
         for attempt in range(2):
             pin = G["pin"]
@@ -727,6 +736,9 @@ class BatchPreparer:
             with torch.cuda.stream(st):
                 G["dbuf"] = torch.empty(cap, dtype=torch.uint8, device=self.device)
         del keep
+        if T is not None:
+            t_2 = time.perf_counter()
+            T["stage"] = T.get("stage", 0.0) + t_2 - t_1
         _lib.check(self.lib.efd_upload(G["dbuf"].data_ptr(), G["pin"].data_ptr(), total.value,
                                        st.cuda_stream), "efd_upload", self.lib)
         if G["pin_done"] is None:
@@ -736,6 +748,9 @@ class BatchPreparer:
         if "A_i" not in G:   # stable views of the group's argument structs, made once
             G["A_i"] = [A[i] for i in range(self.group)]
         A_i, engines = G["A_i"], G["engines"]
+        if T is not None:
+            t_3 = time.perf_counter()
+            T["upload+event"] = T.get("upload+event", 0.0) + t_3 - t_2
         jobs = []
         dev = freq.device
         for i, (nt_i, K_i) in enumerate(shape.tolist()):
@@ -748,8 +763,13 @@ class BatchPreparer:
             a_i = A_i[i]
             eng._last_args = a_i
             jobs.append((eng, {"freq": freq, "k0": k0, "grid_symmetric": sym, "_args": a_i}))
+        if T is not None:
+            t_4 = time.perf_counter()
+            T["jobs"] = T.get("jobs", 0.0) + t_4 - t_3
         _lib.check(self.lib.efd_modesum_prepare_batch(G["pa"], ctypes.cast(pw, ctypes.POINTER(
             ctypes.c_void_p)), pb, n, st.cuda_stream), "efd_modesum_prepare_batch", self.lib)
+        if T is not None:
+            T["prepare_batch"] = T.get("prepare_batch", 0.0) + time.perf_counter() - t_4
         G["used"] = True
         G["n"] = n
         self.last_jobs = jobs

@@ -90,10 +90,12 @@ for i in range(5):
     s.like(batches[i % len(batches)], **s.kwargs)
 torch.cuda.synchronize()
 acc.clear()
+ft = BatchPreparer.FLUSH_TIMERS = {}
 N = 40
 t0 = pc()
 for i in range(N):
     s.like(batches[i % len(batches)], **s.kwargs)
 wall = pc() - t0
 print(json.dumps({"cfg": sys.argv[1:], "walkers": s.half_step, "ms_per_half_step": wall / N * 1e3,
-                  "us_per_half_step": {k: v / N * 1e6 for k, v in acc.items()}}, indent=1))
+                  "us_per_half_step": {k: v / N * 1e6 for k, v in acc.items()},
+                  "flush_us_per_half_step": {k: v / N * 1e6 for k, v in ft.items()}}, indent=1))
