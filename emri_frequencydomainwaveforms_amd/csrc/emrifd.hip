@@ -2132,6 +2132,9 @@ __global__ __launch_bounds__(SEG1_NT) void k_segments_one(const PrepBatch B) {
         my_items += nS[i];
         my_split += S > 1 ? 1 : 0;
     }
+    // no tile above the share (config 4's full grid: costs within 1.5x of the median): no plan,
+    // and none of the scans below
+    if (!__syncthreads_or(my_split > 0)) return;
     int n_items, n_split;
     const int io = seg1_excl_scan(my_items, wsum, n_items);
     const int po = seg1_excl_scan(my_split, wsum, n_split);
