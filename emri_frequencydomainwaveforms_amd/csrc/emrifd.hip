@@ -4711,96 +4711,6 @@ void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __r
     }
 }
 
-// k_fc_rows with each exchange done in two halves of k1 (34.8 KB of LDS instead of 65.8: three
-// workgroups per CU instead of two, at twice the barriers). Same tasks and arithmetic, so the
-// same values bit for bit; the B/C tasks of half h are k1 = (t & 15) + 16 h.
-constexpr int FRH_S1 = 258, FRH_S2 = 17;   // exchange 1 [k1 % 16][n2]; exchange 2 [k2a][n2a][k1 % 16]
-__global__ __launch_bounds__(FR_NT) __attribute__((amdgpu_waves_per_eu(3, 8)))
-void k_fc_rows_h(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
-    __shared__ fcv sm[(15 * 16 + 15) * FRH_S2 + 16];
-    const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
-    fcv* Y = reinterpret_cast<fcv*>(Yv);
-    const int64_t npair = (int64_t)gridDim.x;
-    const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
-    const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
-    fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C;
-    const fcv* kr = kfp + (int64_t)fr * FC_C;
-    const int t = threadIdx.x;
-    const int kl = t & 15, hi = t >> 4;   // B tasks: (kl + 16 h, n2a = hi); C tasks: (kl + 16 h, k2a = hi)
-    constexpr float W8192 = FC_2PI / 8192.0f, W256 = FC_2PI / 256.0f;
-    fcv v[32];
-#pragma unroll
-    for (int n1 = 0; n1 < 32; ++n1) v[n1] = y[t + 256 * n1];
-    fc_dft32<-1>(v);
-    fc_twiddle_pow<32>(v, -W8192 * (float)t);
-    fcv u[2][16];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // exchange 1, half h: forward (B)'s inputs
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) sm[kk * FRH_S1 + t] = v[16 * h + kk];
-        __syncthreads();
-#pragma unroll
-        for (int n2b = 0; n2b < 16; ++n2b) u[h][n2b] = sm[kl * FRH_S1 + hi + 16 * n2b];
-        __syncthreads();
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // forward (B): n2a = hi
-        fc_dft16<-1>(u[h]);
-        fc_twiddle_pow<16>(u[h], -W256 * (float)hi);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // exchange 2, half h; forward (C) reads k2a = hi
-#pragma unroll
-        for (int k2a = 0; k2a < 16; ++k2a) sm[(k2a * 16 + hi) * FRH_S2 + kl] = u[h][k2a];
-        __syncthreads();
-#pragma unroll
-        for (int n2a = 0; n2a < 16; ++n2a) u[h][n2a] = sm[(hi * 16 + n2a) * FRH_S2 + kl];
-        __syncthreads();
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // forward (C), the kernel's spectrum, inverse (C)
-        const int k1 = kl + 16 * h, k2a = hi;
-        fc_dft16<-1>(u[h]);
-#pragma unroll
-        for (int k2b = 0; k2b < 16; ++k2b)
-            u[h][k2b] = cmulf(u[h][k2b], kr[k1 + 32 * k2a + 512 * k2b]);
-        fc_dft16<1>(u[h]);
-        fc_twiddle_pow<16>(u[h], W256 * (float)k2a);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // exchange 2 back; inverse (B) reads n2a = hi
-#pragma unroll
-        for (int n2a = 0; n2a < 16; ++n2a) sm[(hi * 16 + n2a) * FRH_S2 + kl] = u[h][n2a];
-        __syncthreads();
-#pragma unroll
-        for (int k2a = 0; k2a < 16; ++k2a) u[h][k2a] = sm[(k2a * 16 + hi) * FRH_S2 + kl];
-        __syncthreads();
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // inverse (B) -> n2b, times w_8192^(-n2 k1)
-        const int k1 = kl + 16 * h, n2a = hi;
-        fc_dft16<1>(u[h]);
-        float s0, c0;
-        __sincosf(W8192 * (float)(n2a * k1), &s0, &c0);
-        const fcv w0 = {c0, s0};
-#pragma unroll
-        for (int n2b = 0; n2b < 16; ++n2b) u[h][n2b] = cmulf(u[h][n2b], w0);
-        fc_twiddle_pow<16>(u[h], W8192 * 16.0f * (float)k1);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // exchange 1 back; inverse (A) reads n2 = t
-#pragma unroll
-        for (int n2b = 0; n2b < 16; ++n2b) sm[kl * FRH_S1 + hi + 16 * n2b] = u[h][n2b];
-        __syncthreads();
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) v[16 * h + kk] = sm[kk * FRH_S1 + t];
-        __syncthreads();
-    }
-    fc_dft32<1>(v);
-#pragma unroll
-    for (int n1 = 0; n1 < 32; ++n1) y[t + 256 * n1] = v[n1];
-}
-
 // (A) and (C) for R = 2048 (m = 2^24, test.sh's transform), NCOL = 4 columns per workgroup, as
 // register stages with two LDS exchanges (2048 = 16 x 16 x 8; n = n2 + 128 n1, n2 = n2a + 8 n2b;
 // k = k1 + 16 k2a + 256 k2b): forward (A) task (j, n2): DFT-16 over n1, times w_2048^(n2 k1);
@@ -5927,14 +5837,6 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }
-// the row kernel with half-size exchanges (EFD_FC_ROWS=half; an experiment switch, read once)
-static bool fc_rows_half() {
-    static const bool v = [] {
-        const char* e = getenv("EFD_FC_ROWS");
-        return e && std::string(e) == "half";
-    }();
-    return v;
-}
 // the register-staged column kernels at R = 2048 (EFD_FC_COLS=0: the Stockham ones, an
 // experiment switch for paired A/B runs; read once)
 static bool fc_cols_staged() {
@@ -5959,8 +5861,8 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         hipLaunchKernelGGL((k_fc_cols<true, RR>), dim3(FC_C / NC, (unsigned)rows), dim3(FC_NT), \
                            0, st, (const double2*)S, stride, info, y);                        \
         HIP_TRY(hipGetLastError());                                                           \
-        hipLaunchKernelGGL(fc_rows_half() ? k_fc_rows_h : k_fc_rows, dim3(RR * (unsigned)rows),  \
-                           dim3(FR_NT), 0, st, (const float2*)kfp, m, (int)rows, y);          \
+        hipLaunchKernelGGL(k_fc_rows, dim3(RR * (unsigned)rows), dim3(FR_NT), 0, st,          \
+                           (const float2*)kfp, m, (int)rows, y);                              \
         HIP_TRY(hipGetLastError());                                                           \
         hipLaunchKernelGGL((k_fc_cols<false, RR>), dim3(FC_C / NC, (unsigned)rows),          \
                            dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,           \
@@ -5976,8 +5878,7 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                 hipLaunchKernelGGL((k_fc_cols2048<true>), dim3(FC_C / FCC_NCOL, (unsigned)rows),
                                    dim3(FC_NT), 0, st, (const double2*)S, stride, info, y);
                 HIP_TRY(hipGetLastError());
-                hipLaunchKernelGGL(fc_rows_half() ? k_fc_rows_h : k_fc_rows,
-                                   dim3(2048 * (unsigned)rows), dim3(FR_NT), 0, st,
+                hipLaunchKernelGGL(k_fc_rows, dim3(2048 * (unsigned)rows), dim3(FR_NT), 0, st,
                                    (const float2*)kfp, m, (int)rows, y);
                 HIP_TRY(hipGetLastError());
                 // the inverse pass stays on the Stockham kernel: its staged form measured 649
