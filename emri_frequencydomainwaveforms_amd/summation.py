@@ -685,20 +685,21 @@ class BatchPreparer:
             raise ValueError("flush: grid symmetry, k0 and accumulate must agree in a group")
         keep = []    # arrays converted here stay alive until the staging copy below
         fast = [p[0].get("_src") for p in pend]
-        scale = np.array([(p[3].real, p[3].imag) for p in pend], dtype=np.float64)
-        allfast = all(f is not None for f in fast)
+        scale = np.array([p[3] for p in pend], dtype=np.complex128).view(np.float64)
+        allfast = None not in fast
         if allfast:
-            # the native upstream's walkers (prepare() records their arrays' addresses): one
-            # conversion for the group instead of row by row
-            src = np.array(fast, dtype=np.uint64)
-            shape = np.array([p[0]["_shape"] for p in pend], dtype=np.int32)
+            # the native upstream's walkers (prepare() packs their arrays' addresses and shape
+            # as bytes): one join per group instead of a conversion row by row
+            src = np.frombuffer(b"".join(fast), dtype=np.uint64)
+            shape = np.frombuffer(b"".join([p[0]["_shape"] for p in pend]),
+                                  dtype=np.int32).reshape(n, 2)
         else:
             src = np.empty((n, 10), dtype=np.uint64)
             shape = np.empty((n, 2), dtype=np.int32)
         for i, (host, _, _, sc, _, _) in enumerate(() if allfast else pend):
             if fast[i] is not None:
-                src[i] = fast[i]
-                shape[i] = host["_shape"]
+                src[i] = np.frombuffer(fast[i], dtype=np.uint64)
+                shape[i] = np.frombuffer(host["_shape"], dtype=np.int32)
             else:
                 amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
                 nt, K = amps.shape

@@ -147,8 +147,9 @@ class FastSchwarzschildEccentricFlux:
             if all(a.flags.c_contiguous and a.dtype == dt for a, dt in zip(arrs, dts)):
                 k = len(keep)
                 ptr = [a.ctypes.data for a in arrs]
-                d["_src"] = ptr + [ptr[-1] + 16 * k]
-                d["_shape"] = (len(t), k)
+                # as packed bytes: the group's flush joins its walkers' in one call
+                d["_src"] = np.array(ptr + [ptr[-1] + 16 * k], dtype=np.uint64).tobytes()
+                d["_shape"] = np.array((len(t), k), dtype=np.int32).tobytes()
             return d
         t, p, e, x, Phi_phi, Phi_theta, Phi_r = self.inspiral_generator(
             M, mu, 0.0, p0, e0, 1.0, Phi_phi0=Phi_phi0, Phi_r0=Phi_r0, T=T)
@@ -405,6 +406,11 @@ class GenerateEMRIWaveform:
             raise ValueError("submit_batch needs a symmetric grid (the fused likelihood's)")
         kc = cw._k0
         submit = preparer.submit
+        # the native upstream's walkers go straight onto the preparer's pending list (what
+        # submit(d, freq, True, scale, k0=kc, prepare_only=True) appends, without its argument
+        # handling per walker)
+        pend = getattr(preparer, "_pending", None)
+        room = getattr(preparer, "group", 0)
         for prm in np.asarray(params, dtype=np.float64).reshape(-1, 14).tolist():
             M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
             theta, phi, rot = self._angles(qS, phiS, qK, phiK)
@@ -414,7 +420,10 @@ class GenerateEMRIWaveform:
             if "_src" in d:
                 # the native upstream recorded its arrays' addresses: the preparer stages them
                 # straight from prepare()'s dict
-                submit(d, freq, True, scale, k0=kc, prepare_only=True)
+                if pend is not None and len(pend) < room:
+                    pend.append((d, freq, True, complex(scale), int(kc), False))
+                else:
+                    submit(d, freq, True, scale, k0=kc, prepare_only=True)
                 continue
             K = len(d["m"])
             y = d["ylms"]
