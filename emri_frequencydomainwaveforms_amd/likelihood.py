@@ -249,7 +249,7 @@ class Likelihood:
     # Balanced groups of at most 16 (EFD_BATCH_MAX): config 5's 64-walker half-steps (host-bound,
     # 43-tile grids) ran 54-60 k logL/s in 4 groups against 40-51 k in 8 (5 interleaved rounds);
     # config 4's 8 walkers are one group either way (groups of 4 or 3: -5 to -10%)
-    FUSED_GROUP = min(max(1, int(os.environ.get("EFD_FUSED_GROUP", "16"))), 16)
+    FUSED_GROUP = min(max(1, int(os.environ.get("EFD_FUSED_GROUP", "16"))), 64)
     FUSED_DEPTH = 2
     # each group's sum on the group's own stream, right behind its preparation: no
     # cross-stream wait between the two (~12 us of idle device per group on config 4's chain,

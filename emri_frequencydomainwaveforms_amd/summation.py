@@ -599,10 +599,14 @@ class BatchPreparer:
     copies and one argument struct instead of ~10 launches (efd_modesum_prepare).
     """
 
+    # walkers per flush: up to GROUP_MAX, staged and uploaded together; the preparation and sum
+    # launches take them EFD_BATCH_MAX at a time (the kernels' argument limit)
+    GROUP_MAX = 4 * _lib.EFD_BATCH_MAX
+
     def __init__(self, group=8, depth=2, caustic="uniform", device=None):
         torch = require_gpu()
-        if not 1 <= group <= _lib.EFD_BATCH_MAX or depth < 1:
-            raise ValueError(f"group must be in 1..{_lib.EFD_BATCH_MAX}, depth >= 1")
+        if not 1 <= group <= self.GROUP_MAX or depth < 1:
+            raise ValueError(f"group must be in 1..{self.GROUP_MAX}, depth >= 1")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.caustic = caustic
         self.group = group
@@ -767,8 +771,9 @@ class BatchPreparer:
         if T is not None:
             t_4 = time.perf_counter()
             T["jobs"] = T.get("jobs", 0.0) + t_4 - t_3
-        _lib.check(self.lib.efd_modesum_prepare_batch(G["pa"], ctypes.cast(pw, ctypes.POINTER(
-            ctypes.c_void_p)), pb, n, st.cuda_stream), "efd_modesum_prepare_batch", self.lib)
+        for c0, cnt, pa_c, pw_c, pb_c in self._chunks(G, n):
+            _lib.check(self.lib.efd_modesum_prepare_batch(pa_c, pw_c, pb_c, cnt, st.cuda_stream),
+                       "efd_modesum_prepare_batch", self.lib)
         if T is not None:
             T["prepare_batch"] = T.get("prepare_batch", 0.0) + time.perf_counter() - t_4
         G["used"] = True
@@ -787,16 +792,35 @@ class BatchPreparer:
         A = G["args"]
         nb = int(A[0].nf) - int(A[0].k0)
         _check_ll_io(torch, d, w, out, nb, n)
-        if tile_const is None:
-            _lib.check(self.lib.efd_modesum_sum_loglike(
-                G["pa"], ctypes.cast(G["pw"], ctypes.POINTER(ctypes.c_void_p)), G["pb"], n,
-                torch.view_as_real(d).data_ptr(), w.data_ptr(), out.data_ptr(), stream),
-                "efd_modesum_sum_loglike", self.lib)
-        else:   # (checked by the caller that made them for this grid: no per-call recount)
-            _lib.check(self.lib.efd_modesum_sum_loglike_ex(
-                G["pa"], ctypes.cast(G["pw"], ctypes.POINTER(ctypes.c_void_p)), G["pb"], n,
-                torch.view_as_real(d).data_ptr(), w.data_ptr(), tile_const.data_ptr(),
-                out.data_ptr(), stream), "efd_modesum_sum_loglike_ex", self.lib)
+        dp, wp, op = torch.view_as_real(d).data_ptr(), w.data_ptr(), out.data_ptr()
+        for c0, cnt, pa_c, pw_c, pb_c in self._chunks(G, n):
+            if tile_const is None:
+                _lib.check(self.lib.efd_modesum_sum_loglike(pa_c, pw_c, pb_c, cnt, dp, wp,
+                                                            op + 8 * c0, stream),
+                           "efd_modesum_sum_loglike", self.lib)
+            else:   # (checked by the caller that made them for this grid: no per-call recount)
+                _lib.check(self.lib.efd_modesum_sum_loglike_ex(
+                    pa_c, pw_c, pb_c, cnt, dp, wp, tile_const.data_ptr(), op + 8 * c0, stream),
+                    "efd_modesum_sum_loglike_ex", self.lib)
+
+    def _chunks(self, G, n):
+        """(first, count, args**, workspaces*, bytes*) per launch of at most EFD_BATCH_MAX of the
+        group's first n walkers (pointers into the group's arrays; made once per (group, n))."""
+        import ctypes
+        key = ("chunks", n)
+        ch = G.get(key)
+        if ch is None:
+            ch = []
+            step = _lib.EFD_BATCH_MAX
+            pa0 = ctypes.cast(G["pa"], ctypes.c_void_p).value
+            pw0, pb0 = ctypes.addressof(G["pw"]), ctypes.addressof(G["pb"])
+            for c0 in range(0, n, step):
+                ch.append((c0, min(step, n - c0),
+                           ctypes.cast(pa0 + 8 * c0, type(G["pa"])),
+                           ctypes.cast(pw0 + 8 * c0, ctypes.POINTER(ctypes.c_void_p)),
+                           ctypes.cast(pb0 + 8 * c0, ctypes.POINTER(ctypes.c_size_t))))
+            G[key] = ch
+        return ch
 
     def release(self, gi, event):
         """The group's workspaces and inputs are free again once `event` (recorded after the sum
@@ -810,10 +834,12 @@ class BatchPreparer:
             wss = [eng._ws.data_ptr() for eng in G["engines"] if eng._ws is not None]
             if not G["used"] or not wss:
                 continue
-            pw = (ctypes.c_void_p * len(wss))(*wss)
-            if self.lib.efd_modesum_status_batch(pw, len(wss), None,
-                                                 G["stream"].cuda_stream) != _lib.EFD_OK:
-                raise _lib.EFDError(_lib.last_error(self.lib))
+            for c0 in range(0, len(wss), _lib.EFD_BATCH_MAX):
+                part = wss[c0:c0 + _lib.EFD_BATCH_MAX]
+                pw = (ctypes.c_void_p * len(part))(*part)
+                if self.lib.efd_modesum_status_batch(pw, len(part), None,
+                                                     G["stream"].cuda_stream) != _lib.EFD_OK:
+                    raise _lib.EFDError(_lib.last_error(self.lib))
 
 
 def td_length(T, dt, odd_len=True):

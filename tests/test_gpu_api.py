@@ -197,6 +197,30 @@ def test_fused_likelihood_many_walkers(setup):
     np.testing.assert_array_equal(like.get_ll(walkers, **kw), llf)
 
 
+def test_fused_likelihood_large_group(setup):
+    """One fused group of 32 walkers (BatchPreparer.GROUP_MAX > EFD_BATCH_MAX: one staging copy
+    and upload, the preparation and sum launches 16 walkers at a time) gives bitwise the
+    log-likelihoods of groups of at most 16."""
+    params, kw, gen, gen_list = setup
+    freq = gen_list.waveform_generator.create_waveform.frequency
+    pos = freq >= 0
+    fd_gen = get_fd_waveform_fromFD(gen_list, pos, DT)
+    sig = fd_gen(*params, **kw)
+    like = Likelihood(fd_gen, 2, f_arr=freq[pos].cpu().numpy(), use_gpu=True)
+    like.inject_signal(data_stream=sig, noise_fn=[get_sensitivity] * 2, noise_kwargs=[{}, {}])
+    rng = np.random.default_rng(9)
+    walkers = np.stack([params] * 27)
+    walkers[1:, 0] *= 1.0 + 1e-5 * rng.standard_normal(26)
+    walkers[1:, 11] += 0.1 * rng.standard_normal(26)
+    ref = like.get_ll(walkers, **kw)
+    like.FUSED_GROUP = 32
+    like._fused = None
+    got = like.get_ll(walkers, **kw)
+    assert like._fused["prep"].group == 32
+    np.testing.assert_array_equal(got, ref)
+    assert got[0] == 0.0
+
+
 def test_spectrum_matches_oracle_through_api(setup):
     params, kw, gen, _ = setup
     wg = gen.waveform_generator
