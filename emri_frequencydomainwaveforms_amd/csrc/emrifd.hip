@@ -2219,32 +2219,23 @@ constexpr int SCTAB = 512;
 // fma(-v, v, COS_A) = COS_A rho to 2e-20).
 constexpr double COS_A = 1.000000000029531;
 constexpr double COS_B = -0.5;
-// q = nearest integer to x / step by a shifter: with 1.5 * 2^56, whose ulp is 16, the sum's low
-// word is 16 q, the table entry's byte offset, and the table's 3 pi / 4 shift (+-192 entries,
-// by the sign of F') rides in the shifter constant (tab_shifter: exact, even, so the rounding
-// and its ties are those of the 1.5 * 2^52 form, and q STEP = (16 q)(STEP / 16) exactly): the
-// byte offset is one v_and instead of v_lshl_add + v_and (round 4's form), bitwise the same
-constexpr double SHIFTER16 = 108086391056891904.0;    // 1.5 * 2^56
-__host__ __device__ constexpr double tab_shifter(int shift) {
-    return SHIFTER16 + 16.0 * (double)shift;
-}
-__device__ __forceinline__ void sincos_tab(double x, double shifter,
-                                           const double2* __restrict__ tab, double& s, double& c,
-                                           double extra = 0.0, bool use_extra = false,
-                                           double extra_scale = 1.0, double c0 = COS_A) {
-    constexpr double INV_STEP16 = 16.0 * 81.48733086305042;     // 16 * 256 / pi
-    constexpr double STEP_1_16 = 0.01227184630308513 / 16.0;    // (pi/256, leading part) / 16
-    const double qs = fma(x, INV_STEP16, shifter);
-    const double q16 = qs - shifter;                              // 16 q
-    double r = fma(-q16, STEP_1_16, x);
+__device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
+                                           double& s, double& c, double extra = 0.0,
+                                           bool use_extra = false, double extra_scale = 1.0,
+                                           double c0 = COS_A) {
+    constexpr double INV_STEP = 81.48733086305042;       // 256 / pi
+    constexpr double STEP_1 = 0.01227184630308513;       // pi/256, leading part
+    // q = nearest integer to x / step via the 1.5 * 2^52 shifter: its low word is q itself
+    // (two's complement), so neither rint nor a float->int conversion is needed
+    constexpr double SHIFTER = 6755399441055744.0;
+    const double qs = fma(x, INV_STEP, SHIFTER);
+    const double q = qs - SHIFTER;
+    double r = fma(-q, STEP_1, x);
     // a small angle (|extra_scale * extra| < 1e-3) added after the reduction
     if (use_extra) r = fma(extra_scale, extra, r);
-    // (sin, cos)((q + shift) pi/256), addressed in bytes: one v_and on the sum's low word (inline
-    // asm: the compiler otherwise packed the three bins' offsets through v_perm / v_bitop3, as
-    // many instructions as before)
-    static_assert(16 * (SCTAB - 1) == 0x1ff0, "table byte-offset mask");
-    uint32_t off;
-    asm("v_and_b32 %0, 0x1ff0, %1" : "=v"(off) : "v"(__double2loint(qs)));
+    const int qi = __double2loint(qs);
+    // (sin, cos)((q + shift) pi/256), addressed in bytes: v_lshl_add + v_and
+    const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
     const double2 t = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
     const double z = r * r;
     const double sr = fma(r * z, -1.6666666666666666e-01, r);
@@ -2477,7 +2468,7 @@ __device__ __forceinline__ uint64_t lane_range_mask(int32_t lo, int32_t hi) {
 // boolean is turned into a VGPR and compared back (2 VALU) before a ballot.
 struct RecSign {
     int32_t fdcls;   // v_cmp_class mask: F' normal or subnormal of the record's sign
-    double shifter;  // sincos_tab's shifter with sign(F') 3 pi / 4 in table steps
+    int32_t shift;   // sign(F') 3 pi / 4 in table steps
     double kth;      // theta = kth * min(|thn|, 1): KTH0 with the sign of F'
     bool safe;       // every lane passes the interval and sign tests (record_safe)
 };
@@ -2487,7 +2478,7 @@ __device__ __forceinline__ RecSign rec_sign(uint32_t bits) {
     RecSign r;
     r.safe = (bits & 2u) != 0;
     r.fdcls = fdneg ? 0x018 : 0x180;
-    r.shifter = fdneg ? tab_shifter(-192) : tab_shifter(192);
+    r.shift = fdneg ? -192 : 192;
     r.kth = fdneg ? -KTH0 / VS : KTH0 / VS;
     return r;
 }
@@ -2541,7 +2532,7 @@ __device__ __forceinline__ void spa_simple(const Item* __restrict__ it, double s
     const double t3 = fdds * a3;
     const double ww = t3 * t3;
     double sn, cs;
-    sincos_tab(psi0, rs.shifter, sct, sn, cs, ww, true, rs.kth, fma(-ww, ww, COS_A));
+    sincos_tab(psi0, rs.shift, sct, sn, cs, ww, true, rs.kth, fma(-ww, ww, COS_A));
     wr = amp * cs;
     wi = amp * sn;
 }
@@ -2568,7 +2559,7 @@ __device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double 
     const double thn = ww * fma(-14.733333333333333333, uu, 1.0);
     const double am = amp * r;
     double sn, cs;
-    sincos_tab(psi0, rs.shifter, sct, sn, cs, thn, true, rs.kth, COS_A);
+    sincos_tab(psi0, rs.shift, sct, sn, cs, thn, true, rs.kth, COS_A);
     wr = am * cs;
     wi = am * sn;
 }
@@ -2635,13 +2626,13 @@ __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double s
             thn = ww;
             am = ampm;
         }
-        sincos_tab(psi0, rs.shifter, sct, sn, cs, thn, true, rs.kth, c0);
+        sincos_tab(psi0, rs.shift, sct, sn, cs, thn, true, rs.kth, c0);
         wr = am * cs;
         wi = am * sn;
     } else {
         const bool ok = __builtin_amdgcn_inverse_ballot_w64(actm & goodm);
         const double am = ftz_select(ok, amp);
-        sincos_tab(psi0, rs.shifter, sct, sn, cs);
+        sincos_tab(psi0, rs.shift, sct, sn, cs);
         wr = am * cs;
         wi = am * sn;
     }
