@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "efd_hann_extent",
     "efd_hann_stage",
     "efd_hann_convolve",
+    "efd_hann_four_step_cols",
     "efd_hann_polarizations",
     "efd_hann_loglike",
     "efd_loglike",
@@ -232,6 +233,8 @@ def load(path=None):
     lib.efd_hann_stage.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp]
     lib.efd_hann_convolve.restype = ctypes.c_int
     lib.efd_hann_convolve.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp, vp]
+    lib.efd_hann_four_step_cols.restype = ctypes.c_int
+    lib.efd_hann_four_step_cols.argtypes = [i64]
     lib.efd_hann_polarizations.restype = ctypes.c_int
     lib.efd_hann_polarizations.argtypes = [vp, vp, vp, i64, i64, i64, vp, vp, vp]
     lib.efd_hann_loglike.restype = ctypes.c_int

@@ -4450,12 +4450,12 @@ struct FcCols {
 // straight from S (efd_hann_stage's values), forward FFT, twiddle, store. Inverse: load,
 // conjugate twiddle, inverse FFT, store in natural order.
 // (<= 128 VGPRs: two 8-wave workgroups per CU, 4 waves per SIMD)
-template <bool FWD, int R>
+template <bool FWD, int R, int C = FC_C>
 __global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
                float2* __restrict__ Yv) {
     constexpr int NCOL = FcCols<R>::NCOL, LOGL = FcCols<R>::LOGL;
-    constexpr int64_t M = (int64_t)R * FC_C;
+    constexpr int64_t M = (int64_t)R * C;
     constexpr int NQ = R * NCOL / FC_NT;   // elements per thread
     static_assert(R * NCOL % FC_NT == 0, "whole rounds of elements per thread");
     __shared__ fcv sm[R * FcColIdx<NCOL>::STRIDE];
@@ -4466,7 +4466,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
     // so XCD x takes the contiguous eighth [x G/8, (x+1) G/8) of the G column blocks in order;
     // a block's rows are NCOL * 8 or 16 B wide, and the neighbouring blocks sharing their
     // 128-B lines then hit the same L2
-    constexpr int G = FC_C / NCOL;
+    constexpr int G = C / NCOL;
     static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
     const int c0 = ((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * NCOL;
     fcv* y = Y + (int64_t)row * M;
@@ -4479,7 +4479,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
         for (int q = 0; q < NQ; ++q) {
             const int i = threadIdx.x + q * FC_NT;
             const int e = i / NCOL, j = i % NCOL;
-            const int64_t s = (int64_t)e * FC_C + c0 + j;
+            const int64_t s = (int64_t)e * C + c0 + j;
             fcv v = {0.f, 0.f};
             if (bad) {
                 v = (fcv){__int_as_float(0x7fc00000), 0.f};
@@ -4499,7 +4499,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
             const uint32_t p = (uint32_t)c * (uint32_t)e;   // < C R = M: no reduction
             float sn, cs;
             __sincosf(-FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
-            y[(int64_t)e * FC_C + c] = cmulf(sm[idx(j, e)], (fcv){cs, sn});
+            y[(int64_t)e * C + c] = cmulf(sm[idx(j, e)], (fcv){cs, sn});
         }
     } else {
 #pragma unroll
@@ -4510,7 +4510,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
             const uint32_t p = (uint32_t)c * (uint32_t)e;   // < C R = M: no reduction
             float sn, cs;
             __sincosf(FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
-            sm[idx(j, e)] = cmulf(y[(int64_t)e * FC_C + c], (fcv){cs, sn});
+            sm[idx(j, e)] = cmulf(y[(int64_t)e * C + c], (fcv){cs, sn});
         }
         __syncthreads();
         fc_fft<1, R, LOGL>(sm, idx);
@@ -4518,7 +4518,7 @@ void k_fc_cols(const double2* __restrict__ S, int64_t stride, const uint64_t* __
         for (int q = 0; q < NQ; ++q) {
             const int i = threadIdx.x + q * FC_NT;
             const int e = i / NCOL, j = i % NCOL;
-            y[(int64_t)e * FC_C + c0 + j] = sm[idx(j, e)];
+            y[(int64_t)e * C + c0 + j] = sm[idx(j, e)];
         }
     }
 }
@@ -4708,6 +4708,43 @@ void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __r
         fc_dft32<1>(v);
 #pragma unroll
         for (int n1 = 0; n1 < 32; ++n1) y[t + 256 * n1] = v[n1];
+    }
+}
+
+// (B) for rows of C = 16384 (m = 2^24 as 1024 x 16384, EFD_FC_C16: wider column segments, 128 B
+// of S and 64 B of Y per row of a column block): the Stockham passes in LDS (139 KB, one
+// workgroup per CU), XCD-aware (row, walker) pairs as k_fc_rows
+constexpr int FC_C16 = 16384;
+__global__ __launch_bounds__(FC_NT)
+void k_fc_rows16k(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
+    __shared__ fcv sm[FC_C16 + FC_C16 / 16];
+    const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
+    fcv* Y = reinterpret_cast<fcv*>(Yv);
+    const FcRowIdx idx;
+    const int64_t npair = (int64_t)gridDim.x;
+    const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
+    const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
+    fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C16;
+    const fcv* k = kfp + (int64_t)fr * FC_C16;
+    constexpr int NQ = FC_C16 / FC_NT;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + q * FC_NT;
+        sm[idx(0, e)] = y[e];
+    }
+    __syncthreads();
+    fc_fft<-1, FC_C16, 0>(sm, idx);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + q * FC_NT;
+        sm[idx(0, e)] = cmulf(sm[idx(0, e)], k[e]);
+    }
+    __syncthreads();
+    fc_fft<1, FC_C16, 0>(sm, idx);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + q * FC_NT;
+        y[e] = sm[idx(0, e)];
     }
 }
 
@@ -5837,6 +5874,16 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
     HIP_TRY(hipGetLastError());
     return EFD_OK;
 }
+// the four-step split's row length C for a transform length m (the lag kernel's spectrum is
+// laid out [f_r][f_c], R = m / C): 8192, or 16384 at m = 2^24 with EFD_FC_C16=1 (an experiment
+// switch, read once)
+int efd_hann_four_step_cols(int64_t m) {
+    static const bool c16 = [] {
+        const char* e = getenv("EFD_FC_C16");
+        return e && e[0] == '1';
+    }();
+    return (c16 && m == ((int64_t)1 << 24)) ? FC_C16 : FC_C;
+}
 // the register-staged column kernels at R = 2048 (EFD_FC_COLS=0: the Stockham ones, an
 // experiment switch for paired A/B runs; read once)
 static bool fc_cols_staged() {
@@ -5853,6 +5900,21 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         return fail(EFD_ERR_ARG, "efd_hann_convolve: bad arguments (m: a power of two in "
                                  "[2^21, 2^25], >= nf)");
     hipStream_t st = (hipStream_t)stream;
+    if (m == ((int64_t)1 << 24) && efd_hann_four_step_cols(m) == FC_C16) {
+        constexpr int R16 = (1 << 24) / FC_C16;
+        constexpr int NC16 = FcCols<R16>::NCOL;
+        hipLaunchKernelGGL((k_fc_cols<true, R16, FC_C16>), dim3(FC_C16 / NC16, (unsigned)rows),
+                           dim3(FC_NT), 0, st, (const double2*)S, stride, info, (float2*)Y);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_fc_rows16k, dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st,
+                           (const float2*)kfp, m, (int)rows, (float2*)Y);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL((k_fc_cols<false, R16, FC_C16>), dim3(FC_C16 / NC16, (unsigned)rows),
+                           dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,
+                           (const uint64_t*)nullptr, (float2*)Y);
+        HIP_TRY(hipGetLastError());
+        return EFD_OK;
+    }
     const int R = (int)(m / FC_C);
     float2* y = (float2*)Y;
 #define EFD_FC(RR)                                                                            \

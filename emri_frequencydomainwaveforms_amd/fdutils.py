@@ -176,7 +176,8 @@ class HannConvolution:
 
     def kernel_spectrum(self, m, four=False):
         """fft(z) / m in complex64, z[t] = K[(t - (m - n)) mod n] (computed in complex128); with
-        four=True in efd_hann_convolve's order: [f_r][f_c] = kf[f_r + R f_c], R = m / 8192."""
+        four=True in efd_hann_convolve's order: [f_r][f_c] = kf[f_r + R f_c], R = m / C with the
+        library's C for m (efd_hann_four_step_cols: 8192, or 16384 at m = 2^24)."""
         kf = self._kf.get((m, four))
         if kf is None:
             torch = require_gpu()
@@ -189,7 +190,9 @@ class HannConvolution:
                              torch.full_like(mm, -np.pi / n))
             kf = (torch.fft.fft(torch.complex(re, im)) / m).to(torch.complex64)
             if four:
-                kf = kf.view(self.FOUR_STEP_C, m // self.FOUR_STEP_C).t().contiguous()
+                from . import _lib
+                C = int(_lib.load().efd_hann_four_step_cols(m))
+                kf = kf.view(C, m // C).t().contiguous()
             while len(self._kf) >= self.KEEP_KERNELS:
                 self._kf.pop(next(iter(self._kf)))
             self._kf[(m, four)] = kf

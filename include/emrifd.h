@@ -337,6 +337,10 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
  * order kfp[f_r 8192 + f_c] = kf[f_r + R f_c]. Leaves Y as efd_hann_stage + transforms do. */
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream);
+/* The four-step split's row length C that efd_hann_convolve uses for transform length m
+ * (R = m / C; kfp's layout above with 8192 replaced by C): 8192, or 16384 at m = 2^24 when the
+ * library runs with EFD_FC_C16=1. */
+int efd_hann_four_step_cols(int64_t m);
 int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
                            int64_t nf, int64_t k0, double* hp, double* hc, void* stream);
 
