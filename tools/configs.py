@@ -254,7 +254,11 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
     if os.environ.get("FUSED_DEPTH"):
         like.FUSED_DEPTH = int(os.environ["FUSED_DEPTH"])
     B = len(walkers)
-    ll = like.get_ll(walkers, **kw)        # warm-up (also the correctness anchor: ll[0] == 0)
+    # warm-up (also the correctness anchor: ll[0] == 0); three calls, so the upstream pool's
+    # threads have made their OpenMP teams before the timed calls (the first calls of a fresh
+    # process cost several ms more, which a mean over 5 reps otherwise carries)
+    for _ in range(3):
+        ll = like.get_ll(walkers, **kw)
     _sync()
     t0 = time.perf_counter()
     for _ in range(reps):
