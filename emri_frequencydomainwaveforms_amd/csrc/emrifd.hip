@@ -4712,39 +4712,93 @@ void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __r
 }
 
 // (B) for rows of C = 16384 (m = 2^24 as 1024 x 16384, EFD_FC_C16: wider column segments, 128 B
-// of S and 64 B of Y per row of a column block): the Stockham passes in LDS (139 KB, one
-// workgroup per CU), XCD-aware (row, walker) pairs as k_fc_rows
+// of S and 64 B of Y per row of a column block), register-staged as k_fc_rows with 512 threads
+// of 32 elements (16384 = 32 x 32 x 16; n = n2 + 512 n1, n2 = n2a + 16 n2b; k = k1 + 32 k2a +
+// 1024 k2b): forward (A) thread n2: DFT-32 over n1, times w_16384^(n2 k1); (B) task (k1, n2a):
+// DFT-32 over n2b, times w_512^(n2a k2a); (C) task (k1, k2a), two per thread: DFT-16 over n2a;
+// the kernel's spectrum; the transposed steps back. Exchange 1 [k1][n2] (stride 513),
+// exchange 2 [k2a][n2a][k1]: conflict-free as k_fc_rows'. 128.3 KB of LDS, one workgroup per CU.
 constexpr int FC_C16 = 16384;
+constexpr int FR16_S1 = 513;
 __global__ __launch_bounds__(FC_NT)
 void k_fc_rows16k(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
-    __shared__ fcv sm[FC_C16 + FC_C16 / 16];
+    static_assert(FC_NT == 512 && FC_C16 == 32 * 32 * 16, "16384 = 32 x 32 x 16, 512 threads");
+    __shared__ fcv sm[32 * FR16_S1];
     const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
     fcv* Y = reinterpret_cast<fcv*>(Yv);
-    const FcRowIdx idx;
     const int64_t npair = (int64_t)gridDim.x;
     const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
     const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
     fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C16;
-    const fcv* k = kfp + (int64_t)fr * FC_C16;
-    constexpr int NQ = FC_C16 / FC_NT;
+    const fcv* kr = kfp + (int64_t)fr * FC_C16;
+    const int t = threadIdx.x;
+    constexpr float W16K = FC_2PI / 16384.0f, W512 = FC_2PI / 512.0f;
+    {   // forward (A): n2 = t
+        fcv v[32];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = threadIdx.x + q * FC_NT;
-        sm[idx(0, e)] = y[e];
+        for (int n1 = 0; n1 < 32; ++n1) v[n1] = y[t + 512 * n1];
+        fc_dft32<-1>(v);
+        fc_twiddle_pow<32>(v, -W16K * (float)t);
+#pragma unroll
+        for (int k1 = 0; k1 < 32; ++k1) sm[k1 * FR16_S1 + t] = v[k1];
     }
     __syncthreads();
-    fc_fft<-1, FC_C16, 0>(sm, idx);
+    const int kb = t & 31, nb = t >> 5;   // (B) task (k1 = kb, n2a = nb)
+    {
+        fcv u[32];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = threadIdx.x + q * FC_NT;
-        sm[idx(0, e)] = cmulf(sm[idx(0, e)], k[e]);
+        for (int n2b = 0; n2b < 32; ++n2b) u[n2b] = sm[kb * FR16_S1 + nb + 16 * n2b];
+        __syncthreads();
+        fc_dft32<-1>(u);
+        fc_twiddle_pow<32>(u, -W512 * (float)nb);
+#pragma unroll
+        for (int k2a = 0; k2a < 32; ++k2a) sm[(k2a * 16 + nb) * 32 + kb] = u[k2a];
     }
     __syncthreads();
-    fc_fft<1, FC_C16, 0>(sm, idx);
+    fcv w[2][16];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int e = threadIdx.x + q * FC_NT;
-        y[e] = sm[idx(0, e)];
+    for (int h = 0; h < 2; ++h) {   // forward (C), the kernel's spectrum, inverse (C): (k1, k2a)
+        const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
+#pragma unroll
+        for (int n2a = 0; n2a < 16; ++n2a) w[h][n2a] = sm[(k2a * 16 + n2a) * 32 + k1];
+        fc_dft16<-1>(w[h]);
+#pragma unroll
+        for (int k2b = 0; k2b < 16; ++k2b)
+            w[h][k2b] = cmulf(w[h][k2b], kr[k1 + 32 * k2a + 1024 * k2b]);
+        fc_dft16<1>(w[h]);
+        fc_twiddle_pow<16>(w[h], W512 * (float)k2a);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
+#pragma unroll
+        for (int n2a = 0; n2a < 16; ++n2a) sm[(k2a * 16 + n2a) * 32 + k1] = w[h][n2a];
+    }
+    __syncthreads();
+    {   // inverse (B): task (k1 = kb, n2a = nb) -> n2b, times w_16384^(-n2 k1)
+        fcv u[32];
+#pragma unroll
+        for (int k2a = 0; k2a < 32; ++k2a) u[k2a] = sm[(k2a * 16 + nb) * 32 + kb];
+        __syncthreads();
+        fc_dft32<1>(u);
+        float s0, c0;
+        __sincosf(W16K * (float)(nb * kb), &s0, &c0);
+        const fcv w0 = {c0, s0};
+#pragma unroll
+        for (int n2b = 0; n2b < 32; ++n2b) u[n2b] = cmulf(u[n2b], w0);
+        fc_twiddle_pow<32>(u, W16K * 16.0f * (float)kb);
+#pragma unroll
+        for (int n2b = 0; n2b < 32; ++n2b) sm[kb * FR16_S1 + nb + 16 * n2b] = u[n2b];
+    }
+    __syncthreads();
+    {   // inverse (A): n2 = t -> x[n2 + 512 n1]
+        fcv v[32];
+#pragma unroll
+        for (int k1 = 0; k1 < 32; ++k1) v[k1] = sm[k1 * FR16_S1 + t];
+        fc_dft32<1>(v);
+#pragma unroll
+        for (int n1 = 0; n1 < 32; ++n1) y[t + 512 * n1] = v[n1];
     }
 }
 
