@@ -5929,12 +5929,13 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
     return EFD_OK;
 }
 // the four-step split's row length C for a transform length m (the lag kernel's spectrum is
-// laid out [f_r][f_c], R = m / C): 8192, or 16384 at m = 2^24 with EFD_FC_C16=1 (an experiment
-// switch, read once)
+// laid out [f_r][f_c], R = m / C): 16384 at m = 2^24 (1024 x 16384: the column kernels read
+// 128 B segments, r05z), else 8192; EFD_FC_C16=0 keeps 8192 at 2^24 too (an experiment switch
+// for paired A/B runs, read once)
 int efd_hann_four_step_cols(int64_t m) {
     static const bool c16 = [] {
         const char* e = getenv("EFD_FC_C16");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     return (c16 && m == ((int64_t)1 << 24)) ? FC_C16 : FC_C;
 }

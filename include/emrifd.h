@@ -338,8 +338,8 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream);
 /* The four-step split's row length C that efd_hann_convolve uses for transform length m
- * (R = m / C; kfp's layout above with 8192 replaced by C): 8192, or 16384 at m = 2^24 when the
- * library runs with EFD_FC_C16=1. */
+ * (R = m / C; kfp's layout above with 8192 replaced by C): 16384 at m = 2^24, else 8192
+ * (EFD_FC_C16=0 in the environment keeps 8192 at 2^24 as well). */
 int efd_hann_four_step_cols(int64_t m);
 int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
                            int64_t nf, int64_t k0, double* hp, double* hc, void* stream);

@@ -211,15 +211,33 @@ def test_hann_loglike_matches_templates():
     (4000001, (0.3, 0.9), 2, 1 << 23), (12623261, (0.43, 0.57), 2, 1 << 24),
     (12623261, (0.2, 0.8), 2, 1 << 25)])
 def test_four_step_convolution(n, support, rows, m):
-    """efd_hann_convolve (the four-step complex64 FFT pipeline, every column length it has:
-    m = 2^21 .. 2^25, R = m / 8192 = 256 .. 4096) against
+    """efd_hann_convolve (the four-step complex64 FFT pipeline, every split it has: m = 2^21 ..
+    2^25 as R x 8192, R = 256 .. 4096, except 2^24 = 1024 x 16384) against
     the same correction on hipFFT transforms and against an exact complex128 convolution
     (torch.fft on the zero-padded support): C within 1e-5 of max|C| in both comparisons (float
     transforms: ~1e-6; the correction needs ~3 digits), rows of different supports, one of
     them all zero."""
+    _four_step_check(n, support, rows, m, 16384 if m == 1 << 24 else 8192)
+
+
+def test_four_step_convolution_8192_rows_at_2_24():
+    """The 2048 x 8192 split at m = 2^24 (EFD_FC_C16=0, read once per process: a child
+    process) to the same checks as test_four_step_convolution."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("from tests.test_gpu_windowed import _four_step_check; "
+            "_four_step_check(12623261, (0.43, 0.57), 2, 1 << 24, 8192)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                       env=dict(os.environ, EFD_FC_C16="0"), timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def _four_step_check(n, support, rows, m, cols):
     from emri_frequencydomainwaveforms_amd import _lib
     from emri_frequencydomainwaveforms_amd.fdutils import HannConvolution
     lib = _lib.load()
+    assert lib.efd_hann_four_step_cols(m) == cols
     rng = np.random.default_rng(n % 1000)
     S = torch.zeros((rows, n), dtype=torch.complex128, device="cuda")
     lo, hi = int(support[0] * n), int(support[1] * n)
