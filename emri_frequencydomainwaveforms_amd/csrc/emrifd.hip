@@ -4802,6 +4802,118 @@ void k_fc_rows16k(const float2* __restrict__ kfpv, int64_t m, int rows, float2* 
     }
 }
 
+// k_fc_rows16k with every exchange in two passes (real parts, then imaginary parts) through a
+// float array: 69.6 KB of LDS and at most 128 VGPRs, so two workgroups share a CU and one's
+// loads and stores overlap the other's transforms (one per CU leaves HBM idle while it
+// computes). Exchange 1 [k1][n2] stride 514, exchange 2 [k2a] stride 544 [n2a][k1]: every b32
+// access of a wave hits 64 distinct banks.
+constexpr int FR16_T1 = 514, FR16_T2 = 544;
+__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_fc_rows16k_h(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
+    static_assert(FC_NT == 512 && FC_C16 == 32 * 32 * 16, "16384 = 32 x 32 x 16, 512 threads");
+    __shared__ float sf[32 * FR16_T2];
+    const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
+    fcv* Y = reinterpret_cast<fcv*>(Yv);
+    const int64_t npair = (int64_t)gridDim.x;
+    const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
+    const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
+    fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C16;
+    const fcv* kr = kfp + (int64_t)fr * FC_C16;
+    const int t = threadIdx.x;
+    const int kb = t & 31, nb = t >> 5;
+    constexpr float W16K = FC_2PI / 16384.0f, W512 = FC_2PI / 512.0f;
+    fcv v[32], u[32], w[2][16];
+#pragma unroll
+    for (int n1 = 0; n1 < 32; ++n1) v[n1] = y[t + 512 * n1];
+    fc_dft32<-1>(v);   // forward (A): n2 = t
+    fc_twiddle_pow<32>(v, -W16K * (float)t);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {   // exchange 1 -> (B) task (k1 = kb, n2a = nb)
+#pragma unroll
+        for (int k1 = 0; k1 < 32; ++k1) sf[k1 * FR16_T1 + t] = c ? v[k1].y : v[k1].x;
+        __syncthreads();
+#pragma unroll
+        for (int n2b = 0; n2b < 32; ++n2b) {
+            const float x = sf[kb * FR16_T1 + nb + 16 * n2b];
+            if (c) u[n2b].y = x; else u[n2b].x = x;
+        }
+        __syncthreads();
+    }
+    fc_dft32<-1>(u);
+    fc_twiddle_pow<32>(u, -W512 * (float)nb);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {   // exchange 2 -> (C) tasks (k1, k2a)
+#pragma unroll
+        for (int k2a = 0; k2a < 32; ++k2a) sf[k2a * FR16_T2 + nb * 32 + kb] = c ? u[k2a].y : u[k2a].x;
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
+#pragma unroll
+            for (int n2a = 0; n2a < 16; ++n2a) {
+                const float x = sf[k2a * FR16_T2 + n2a * 32 + k1];
+                if (c) w[h][n2a].y = x; else w[h][n2a].x = x;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // forward (C), the kernel's spectrum, inverse (C)
+        const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
+        fc_dft16<-1>(w[h]);
+#pragma unroll
+        for (int k2b = 0; k2b < 16; ++k2b)
+            w[h][k2b] = cmulf(w[h][k2b], kr[k1 + 32 * k2a + 1024 * k2b]);
+        fc_dft16<1>(w[h]);
+        fc_twiddle_pow<16>(w[h], W512 * (float)k2a);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {   // exchange 2 back -> inverse (B)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
+#pragma unroll
+            for (int n2a = 0; n2a < 16; ++n2a)
+                sf[k2a * FR16_T2 + n2a * 32 + k1] = c ? w[h][n2a].y : w[h][n2a].x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k2a = 0; k2a < 32; ++k2a) {
+            const float x = sf[k2a * FR16_T2 + nb * 32 + kb];
+            if (c) u[k2a].y = x; else u[k2a].x = x;
+        }
+        __syncthreads();
+    }
+    fc_dft32<1>(u);   // -> n2b, times w_16384^(-n2 k1)
+    {
+        float s0, c0;
+        __sincosf(W16K * (float)(nb * kb), &s0, &c0);
+        const fcv w0 = {c0, s0};
+#pragma unroll
+        for (int n2b = 0; n2b < 32; ++n2b) u[n2b] = cmulf(u[n2b], w0);
+    }
+    fc_twiddle_pow<32>(u, W16K * 16.0f * (float)kb);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {   // exchange 1 back -> inverse (A): n2 = t
+#pragma unroll
+        for (int n2b = 0; n2b < 32; ++n2b) sf[kb * FR16_T1 + nb + 16 * n2b] = c ? u[n2b].y : u[n2b].x;
+        __syncthreads();
+#pragma unroll
+        for (int k1 = 0; k1 < 32; ++k1) {
+            const float x = sf[k1 * FR16_T1 + t];
+            if (c) v[k1].y = x; else v[k1].x = x;
+        }
+        if (c == 0) __syncthreads();
+    }
+    fc_dft32<1>(v);
+    // the store offsets from an opaque copy of t: else the compiler keeps the loads' 32
+    // addresses live across the kernel (spilled to scratch)
+    int to = t;
+    __asm__ volatile("" : "+v"(to));
+#pragma unroll
+    for (int n1 = 0; n1 < 32; ++n1) y[to + 512 * n1] = v[n1];
+}
+
 // (A) and (C) for R = 2048 (m = 2^24, test.sh's transform), NCOL = 4 columns per workgroup, as
 // register stages with two LDS exchanges (2048 = 16 x 16 x 8; n = n2 + 128 n1, n2 = n2a + 8 n2b;
 // k = k1 + 16 k2a + 256 k2b): forward (A) task (j, n2): DFT-16 over n1, times w_2048^(n2 k1);
@@ -5948,6 +6060,15 @@ static bool fc_cols_staged() {
     }();
     return v;
 }
+// the 16384-point rows with two-pass exchanges, two workgroups per CU (EFD_FC_R16H=0: one
+// workgroup per CU with complex exchanges, an experiment switch; read once)
+static bool fc_rows16k_half() {
+    static const bool v = [] {
+        const char* e = getenv("EFD_FC_R16H");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream) {
     if (!hann_rows_ok("efd_hann_convolve", S, stride, nf, rows) || !info || !kfp || !Y ||
@@ -5961,8 +6082,9 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         hipLaunchKernelGGL((k_fc_cols<true, R16, FC_C16>), dim3(FC_C16 / NC16, (unsigned)rows),
                            dim3(FC_NT), 0, st, (const double2*)S, stride, info, (float2*)Y);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_fc_rows16k, dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st,
-                           (const float2*)kfp, m, (int)rows, (float2*)Y);
+        hipLaunchKernelGGL(fc_rows16k_half() ? k_fc_rows16k_h : k_fc_rows16k,
+                           dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st, (const float2*)kfp, m,
+                           (int)rows, (float2*)Y);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL((k_fc_cols<false, R16, FC_C16>), dim3(FC_C16 / NC16, (unsigned)rows),
                            dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,
