@@ -5048,6 +5048,152 @@ void k_fc_cols2048(const double2* __restrict__ S, int64_t stride, const uint64_t
     }
 }
 
+// (A) and (C) for R = 1024 with rows of C = 16384 (m = 2^24 as 1024 x 16384), NCOL = 8 columns
+// per workgroup, register-staged as k_fc_cols2048 (1024 = 16 x 8 x 8; n = n2 + 64 n1,
+// n2 = n2a + 8 n2b; k = k1 + 16 k2a + 128 k2b): forward (A) task (j, n2): DFT-16 over n1, times
+// w_1024^(n2 k1); (B) tasks (j, k1, n2a), two per thread: DFT-8 over n2b, times w_64^(n2a k2a);
+// (C) tasks (j, k1, k2a), two per thread: DFT-8 over n2a -> f_r = k. Exchange 1 [k1][n2][j],
+// exchange 2 [k1][k2a][n2a (pad to 9)][j]: lanes along j then n2a / k2a, conflict-free.
+constexpr int FCD_R = 1024, FCD_NCOL = 8, FCD_S2 = 9;
+template <bool FWD>
+__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
+                   float2* __restrict__ Yv) {
+    static_assert(FC_NT == 512 && FCD_R * FCD_NCOL == 16 * FC_NT, "16 elements per thread");
+    constexpr int C = FC_C16;
+    constexpr int64_t M = (int64_t)FCD_R * C;
+    // exchange 1: 16 x 64 x 8 = 8192; exchange 2: 16 x 8 x 9 x 8 = 9216 elements (73.7 KB)
+    __shared__ fcv sm[16 * 8 * FCD_S2 * FCD_NCOL];
+    fcv* Y = reinterpret_cast<fcv*>(Yv);
+    const int row = blockIdx.y;
+    constexpr int G = C / FCD_NCOL;
+    static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
+    const int c0 = ((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * FCD_NCOL;
+    fcv* y = Y + (int64_t)row * M;
+    const int t = threadIdx.x;
+    const int j = t & 7;
+    const int c = c0 + j;
+    constexpr float W1024 = FC_2PI / 1024.0f, W64 = FC_2PI / 64.0f;
+    auto e1 = [](int k1, int n2, int jj) { return (k1 * 64 + n2) * FCD_NCOL + jj; };
+    auto e2 = [](int k1, int k2a, int n2a, int jj) {
+        return ((k1 * 8 + k2a) * FCD_S2 + n2a) * FCD_NCOL + jj;
+    };
+    if (FWD) {
+        const HannRow h = hann_row(info, row);
+        const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;
+        const double2* src = S + (int64_t)row * stride + h.first;
+        const bool bad = h.len > M;
+        {   // (A): task (j, n2)
+            const int n2 = t >> 3;
+            fcv v[16];
+#pragma unroll
+            for (int n1 = 0; n1 < 16; ++n1) {
+                const int64_t s = (int64_t)(n2 + 64 * n1) * C + c;
+                fcv x = {0.f, 0.f};
+                if (bad) {
+                    x = (fcv){__int_as_float(0x7fc00000), 0.f};
+                } else if (s < h.len) {
+                    const double2 d = src[s];
+                    x = (fcv){(float)(d.x * inv), (float)(d.y * inv)};
+                }
+                v[n1] = x;
+            }
+            fc_dft16<-1>(v);
+            fc_twiddle_pow<16>(v, -W1024 * (float)n2);
+#pragma unroll
+            for (int k1 = 0; k1 < 16; ++k1) sm[e1(k1, n2, j)] = v[k1];
+        }
+        __syncthreads();
+        fcv u[2][8];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // (B): tasks (j, n2a, k1)
+            const int q = t + FC_NT * hh, n2a = (q >> 3) & 7, k1 = q >> 6;
+#pragma unroll
+            for (int n2b = 0; n2b < 8; ++n2b) u[hh][n2b] = sm[e1(k1, n2a + 8 * n2b, j)];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int q = t + FC_NT * hh, n2a = (q >> 3) & 7, k1 = q >> 6;
+            fc_dft8<-1>(u[hh]);
+            fc_twiddle_pow<8>(u[hh], -W64 * (float)n2a);
+#pragma unroll
+            for (int k2a = 0; k2a < 8; ++k2a) sm[e2(k1, k2a, n2a, j)] = u[hh][k2a];
+        }
+        __syncthreads();
+        int to = t;   // opaque: no store address kept live from (A)
+        __asm__ volatile("" : "+v"(to));
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // (C): tasks (j, k2a, k1)
+            const int q = to + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
+            fcv w[8];
+#pragma unroll
+            for (int a = 0; a < 8; ++a) w[a] = sm[e2(k1, k2a, a, j)];
+            fc_dft8<-1>(w);
+#pragma unroll
+            for (int k2b = 0; k2b < 8; ++k2b) {
+                const int fr = k1 + 16 * k2a + 128 * k2b;
+                const uint32_t pp = (uint32_t)c * (uint32_t)fr;   // < C R = M: no reduction
+                float sn, cs;
+                __sincosf(-FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
+                y[(int64_t)fr * C + c] = cmulf(w[k2b], (fcv){cs, sn});
+            }
+        }
+    } else {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // inverse (C): tasks (j, k2a, k1)
+            const int q = t + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
+            fcv w[8];
+#pragma unroll
+            for (int k2b = 0; k2b < 8; ++k2b) {
+                const int fr = k1 + 16 * k2a + 128 * k2b;
+                const uint32_t pp = (uint32_t)c * (uint32_t)fr;
+                float sn, cs;
+                __sincosf(FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
+                w[k2b] = cmulf(y[(int64_t)fr * C + c], (fcv){cs, sn});
+            }
+            fc_dft8<1>(w);   // -> n2a
+            fc_twiddle_pow<8>(w, W64 * (float)k2a);
+#pragma unroll
+            for (int a = 0; a < 8; ++a) sm[e2(k1, k2a, a, j)] = w[a];
+        }
+        __syncthreads();
+        fcv u[2][8];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // inverse (B): tasks (j, n2a, k1)
+            const int q = t + FC_NT * hh, n2a = (q >> 3) & 7, k1 = q >> 6;
+#pragma unroll
+            for (int k2a = 0; k2a < 8; ++k2a) u[hh][k2a] = sm[e2(k1, k2a, n2a, j)];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int q = t + FC_NT * hh, n2a = (q >> 3) & 7, k1 = q >> 6;
+            fc_dft8<1>(u[hh]);   // -> n2b; times w_1024^(-n2 k1), n2 = n2a + 8 n2b
+            float s0, cz;
+            __sincosf(W1024 * (float)(n2a * k1), &s0, &cz);
+            const fcv w0 = {cz, s0};
+#pragma unroll
+            for (int n2b = 0; n2b < 8; ++n2b) u[hh][n2b] = cmulf(u[hh][n2b], w0);
+            fc_twiddle_pow<8>(u[hh], W1024 * 8.0f * (float)k1);
+#pragma unroll
+            for (int n2b = 0; n2b < 8; ++n2b) sm[e1(k1, n2a + 8 * n2b, j)] = u[hh][n2b];
+        }
+        __syncthreads();
+        {   // inverse (A): task (j, n2) -> r = n2 + 64 n1
+            int to = t;   // opaque: no store address kept live from inverse (C)
+            __asm__ volatile("" : "+v"(to));
+            const int n2 = to >> 3, jo = to & 7;
+            fcv v[16];
+#pragma unroll
+            for (int k1 = 0; k1 < 16; ++k1) v[k1] = sm[e1(k1, n2, jo)];
+            fc_dft16<1>(v);
+#pragma unroll
+            for (int n1 = 0; n1 < 16; ++n1) y[(int64_t)(n2 + 64 * n1) * C + c0 + jo] = v[n1];
+        }
+    }
+}
+
 // S_w at bin k: the 3-point stencil on S and the correction's difference (neighbours mod nf).
 // S is zero outside the row's support [first, first + len) (cyclic; efd_hann_extent's bounds),
 // so it is read only there: the support is ~40% of test.sh's grid, and the skipped reads were
@@ -6060,6 +6206,15 @@ static bool fc_cols_staged() {
     }();
     return v;
 }
+// the register-staged column kernels at 1024 x 16384 (EFD_FC_COLS16=0: the Stockham ones, an
+// experiment switch; read once)
+static bool fc_cols1024_staged() {
+    static const bool v = [] {
+        const char* e = getenv("EFD_FC_COLS16");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 // the 16384-point rows with two-pass exchanges, two workgroups per CU (EFD_FC_R16H=0: one
 // workgroup per CU with complex exchanges, an experiment switch; read once)
 static bool fc_rows16k_half() {
@@ -6079,16 +6234,20 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
     if (m == ((int64_t)1 << 24) && efd_hann_four_step_cols(m) == FC_C16) {
         constexpr int R16 = (1 << 24) / FC_C16;
         constexpr int NC16 = FcCols<R16>::NCOL;
-        hipLaunchKernelGGL((k_fc_cols<true, R16, FC_C16>), dim3(FC_C16 / NC16, (unsigned)rows),
-                           dim3(FC_NT), 0, st, (const double2*)S, stride, info, (float2*)Y);
+        static_assert(NC16 == FCD_NCOL && R16 == FCD_R, "1024 x 16384: 8 columns per block");
+        hipLaunchKernelGGL((fc_cols1024_staged() ? k_fc_cols1024<true> : k_fc_cols<true, R16, FC_C16>),
+                           dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
+                           (const double2*)S, stride, info, (float2*)Y);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(fc_rows16k_half() ? k_fc_rows16k_h : k_fc_rows16k,
                            dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st, (const float2*)kfp, m,
                            (int)rows, (float2*)Y);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL((k_fc_cols<false, R16, FC_C16>), dim3(FC_C16 / NC16, (unsigned)rows),
-                           dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,
-                           (const uint64_t*)nullptr, (float2*)Y);
+        hipLaunchKernelGGL((fc_cols1024_staged() ? k_fc_cols1024<false>
+                                                 : k_fc_cols<false, R16, FC_C16>),
+                           dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
+                           (const double2*)nullptr, (int64_t)0, (const uint64_t*)nullptr,
+                           (float2*)Y);
         HIP_TRY(hipGetLastError());
         return EFD_OK;
     }
