@@ -5140,6 +5140,13 @@ void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t
             }
         }
     } else {
+        fcv r[2][8];   // all 16 loads in flight before any arithmetic
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int q = t + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
+#pragma unroll
+            for (int k2b = 0; k2b < 8; ++k2b) r[hh][k2b] = y[(int64_t)(k1 + 16 * k2a + 128 * k2b) * C + c];
+        }
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {   // inverse (C): tasks (j, k2a, k1)
             const int q = t + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
@@ -5150,7 +5157,7 @@ void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t
                 const uint32_t pp = (uint32_t)c * (uint32_t)fr;
                 float sn, cs;
                 __sincosf(FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
-                w[k2b] = cmulf(y[(int64_t)fr * C + c], (fcv){cs, sn});
+                w[k2b] = cmulf(r[hh][k2b], (fcv){cs, sn});
             }
             fc_dft8<1>(w);   // -> n2a
             fc_twiddle_pow<8>(w, W64 * (float)k2a);
@@ -6206,12 +6213,13 @@ static bool fc_cols_staged() {
     }();
     return v;
 }
-// the register-staged column kernels at 1024 x 16384 (EFD_FC_COLS16=0: the Stockham ones, an
-// experiment switch; read once)
-static bool fc_cols1024_staged() {
-    static const bool v = [] {
+// the column kernels at 1024 x 16384: the register-staged forward and the Stockham inverse
+// (r05z3: staged forward 252 against 369 us, staged inverse 549 against 476 us); EFD_FC_COLS16
+// = 0 both Stockham, 2 both staged (an experiment switch; read once)
+static int fc_cols1024_mode() {
+    static const int v = [] {
         const char* e = getenv("EFD_FC_COLS16");
-        return !(e && e[0] == '0');
+        return (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
     }();
     return v;
 }
@@ -6235,7 +6243,7 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         constexpr int R16 = (1 << 24) / FC_C16;
         constexpr int NC16 = FcCols<R16>::NCOL;
         static_assert(NC16 == FCD_NCOL && R16 == FCD_R, "1024 x 16384: 8 columns per block");
-        hipLaunchKernelGGL((fc_cols1024_staged() ? k_fc_cols1024<true> : k_fc_cols<true, R16, FC_C16>),
+        hipLaunchKernelGGL((fc_cols1024_mode() >= 1 ? k_fc_cols1024<true> : k_fc_cols<true, R16, FC_C16>),
                            dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
                            (const double2*)S, stride, info, (float2*)Y);
         HIP_TRY(hipGetLastError());
@@ -6243,7 +6251,7 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                            dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st, (const float2*)kfp, m,
                            (int)rows, (float2*)Y);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL((fc_cols1024_staged() ? k_fc_cols1024<false>
+        hipLaunchKernelGGL((fc_cols1024_mode() == 2 ? k_fc_cols1024<false>
                                                  : k_fc_cols<false, R16, FC_C16>),
                            dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
                            (const double2*)nullptr, (int64_t)0, (const uint64_t*)nullptr,
