@@ -4369,8 +4369,11 @@ __device__ __forceinline__ void fc_dft8(fcv* v) {
 // with a pad element every 16
 template <int NCOL>
 struct FcColIdx {
-    // (2 columns: no pad, so m = 2^25's 4096-row blocks fit two workgroups per CU)
-    static constexpr int STRIDE = NCOL > 2 ? NCOL + 1 : NCOL;
+    // (2 columns: no pad, so m = 2^25's 4096-row blocks fit two workgroups per CU; 8 columns: no
+    // pad either, the reads of 4 lines x 8 columns by 32 lanes then fill the 64 banks (the pad
+    // of 9 made them 2-way, r05z5: 0.47 of the LDS cycles conflicts) and only the first
+    // pass's stores, 2 lines x 8 columns per 16-lane group at 8 lines apart, are 2-way)
+    static constexpr int STRIDE = (NCOL > 2 && NCOL != 8) ? NCOL + 1 : NCOL;
     __device__ __forceinline__ int operator()(int j, int e) const { return e * STRIDE + j; }
 };
 struct FcRowIdx {
@@ -4805,13 +4808,14 @@ void k_fc_rows16k(const float2* __restrict__ kfpv, int64_t m, int rows, float2* 
 // k_fc_rows16k with every exchange in two passes (real parts, then imaginary parts) through a
 // float array: 69.6 KB of LDS and at most 128 VGPRs, so two workgroups share a CU and one's
 // loads and stores overlap the other's transforms (one per CU leaves HBM idle while it
-// computes). Exchange 1 [k1][n2] stride 514, exchange 2 [k2a] stride 544 [n2a][k1]: every b32
-// access of a wave hits 64 distinct banks.
-constexpr int FR16_T1 = 514, FR16_T2 = 544;
+// computes). Exchange 1 [k1][n2] stride 513, exchange 2 [k2a][n2a][k1] unpadded: every b32
+// access of a 32-lane bank group hits 32 distinct banks (ds_read_b32 / ds_write_b32 bank
+// (a/4) mod 32; stride 514 read exchange 1 2-way, r05z5: 0.20 of the LDS cycles conflicts).
+constexpr int FR16_T1 = 513, FR16_T2 = 512;
 __global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_fc_rows16k_h(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
     static_assert(FC_NT == 512 && FC_C16 == 32 * 32 * 16, "16384 = 32 x 32 x 16, 512 threads");
-    __shared__ float sf[32 * FR16_T2];
+    __shared__ float sf[32 * (FR16_T1 > FR16_T2 ? FR16_T1 : FR16_T2)];
     const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
     fcv* Y = reinterpret_cast<fcv*>(Yv);
     const int64_t npair = (int64_t)gridDim.x;

@@ -4,7 +4,8 @@
 
 Per kernel and counter: the mean over the kernel's dispatches (each dispatch's value summed over
 its instances). The SQ cycle counters count quad-cycles (MI355X_MICROARCH.md); ratios such as
-WAIT_ANY / WAVE_CYCLES are what the notes read.
+WAIT_ANY / WAVE_CYCLES are what the notes read; TA_BUSY_avr / GRBM_GUI_ACTIVE is the texture
+addresser's busy fraction (the vector memory path's issue bound).
 """
 
 import collections
@@ -23,8 +24,10 @@ def short(name):
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     out = collections.defaultdict(dict)
-    for p in ("diag1", "diag2"):
+    for p in ("diag1", "diag2", "diag3"):
         f = os.path.join(src, p, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
         agg = collections.defaultdict(float)
         names = {}
         for r in csv.DictReader(open(f)):
@@ -43,6 +46,8 @@ def main(tag):
                       "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
                 if n in c:
                     c["frac_" + n] = c[n] / w
+        if c.get("GRBM_GUI_ACTIVE") and "TA_BUSY_avr" in c:
+            c["frac_TA_BUSY"] = c["TA_BUSY_avr"] / c["GRBM_GUI_ACTIVE"]
         if c.get("SQ_LDS_IDX_ACTIVE"):
             c["lds_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"]
     dst = os.path.join(ROOT, "profiles", f"{tag}_windowed_diag.json")
