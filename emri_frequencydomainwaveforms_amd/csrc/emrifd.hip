@@ -5255,7 +5255,6 @@ __global__ void k_hann_polarizations(const double2* __restrict__ S, const float2
 // (workgroup b runs on XCD b mod 8), so d and w (48 B per bin, the same for every row) come from
 // HBM once and from that XCD's L2 for the other rows. part[row * nchunk + chunk].
 constexpr int HANN_ROWS_MAX = 16;
-template <int UNROLL>
 __global__ __launch_bounds__(256) void k_hann_loglike_partial(
     const double2* __restrict__ S, int64_t stride, const float2* __restrict__ Y,
     const uint64_t* __restrict__ info, int64_t m, int64_t nf, int64_t k0,
@@ -5270,7 +5269,6 @@ __global__ __launch_bounds__(256) void k_hann_loglike_partial(
     const float2* Yr = Y + (int64_t)r * m;
     const int64_t nb = nf - k0;
     double acc = 0.0;
-#pragma unroll UNROLL
     for (int64_t i = (int64_t)chunk * 256 + threadIdx.x; i < nb; i += (int64_t)nchunk * 256) {
         const double2 d0 = d[i], d1 = d[nb + i];
         const double w0 = w[i], w1 = w[nb + i];
@@ -6335,13 +6333,7 @@ int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint
                                           ((nb + threads - 1) / threads + 7) / 8 * 8);
     hipStream_t st = (hipStream_t)stream;
     static_assert(EFD_LOGLIKE_SCRATCH % 8 == 0, "chunks: whole rounds of the 8 XCDs");
-    static const int unroll = [] {   // EFD_HANN_UNROLL = 2 / 4: an experiment switch (read once)
-        const char* e = getenv("EFD_HANN_UNROLL");
-        return e && (e[0] == '2' || e[0] == '4') ? e[0] - '0' : 1;
-    }();
-    hipLaunchKernelGGL(unroll == 4 ? k_hann_loglike_partial<4>
-                       : unroll == 2 ? k_hann_loglike_partial<2> : k_hann_loglike_partial<1>,
-                       dim3((unsigned)(np * rows)), dim3(threads), 0, st,
+    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)(np * rows)), dim3(threads), 0, st,
                        (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
                        (const double2*)d, w, (int)rows, np, scratch);
     HIP_TRY(hipGetLastError());
