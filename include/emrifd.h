@@ -331,10 +331,11 @@ int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows,
 int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
                    const uint64_t* info, int64_t m, float* Y, void* stream);
 /* efd_hann_stage + the caller's transform pair in one call, for power-of-two m in [2^21, 2^25]
- * (a four-step FFT: column FFTs of length R = m / 8192 with the staging folded in, row FFTs
- * of 8192 with the kernel multiply between forward and inverse, inverse column FFTs; the
- * spectrum is never reordered). kfp: the lag kernel's spectrum / m, complex64 in the four-step
- * order kfp[f_r 8192 + f_c] = kf[f_r + R f_c]. Leaves Y as efd_hann_stage + transforms do. */
+ * (a four-step FFT: column FFTs of length R = m / C with the staging folded in, row FFTs of
+ * C with the kernel multiply between forward and inverse, inverse column FFTs; the spectrum is
+ * never reordered; C = efd_hann_four_step_cols(m)). kfp: the lag kernel's spectrum / m,
+ * complex64 in the four-step order kfp[f_r C + f_c] = kf[f_r + R f_c]. Leaves Y as
+ * efd_hann_stage + transforms do. */
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream);
 /* The four-step split's row length C that efd_hann_convolve uses for transform length m
