@@ -220,16 +220,22 @@ def test_four_step_convolution(n, support, rows, m):
     _four_step_check(n, support, rows, m, 16384 if m == 1 << 24 else 8192)
 
 
-def test_four_step_convolution_8192_rows_at_2_24():
-    """The 2048 x 8192 split at m = 2^24 (EFD_FC_C16=0, read once per process: a child
-    process) to the same checks as test_four_step_convolution."""
+@pytest.mark.parametrize("env,cols", [
+    ({"EFD_FC_C16": "0"}, 8192),
+    ({"EFD_FC_R16H": "0", "EFD_FC_COLS16": "2"}, 16384),
+    ({"EFD_FC_COLS16": "0"}, 16384)])
+def test_four_step_convolution_variants_at_2_24(env, cols):
+    """The experiment switches' kernels at m = 2^24 (read once per process: a child process
+    each) to the same checks as test_four_step_convolution: the 2048 x 8192 split
+    (EFD_FC_C16=0); the one-workgroup-per-CU 16384-point rows with the staged inverse columns;
+    the Stockham forward columns."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = ("from tests.test_gpu_windowed import _four_step_check; "
-            "_four_step_check(12623261, (0.43, 0.57), 2, 1 << 24, 8192)")
+            f"_four_step_check(12623261, (0.43, 0.57), 2, 1 << 24, {cols})")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
-                       env=dict(os.environ, EFD_FC_C16="0"), timeout=240)
+                       env=dict(os.environ, **env), timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
 
 
