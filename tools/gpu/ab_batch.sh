@@ -1,3 +1,6 @@
+#!/bin/bash
+# GPU box: bench.py at 8 and 16 waveforms per launch, 3 rotated rounds (r05zb).
+#   bash tools/gpu/ab_batch.sh
 set -o pipefail
 O=gpurun_out/r05zb; mkdir -p $O
 for r in 1 2 3; do
