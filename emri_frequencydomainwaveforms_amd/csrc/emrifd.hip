@@ -6179,8 +6179,10 @@ int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows,
     hipLaunchKernelGGL(k_hann_info_init, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, info,
                        rows);
     HIP_TRY(hipGetLastError());
-    // (with lane ranges the rows' supports are a fraction of the grid: fewer workgroups)
-    const int64_t cap = lanes ? std::max(16, 256 / rows) : std::max(64, 1024 / rows);
+    // ~4096 workgroups in all: the scan is latency-bound per thread (one load per iteration), so
+    // the grid sets the loads in flight (32 blocks a row with lane ranges took 44 us for 8
+    // rows, r05z6: ~57 dependent iterations a thread); blocks past a row's range leave at once
+    const int64_t cap = std::max(128, 4096 / rows);
     const int64_t blocks = std::min<int64_t>(cap, (nf + 255) / 256);
     hipLaunchKernelGGL(k_hann_extent, dim3((unsigned)blocks, (unsigned)rows), dim3(256), 0, st,
                        (const double2*)S, stride, nf, lanes, info);
