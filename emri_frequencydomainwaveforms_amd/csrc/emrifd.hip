@@ -4229,6 +4229,7 @@ __global__ __launch_bounds__(256) void k_hann_extent(const double2* __restrict__
         }
     }
     uint64_t mx = 0, lo = ~0ull, hi = 0;
+#pragma unroll 8
     for (int64_t k = k_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < k_hi;
          k += (int64_t)gridDim.x * blockDim.x) {
         const double2 v = row[k];
@@ -6179,10 +6180,10 @@ int efd_hann_extent(const double* S, int64_t stride, int64_t nf, int32_t rows,
     hipLaunchKernelGGL(k_hann_info_init, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, info,
                        rows);
     HIP_TRY(hipGetLastError());
-    // ~4096 workgroups in all: the scan is latency-bound per thread (one load per iteration), so
-    // the grid sets the loads in flight (32 blocks a row with lane ranges took 44 us for 8
-    // rows, r05z6: ~57 dependent iterations a thread); blocks past a row's range leave at once
-    const int64_t cap = std::max(128, 4096 / rows);
+    // (with lane ranges the rows' supports are a fraction of the grid: fewer workgroups; each
+    // block's 3 atomics on its row's words serialise, so the grid stays small -- 512 blocks a
+    // row took 94 against 44 us for 32, r05z8 -- and the loop is unrolled for loads in flight)
+    const int64_t cap = lanes ? std::max(16, 512 / rows) : std::max(64, 1024 / rows);
     const int64_t blocks = std::min<int64_t>(cap, (nf + 255) / 256);
     hipLaunchKernelGGL(k_hann_extent, dim3((unsigned)blocks, (unsigned)rows), dim3(256), 0, st,
                        (const double2*)S, stride, nf, lanes, info);
