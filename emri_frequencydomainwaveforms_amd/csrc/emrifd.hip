@@ -5135,23 +5135,13 @@ void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t
 #pragma unroll
             for (int a = 0; a < 8; ++a) w[a] = sm[e2(k1, k2a, a, j)];
             fc_dft8<-1>(w);
-            // times w_M^(c fr), fr = k1 + 16 k2a + 128 k2b: two __sincosf and a product chain
-            // (the per-element form measured no faster and takes 16 transcendental pairs)
-            fcv tw, st;
-            {
-                const uint32_t p0 = (uint32_t)c * (uint32_t)(k1 + 16 * k2a);   // < M
-                const uint32_t ps = (uint32_t)c * 128u;
-                float sn, cs;
-                __sincosf(-FC_2PI * ((float)p0 * (1.0f / (float)M)), &sn, &cs);
-                tw = (fcv){cs, sn};
-                __sincosf(-FC_2PI * ((float)ps * (1.0f / (float)M)), &sn, &cs);
-                st = (fcv){cs, sn};
-            }
 #pragma unroll
             for (int k2b = 0; k2b < 8; ++k2b) {
                 const int fr = k1 + 16 * k2a + 128 * k2b;
-                y[(int64_t)fr * C + c] = cmulf(w[k2b], tw);
-                tw = cmulf(tw, st);
+                const uint32_t pp = (uint32_t)c * (uint32_t)fr;   // < C R = M: no reduction
+                float sn, cs;
+                __sincosf(-FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
+                y[(int64_t)fr * C + c] = cmulf(w[k2b], (fcv){cs, sn});
             }
         }
     } else {
@@ -5165,20 +5155,14 @@ void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {   // inverse (C): tasks (j, k2a, k1)
             const int q = t + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
-            fcv w[8], tw, st;
-            {
-                const uint32_t p0 = (uint32_t)c * (uint32_t)(k1 + 16 * k2a);
-                const uint32_t ps = (uint32_t)c * 128u;
-                float sn, cs;
-                __sincosf(FC_2PI * ((float)p0 * (1.0f / (float)M)), &sn, &cs);
-                tw = (fcv){cs, sn};
-                __sincosf(FC_2PI * ((float)ps * (1.0f / (float)M)), &sn, &cs);
-                st = (fcv){cs, sn};
-            }
+            fcv w[8];
 #pragma unroll
             for (int k2b = 0; k2b < 8; ++k2b) {
-                w[k2b] = cmulf(r[hh][k2b], tw);
-                tw = cmulf(tw, st);
+                const int fr = k1 + 16 * k2a + 128 * k2b;
+                const uint32_t pp = (uint32_t)c * (uint32_t)fr;
+                float sn, cs;
+                __sincosf(FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
+                w[k2b] = cmulf(r[hh][k2b], (fcv){cs, sn});
             }
             fc_dft8<1>(w);   // -> n2a
             fc_twiddle_pow<8>(w, W64 * (float)k2a);
