@@ -209,7 +209,9 @@ def test_hann_loglike_matches_templates():
 @pytest.mark.parametrize("n,support,rows,m", [
     (1000001, (0.4, 0.9), 3, 1 << 21), (2000001, (0.3, 0.9), 2, 1 << 22),
     (4000001, (0.3, 0.9), 2, 1 << 23), (12623261, (0.43, 0.57), 2, 1 << 24),
-    (12623261, (0.2, 0.8), 2, 1 << 25)])
+    (12623261, (0.2, 0.8), 2, 1 << 25),
+    # the most rows a call takes (EFD_HANN_ROWS_MAX) and a lone all-zero row
+    (12623261, (0.45, 0.55), 16, 1 << 24), (12623261, (0.45, 0.55), 1, 1 << 24)])
 def test_four_step_convolution(n, support, rows, m):
     """efd_hann_convolve (the four-step complex64 FFT pipeline, every split it has: m = 2^21 ..
     2^25 as R x 8192, R = 256 .. 4096, except 2^24 = 1024 x 16384) against
