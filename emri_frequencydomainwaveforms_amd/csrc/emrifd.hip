@@ -5256,38 +5256,61 @@ __global__ void k_hann_polarizations(const double2* __restrict__ S, const float2
 // (workgroup b runs on XCD b mod 8), so d and w (48 B per bin, the same for every row) come from
 // HBM once and from that XCD's L2 for the other rows. part[row * nchunk + chunk].
 constexpr int HANN_ROWS_MAX = 16;
+// RPT rows per workgroup (rows = RPT x the row groups; a thread reads its bin's d and w once
+// for all of them: 48 B of the ~176 a bin-row loads from L1/L2). The rows of a chunk's row
+// groups are consecutive workgroups of one XCD as with one row each; every row's partial sums
+// the same bins in the same order, so the output is bitwise that of RPT = 1.
+template <int RPT>
 __global__ __launch_bounds__(256) void k_hann_loglike_partial(
     const double2* __restrict__ S, int64_t stride, const float2* __restrict__ Y,
     const uint64_t* __restrict__ info, int64_t m, int64_t nf, int64_t k0,
     const double2* __restrict__ d, const double* __restrict__ w, int rows, int nchunk,
     double* __restrict__ part) {
 #pragma clang fp contract(off)
+    const int ngr = rows / RPT;
     const int j = (int)(blockIdx.x >> 3);
-    const int r = j % rows, chunk = (int)(blockIdx.x & 7) + 8 * (j / rows);
-    const HannRow h = hann_row(info, r);
-    const double c = h.scale / (4.0 * (double)(nf - 1));
-    const double2* Sr = S + (int64_t)r * stride;
-    const float2* Yr = Y + (int64_t)r * m;
+    const int r0 = (j % ngr) * RPT, chunk = (int)(blockIdx.x & 7) + 8 * (j / ngr);
+    double c[RPT];
+    int64_t first[RPT], len[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const HannRow h = hann_row(info, r0 + q);
+        c[q] = h.scale / (4.0 * (double)(nf - 1));
+        first[q] = h.first;
+        len[q] = h.len;
+    }
     const int64_t nb = nf - k0;
-    double acc = 0.0;
+    double acc[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) acc[q] = 0.0;
     for (int64_t i = (int64_t)chunk * 256 + threadIdx.x; i < nb; i += (int64_t)nchunk * 256) {
         const double2 d0 = d[i], d1 = d[nb + i];
         const double w0 = w[i], w1 = w[nb + i];
-        double2 vp, vc;
-        hann_pol(Sr, Yr, nf, k0 + i, c, h.first, h.len, m - nf, vp, vc);
-        const double r0 = d0.x - vp.x * w0, i0 = d0.y - vp.y * w0;
-        const double r1 = d1.x - vc.x * w1, i1 = d1.y - vc.y * w1;
-        acc = fma(r0, r0, fma(i0, i0, acc));
-        acc = fma(r1, r1, fma(i1, i1, acc));
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            double2 vp, vc;
+            hann_pol(S + (int64_t)(r0 + q) * stride, Y + (int64_t)(r0 + q) * m, nf, k0 + i, c[q],
+                     first[q], len[q], m - nf, vp, vc);
+            const double x0 = d0.x - vp.x * w0, y0 = d0.y - vp.y * w0;
+            const double x1 = d1.x - vc.x * w1, y1 = d1.y - vc.y * w1;
+            acc[q] = fma(x0, x0, fma(y0, y0, acc[q]));
+            acc[q] = fma(x1, x1, fma(y1, y1, acc[q]));
+        }
     }
     // a butterfly over each wave, then the 4 waves in turn (fixed order)
-    __shared__ double red[4];
+    __shared__ double red[RPT][4];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    for (int q = 0; q < RPT; ++q) {
+        double a = acc[q];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = a;
+    }
     __syncthreads();
-    if (threadIdx.x == 0 && chunk < nchunk)
-        part[(int64_t)r * nchunk + chunk] = ((red[0] + red[1]) + red[2]) + red[3];
+    if (threadIdx.x < RPT && chunk < nchunk) {
+        const int q = threadIdx.x;
+        part[(int64_t)(r0 + q) * nchunk + chunk] = ((red[q][0] + red[q][1]) + red[q][2]) + red[q][3];
+    }
 }
 
 // fused log-likelihood partials: one workgroup per chunk, then a second pass
@@ -6336,7 +6359,14 @@ int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint
                                           ((nb + threads - 1) / threads + 7) / 8 * 8);
     hipStream_t st = (hipStream_t)stream;
     static_assert(EFD_LOGLIKE_SCRATCH % 8 == 0, "chunks: whole rounds of the 8 XCDs");
-    hipLaunchKernelGGL(k_hann_loglike_partial, dim3((unsigned)(np * rows)), dim3(threads), 0, st,
+    // two rows a workgroup when the rows pair up (EFD_HANN_RPT=1: one, an experiment switch)
+    static const int rpt_env = [] {
+        const char* e = getenv("EFD_HANN_RPT");
+        return e && e[0] == '1' ? 1 : 2;
+    }();
+    const int rpt = (rows % 2 == 0) ? rpt_env : 1;
+    hipLaunchKernelGGL(rpt == 2 ? k_hann_loglike_partial<2> : k_hann_loglike_partial<1>,
+                       dim3((unsigned)(np * (rows / rpt))), dim3(threads), 0, st,
                        (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
                        (const double2*)d, w, (int)rows, np, scratch);
     HIP_TRY(hipGetLastError());

@@ -14,7 +14,7 @@ for r in $(seq 1 $R); do
     env $( [ "$v" = "-" ] || echo $v ) timeout -k 10 300 python tools/windowed_profile.py 5 > $O/wab.json 2> $O/wab.err || { tail -5 $O/wab.err; exit 2; }
     python -c "
 import json,sys
-d=json.load(open(sys.argv[1])); print('WAB', sys.argv[2], sys.argv[3], round(d['ms_per_half_step'],3))" $O/wab.json "$v" $r
+d=json.load(open(sys.argv[1])); print('WAB', sys.argv[2], sys.argv[3], round(d['ms_per_half_step'],3), d.get('ll_sha16'))" $O/wab.json "$v" $r
   done
 done
 bash tools/gpu/windowed_prof.sh $TAG

@@ -6,9 +6,11 @@ emri_pe.py:259-263, FDutils.py:66-101) for kernel-trace and PMC attribution (GPU
 Device path (host upstream memoised after the warm-up), STEPS timed half-steps of 8 walkers
 between two marker launches (efd_polarizations on a 3-bin grid: k_polarizations, which the
 windowed path never launches otherwise), so a rocprofv3 --kernel-trace CSV of this command can
-be cut to the timed region (tools/windowed_summary.py). Prints one JSON line: ms per half-step.
+be cut to the timed region (tools/windowed_summary.py). Prints one JSON line: ms per half-step
+and a hash of the batch's logL (variants that must agree bitwise compare it).
 """
 
+import hashlib
 import json
 import os
 import sys
@@ -51,10 +53,12 @@ def main():
     el = time.perf_counter() - t0
     marker(lib, buf, st)
     torch.cuda.synchronize()
+    ll = np.asarray(like(batch, **s.kwargs), dtype=np.float64)
     memo.remove()
     print(json.dumps({"config": "test.sh windowed, 8 walkers per half-step", "steps": steps,
                       "ms_per_half_step": el / steps * 1e3, "N_f": s.info["N_f"],
-                      "loglikes_per_s": len(batch) * steps / el}))
+                      "loglikes_per_s": len(batch) * steps / el,
+                      "ll_sha16": hashlib.sha256(ll.tobytes()).hexdigest()[:16]}))
 
 
 if __name__ == "__main__":
