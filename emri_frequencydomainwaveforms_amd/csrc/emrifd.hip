@@ -6362,11 +6362,10 @@ int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint
     // two rows a workgroup when the rows pair up (EFD_HANN_RPT=1: one, an experiment switch)
     static const int rpt_env = [] {
         const char* e = getenv("EFD_HANN_RPT");
-        return e && (e[0] == '1' || e[0] == '4') ? e[0] - '0' : 2;
+        return e && e[0] == '1' ? 1 : 2;
     }();
-    const int rpt = (rows % rpt_env == 0) ? rpt_env : (rows % 2 == 0 ? 2 : 1);
-    hipLaunchKernelGGL(rpt == 4   ? k_hann_loglike_partial<4>
-                       : rpt == 2 ? k_hann_loglike_partial<2> : k_hann_loglike_partial<1>,
+    const int rpt = (rows % 2 == 0) ? rpt_env : 1;
+    hipLaunchKernelGGL(rpt == 2 ? k_hann_loglike_partial<2> : k_hann_loglike_partial<1>,
                        dim3((unsigned)(np * (rows / rpt))), dim3(threads), 0, st,
                        (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,
                        (const double2*)d, w, (int)rows, np, scratch);
