@@ -473,7 +473,9 @@ class get_fd_waveform_fromFD:
             if lb is None or lb.shape[0] < B or lb.device != dev:
                 lb = self._lanes = torch.empty((max(B, 16), 2), dtype=torch.int32, device=dev)
             lanes = lb[:B]
-            gen.spectrum_batch(params, buf[:B], lanes=lanes, **kwargs)
+            # the status is read once the caller's window work is queued (_status): one host
+            # synchronisation fewer between the mode sum and the transforms
+            gen.spectrum_batch(params, buf[:B], lanes=lanes, check=False, **kwargs)
         else:
             for i, p in enumerate(params):
                 gen._spectrum(*p, out=buf[i], check=False, **kwargs)
@@ -483,7 +485,9 @@ class get_fd_waveform_fromFD:
         return buf[:B], cw, single, lanes
 
     def _status(self, cw, single):
-        if single and not cw.engine.status():
+        if not single:
+            self.waveform_generator.check_batch()
+        elif not cw.engine.status():
             from . import _lib
             raise _lib.EFDError(f"efd_modesum: {_lib.last_error(cw.engine.lib)}")
 

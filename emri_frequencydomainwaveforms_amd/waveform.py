@@ -456,12 +456,14 @@ class GenerateEMRIWaveform:
                                T, dt, eps, f_arr, kwargs)
 
     def spectrum_batch(self, params, out, T=1.0, dt=10.0, eps=1e-5, f_arr=None, lanes=None,
-                       **kwargs):
+                       check=True, **kwargs):
         """The two-sided spectra S = h+ - i hx of every row of params into the rows of out
         (complex128 [B][N], contiguous rows, on the device): generate_batch's device groups
         with the sum writing S (the windowed templates' input, fdutils.HannConvolution); bitwise
         the spectrum path's S of each row. lanes (int32 [B][2] on the device, optional): each
-        row's lane range (efd_modesum_lane_ranges), the bins its terms can reach."""
+        row's lane range (efd_modesum_lane_ranges), the bins its terms can reach. check=False
+        leaves the device-side status unread (no host synchronisation here): the caller then
+        calls check_batch() once its own work on the spectra is queued."""
         torch = require_gpu()
         n = self._batch_grid(T, dt, f_arr)[0]
         B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
@@ -472,7 +474,14 @@ class GenerateEMRIWaveform:
                                   or not lanes.is_contiguous()):
             raise ValueError(f"lanes must be contiguous int32 [{B}][2]")
         return self._run_batch(params, out, lambda j: dict(out=torch.view_as_real(out[j])),
-                               T, dt, eps, f_arr, kwargs, lanes=lanes)
+                               T, dt, eps, f_arr, kwargs, lanes=lanes, check=check)
+
+    def check_batch(self):
+        """Synchronise the last batch's groups and raise if a workspace reported a device-side
+        error (what spectrum_batch(check=False) skipped)."""
+        st = getattr(self, "_gen_batch", None)
+        if st is not None:
+            st["prep"].wait()
 
     def positive_bins(self, T=1.0, dt=10.0, f_arr=None):
         """N_pos, the f >= 0 bins of the grid generate_batch writes (its out's last dimension)."""
@@ -488,7 +497,8 @@ class GenerateEMRIWaveform:
             raise ValueError("the batched generator needs a symmetric grid")
         return int(freq.numel()), int(freq.numel()) - cw._k0
 
-    def _run_batch(self, params, out, outputs, T, dt, eps, f_arr, kwargs, lanes=None):
+    def _run_batch(self, params, out, outputs, T, dt, eps, f_arr, kwargs, lanes=None,
+                   check=True):
         torch = require_gpu()
         from .summation import BatchPreparer, sum_batch
         cw = self.waveform_generator.create_waveform
@@ -527,7 +537,8 @@ class GenerateEMRIWaveform:
         finally:
             prep._pending = []
             cur.wait_stream(s_sum)
-        prep.wait()   # device-side errors of the groups' workspaces raise here
+        if check:
+            prep.wait()   # device-side errors of the groups' workspaces raise here
         return out
 
     # prefetch(wait=False) is supported (the likelihood's groups then overlap the upstream)
