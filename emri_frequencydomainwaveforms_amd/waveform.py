@@ -444,8 +444,8 @@ class GenerateEMRIWaveform:
         The host upstream of all rows runs at once on the thread pool (prefetch: trajectory,
         amplitudes, selection; this rank's host-core share), then the device work goes in
         groups of BATCH_GROUP: one packed upload and one efd_modesum_prepare_batch per group on
-        that group's stream, one efd_modesum_sum_batch writing the group's h+/hx, two groups in
-        flight. Returns out, ordered after the work on the current stream."""
+        that group's stream, one efd_modesum_sum_batch writing the group's h+/hx on the same
+        stream, two groups in flight. Returns out, ordered after the work on the current stream."""
         torch = require_gpu()
         npos = self._batch_grid(T, dt, f_arr)[1]
         B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
@@ -513,30 +513,37 @@ class GenerateEMRIWaveform:
                 or st["prep"].group != G):
             st = self._gen_batch = dict(
                 prep=BatchPreparer(group=G, depth=2, caustic=cw.caustic, device=out.device),
-                stream=torch.cuda.Stream(out.device), device=out.device,
+                device=out.device,
                 ev=[torch.cuda.Event(), torch.cuda.Event()])
-        prep, s_sum = st["prep"], st["stream"]
+        prep = st["prep"]
         cur = torch.cuda.current_stream(out.device)
         prep.order_after_current()
-        s_sum.wait_stream(cur)
+        # each group's sum on the group's own stream, right behind its preparation (no
+        # cross-stream wait between the two: ~34 us of idle device a group in the windowed
+        # trace, r05zg); group i + 1's preparation on the other stream still runs beside it,
+        # and the current stream joins every used group stream at the end
+        used = []
         try:
             for g0 in range(0, B, G):
                 rows = params[g0:g0 + G]
                 self.submit_batch(prep, rows, T=T, dt=dt, eps=eps, f_arr=f_arr, **kwargs)
                 gi, jobs = prep.flush()
-                s_sum.wait_stream(prep.stream(gi))
+                gs = prep.stream(gi)
                 sum_batch([(eng, dict(kw, **outputs(g0 + i)))
-                           for i, (eng, kw) in enumerate(jobs)], stream=s_sum.cuda_stream)
+                           for i, (eng, kw) in enumerate(jobs)], stream=gs.cuda_stream)
                 if lanes is not None:   # before the group's workspaces are released
                     _lib.check(prep.lib.efd_modesum_lane_ranges(
                         prep.groups[gi]["pw"], len(jobs), lanes[g0].data_ptr(),
-                        s_sum.cuda_stream), "efd_modesum_lane_ranges", prep.lib)
+                        gs.cuda_stream), "efd_modesum_lane_ranges", prep.lib)
                 ev = st["ev"][gi]
-                ev.record(s_sum)
+                ev.record(gs)
                 prep.release(gi, ev)
+                if gi not in used:
+                    used.append(gi)
         finally:
             prep._pending = []
-            cur.wait_stream(s_sum)
+            for gi in used:
+                cur.wait_stream(prep.stream(gi))
         if check:
             prep.wait()   # device-side errors of the groups' workspaces raise here
         return out
