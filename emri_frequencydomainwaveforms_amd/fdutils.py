@@ -208,12 +208,14 @@ class HannConvolution:
                              f"{self.device}")
         return S
 
-    def transform(self, S, lib, lanes=None):
+    def transform(self, S, lib, lanes=None, support=None):
         """(Y, info, m) for the rows of S ([rows][n], complex128, contiguous): Y complex64
         [rows][m] holds each row's C / scale at ((k - first) mod n) + m - n (efd_hann_stage's
         layout after the transform pair); info int64 [rows][4] (efd_hann_extent). One host
         synchronisation: the rows' supports choose m. lanes: the rows' lane ranges
-        (GenerateEMRIWaveform.spectrum_batch), so the extent reads only their bins."""
+        (GenerateEMRIWaveform.spectrum_batch), so the extent reads only their bins. support:
+        an upper bound of every row's support known on the host (lane_support), which chooses
+        m instead: no synchronisation."""
         from . import _hipfft, _lib
         torch = require_gpu()
         S = self._rows(S)
@@ -230,10 +232,11 @@ class HannConvolution:
             lp = lanes.data_ptr()
         _lib.check(lib.efd_hann_extent(sp, n, n, rows, lp, info.data_ptr(), st),
                    "efd_hann_extent", lib)
-        ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
-        live = ext[:, 1] > 0
-        support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
-        m = self.size_for(n, support, self.four_step)
+        if support is None:
+            ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
+            live = ext[:, 1] > 0
+            support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
+        m = self.size_for(n, max(int(support), 1), self.four_step)
         need = rows * m
         if self._ybuf is None or self._ybuf.numel() < need:
             self._ybuf = None
@@ -294,7 +297,22 @@ class HannConvolution:
         self.polarizations_batch(self._rows(S), [(hp, hc)], k0, lib)
         return hp, hc
 
-    def loglike_batch(self, S, d, w, k0, out, scratch, lib, lanes=None):
+    @staticmethod
+    def lane_support(lanes_host, n):
+        """The largest support any row can have given its lane range (int32 [rows][2] on the
+        host): efd_hann_extent scans [min(lo, n - hi), max(hi, n - lo)) of a row with lanes
+        [lo, hi), and the row's nonzero bins lie inside it, so its support (last + 1 - first)
+        is at most that span; a transform length chosen for the span is long enough."""
+        lo = lanes_host[:, 0].astype(np.int64)
+        hi = lanes_host[:, 1].astype(np.int64)
+        live = hi > lo
+        if not live.any():
+            return 1
+        k_lo = np.maximum(0, np.minimum(lo, n - hi))
+        k_hi = np.minimum(n, np.maximum(hi, n - lo))
+        return int((k_hi - k_lo)[live].max())
+
+    def loglike_batch(self, S, d, w, k0, out, scratch, lib, lanes=None, support=None):
         """efd_hann_loglike: the logL of every row's windowed template against d, w
         (efd_loglike's [2][n - k0] layout) into out (float64 device [rows]); scratch holds
         rows * EFD_LOGLIKE_SCRATCH doubles."""
@@ -302,7 +320,7 @@ class HannConvolution:
         torch = require_gpu()
         S = self._rows(S)
         rows = int(S.shape[0])
-        Y, info, m = self.transform(S, lib, lanes)
+        Y, info, m = self.transform(S, lib, lanes, support)
         st = torch.cuda.current_stream(S.device).cuda_stream
         _lib.check(lib.efd_hann_loglike(
             torch.view_as_real(S).data_ptr(), self.n, torch.view_as_real(Y).data_ptr(),
@@ -473,9 +491,15 @@ class get_fd_waveform_fromFD:
             if lb is None or lb.shape[0] < B or lb.device != dev:
                 lb = self._lanes = torch.empty((max(B, 16), 2), dtype=torch.int32, device=dev)
             lanes = lb[:B]
-            # the status is read once the caller's window work is queued (_status): one host
-            # synchronisation fewer between the mode sum and the transforms
-            gen.spectrum_batch(params, buf[:B], lanes=lanes, check=False, **kwargs)
+            lh = getattr(self, "_lanes_host", None)
+            if lh is None or lh.shape[0] < B:
+                lh = self._lanes_host = torch.empty((max(B, 16), 2), dtype=torch.int32,
+                                                    pin_memory=True)
+            # the status is read once the caller's window work is queued (_status), and the
+            # lane ranges come to the host while the sums run (support): no host
+            # synchronisation between the mode sum and the transforms
+            gen.spectrum_batch(params, buf[:B], lanes=lanes, check=False, lanes_host=lh[:B],
+                               **kwargs)
         else:
             for i, p in enumerate(params):
                 gen._spectrum(*p, out=buf[i], check=False, **kwargs)
@@ -514,7 +538,12 @@ class get_fd_waveform_fromFD:
         if len(params) == 0:
             return out
         S, cw, single, lanes = self._spectra(params, **kwargs)
-        self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib, lanes)
+        support = None
+        if lanes is not None:
+            self.waveform_generator.lanes_ready()
+            support = self._hann.lane_support(self._lanes_host[:len(params)].numpy(), S.shape[1])
+        self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib, lanes,
+                                 support)
         self._status(cw, single)
         return out
 

@@ -456,14 +456,17 @@ class GenerateEMRIWaveform:
                                T, dt, eps, f_arr, kwargs)
 
     def spectrum_batch(self, params, out, T=1.0, dt=10.0, eps=1e-5, f_arr=None, lanes=None,
-                       check=True, **kwargs):
+                       check=True, lanes_host=None, **kwargs):
         """The two-sided spectra S = h+ - i hx of every row of params into the rows of out
         (complex128 [B][N], contiguous rows, on the device): generate_batch's device groups
         with the sum writing S (the windowed templates' input, fdutils.HannConvolution); bitwise
         the spectrum path's S of each row. lanes (int32 [B][2] on the device, optional): each
         row's lane range (efd_modesum_lane_ranges), the bins its terms can reach. check=False
         leaves the device-side status unread (no host synchronisation here): the caller then
-        calls check_batch() once its own work on the spectra is queued."""
+        calls check_batch() once its own work on the spectra is queued. lanes_host (pinned int32
+        [B][2], with lanes): the lane ranges are gathered right after each group's preparation
+        and copied there before its sum; lanes_ready() waits for those copies only, so the host
+        can read them while the sums run."""
         torch = require_gpu()
         n = self._batch_grid(T, dt, f_arr)[0]
         B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
@@ -473,8 +476,21 @@ class GenerateEMRIWaveform:
         if lanes is not None and (tuple(lanes.shape) != (B, 2) or lanes.dtype != torch.int32
                                   or not lanes.is_contiguous()):
             raise ValueError(f"lanes must be contiguous int32 [{B}][2]")
+        if lanes_host is not None and (lanes is None or tuple(lanes_host.shape) != (B, 2)
+                                       or lanes_host.dtype != torch.int32
+                                       or not lanes_host.is_pinned()):
+            raise ValueError(f"lanes_host must be pinned int32 [{B}][2] beside lanes")
         return self._run_batch(params, out, lambda j: dict(out=torch.view_as_real(out[j])),
-                               T, dt, eps, f_arr, kwargs, lanes=lanes, check=check)
+                               T, dt, eps, f_arr, kwargs, lanes=lanes, check=check,
+                               lanes_host=lanes_host)
+
+    def lanes_ready(self):
+        """Wait for the last spectrum_batch's lane-range copies into lanes_host (each group's
+        event; the sums behind them keep running)."""
+        st = getattr(self, "_gen_batch", None)
+        if st is not None:
+            for ev in st.get("lanes_ev_used", ()):
+                ev.synchronize()
 
     def check_batch(self):
         """Synchronise the last batch's groups and raise if a workspace reported a device-side
@@ -498,7 +514,7 @@ class GenerateEMRIWaveform:
         return int(freq.numel()), int(freq.numel()) - cw._k0
 
     def _run_batch(self, params, out, outputs, T, dt, eps, f_arr, kwargs, lanes=None,
-                   check=True):
+                   check=True, lanes_host=None):
         torch = require_gpu()
         from .summation import BatchPreparer, sum_batch
         cw = self.waveform_generator.create_waveform
@@ -514,7 +530,8 @@ class GenerateEMRIWaveform:
             st = self._gen_batch = dict(
                 prep=BatchPreparer(group=G, depth=2, caustic=cw.caustic, device=out.device),
                 device=out.device,
-                ev=[torch.cuda.Event(), torch.cuda.Event()])
+                ev=[torch.cuda.Event(), torch.cuda.Event()],
+                lanes_ev=[torch.cuda.Event(), torch.cuda.Event()])
         prep = st["prep"]
         cur = torch.cuda.current_stream(out.device)
         prep.order_after_current()
@@ -523,18 +540,26 @@ class GenerateEMRIWaveform:
         # trace, r05zg); group i + 1's preparation on the other stream still runs beside it,
         # and the current stream joins every used group stream at the end
         used = []
+        st["lanes_ev_used"] = []
         try:
             for g0 in range(0, B, G):
                 rows = params[g0:g0 + G]
                 self.submit_batch(prep, rows, T=T, dt=dt, eps=eps, f_arr=f_arr, **kwargs)
                 gi, jobs = prep.flush()
                 gs = prep.stream(gi)
-                sum_batch([(eng, dict(kw, **outputs(g0 + i)))
-                           for i, (eng, kw) in enumerate(jobs)], stream=gs.cuda_stream)
-                if lanes is not None:   # before the group's workspaces are released
+                if lanes is not None:   # the preparation's segment ranges: before the sum
                     _lib.check(prep.lib.efd_modesum_lane_ranges(
                         prep.groups[gi]["pw"], len(jobs), lanes[g0].data_ptr(),
                         gs.cuda_stream), "efd_modesum_lane_ranges", prep.lib)
+                    if lanes_host is not None:
+                        _lib.check(prep.lib.efd_download(
+                            lanes_host[g0].data_ptr(), lanes[g0].data_ptr(), 8 * len(jobs),
+                            gs.cuda_stream), "efd_download", prep.lib)
+                        lev = st["lanes_ev"][gi]
+                        lev.record(gs)
+                        st["lanes_ev_used"].append(lev)
+                sum_batch([(eng, dict(kw, **outputs(g0 + i)))
+                           for i, (eng, kw) in enumerate(jobs)], stream=gs.cuda_stream)
                 ev = st["ev"][gi]
                 ev.record(gs)
                 prep.release(gi, ev)

@@ -303,6 +303,20 @@ def test_extent_from_lane_ranges():
         lo, hi = int(ln[r, 0]), int(ln[r, 1])
         k = np.nonzero(nz[r])[0]
         assert len(k) and k.min() >= min(lo, n - hi) and k.max() < max(hi, n - lo)
+    # the host's bound from the lane ranges (what the likelihood chooses m from without a
+    # synchronisation) covers every row's support and gives the same transform length here
+    ext = info0[:, 1:3].cpu().numpy()
+    sup = int((ext[:, 1] - ext[:, 0]).max())
+    bound = HannConvolution.lane_support(ln, n)
+    assert bound >= sup and hcv.size_for(n, bound) == m0
+    Y2, info2, m2 = hcv.transform(S, lib, lanes, support=bound)
+    assert m2 == m0 and torch.equal(info2, info0) and torch.equal(Y2, Y0)
+    # lanes_host: the same ranges copied to pinned memory before the sums
+    lh = torch.empty((3, 2), dtype=torch.int32, pin_memory=True)
+    s.few.spectrum_batch(params, S, lanes=lanes, lanes_host=lh, check=False, **s.kwargs)
+    s.few.lanes_ready()
+    assert np.array_equal(lh.numpy(), ln)
+    s.few.check_batch()
 
 
 def test_windowed_likelihood_short_grid_exact_path():
