@@ -465,8 +465,8 @@ class GenerateEMRIWaveform:
         leaves the device-side status unread (no host synchronisation here): the caller then
         calls check_batch() once its own work on the spectra is queued. lanes_host (pinned int32
         [B][2], with lanes): the lane ranges are gathered right after each group's preparation
-        and copied there before its sum; lanes_ready() waits for those copies only, so the host
-        can read them while the sums run."""
+        and copied there on a side stream, beside the sum; lanes_ready() waits for those copies
+        only, so the host can read them while the sums run."""
         torch = require_gpu()
         n = self._batch_grid(T, dt, f_arr)[0]
         B = len(np.asarray(params, dtype=np.float64).reshape(-1, 14))
@@ -531,7 +531,9 @@ class GenerateEMRIWaveform:
                 prep=BatchPreparer(group=G, depth=2, caustic=cw.caustic, device=out.device),
                 device=out.device,
                 ev=[torch.cuda.Event(), torch.cuda.Event()],
-                lanes_ev=[torch.cuda.Event(), torch.cuda.Event()])
+                lanes_ev=[torch.cuda.Event(), torch.cuda.Event()],
+                prep_ev=[torch.cuda.Event(), torch.cuda.Event()],
+                lstream=torch.cuda.Stream(out.device))
         prep = st["prep"]
         cur = torch.cuda.current_stream(out.device)
         prep.order_after_current()
@@ -547,19 +549,29 @@ class GenerateEMRIWaveform:
                 self.submit_batch(prep, rows, T=T, dt=dt, eps=eps, f_arr=f_arr, **kwargs)
                 gi, jobs = prep.flush()
                 gs = prep.stream(gi)
-                if lanes is not None:   # the preparation's segment ranges: before the sum
+                if lanes_host is not None:
+                    pev = st["prep_ev"][gi]
+                    pev.record(gs)
+                sum_batch([(eng, dict(kw, **outputs(g0 + i)))
+                           for i, (eng, kw) in enumerate(jobs)], stream=gs.cuda_stream)
+                if lanes is not None:   # the preparation's segment ranges
+                    # with lanes_host: gathered and copied on a side stream behind the
+                    # preparation, beside the sum, so the host has them while the sum runs;
+                    # the group's release waits for that stream too
+                    ls = st["lstream"] if lanes_host is not None else gs
+                    if lanes_host is not None:
+                        ls.wait_event(pev)
                     _lib.check(prep.lib.efd_modesum_lane_ranges(
                         prep.groups[gi]["pw"], len(jobs), lanes[g0].data_ptr(),
-                        gs.cuda_stream), "efd_modesum_lane_ranges", prep.lib)
+                        ls.cuda_stream), "efd_modesum_lane_ranges", prep.lib)
                     if lanes_host is not None:
                         _lib.check(prep.lib.efd_download(
                             lanes_host[g0].data_ptr(), lanes[g0].data_ptr(), 8 * len(jobs),
-                            gs.cuda_stream), "efd_download", prep.lib)
+                            ls.cuda_stream), "efd_download", prep.lib)
                         lev = st["lanes_ev"][gi]
-                        lev.record(gs)
+                        lev.record(ls)
                         st["lanes_ev_used"].append(lev)
-                sum_batch([(eng, dict(kw, **outputs(g0 + i)))
-                           for i, (eng, kw) in enumerate(jobs)], stream=gs.cuda_stream)
+                        gs.wait_event(lev)
                 ev = st["ev"][gi]
                 ev.record(gs)
                 prep.release(gi, ev)
