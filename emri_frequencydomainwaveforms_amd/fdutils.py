@@ -277,13 +277,13 @@ class HannConvolution:
         C = torch.gather(Y, 1, q).to(torch.complex128) * scale[:, None]
         return C[0] if one else C
 
-    def polarizations_batch(self, S, outs, k0, lib, lanes=None):
+    def polarizations_batch(self, S, outs, k0, lib, lanes=None, support=None):
         """polarizations for every row of S ([B][n], contiguous): one transform pair over the
         rows and one efd_hann_polarizations per row into outs[i] = (hp, hc)."""
         from . import _lib
         torch = require_gpu()
         S = self._rows(S)
-        Y, info, m = self.transform(S, lib, lanes)
+        Y, info, m = self.transform(S, lib, lanes, support)
         st = torch.cuda.current_stream(S.device).cuda_stream
         for i, (hp, hc) in enumerate(outs):
             _lib.check(lib.efd_hann_polarizations(
@@ -526,9 +526,17 @@ class get_fd_waveform_fromFD:
             return outs
         S, cw, single, lanes = self._spectra(params, **kwargs)
         self._hann.polarizations_batch(S, [(o[0], o[1]) for o in outs], self._suffix_k0,
-                                       cw.engine.lib, lanes)
+                                       cw.engine.lib, lanes, self._lane_support(S, lanes))
         self._status(cw, single)
         return outs
+
+    def _lane_support(self, S, lanes):
+        """The rows' support bound from their lane ranges, on the host as soon as the copies
+        _spectra queued are done (the sums may still run), or None without lane ranges."""
+        if lanes is None:
+            return None
+        self.waveform_generator.lanes_ready()
+        return self._hann.lane_support(self._lanes_host[:S.shape[0]].numpy(), S.shape[1])
 
     def loglike_batch(self, out, params, d, w, scratch, **kwargs):
         """The windowed templates' log-likelihoods of a batch of walkers into out (float64
@@ -538,12 +546,8 @@ class get_fd_waveform_fromFD:
         if len(params) == 0:
             return out
         S, cw, single, lanes = self._spectra(params, **kwargs)
-        support = None
-        if lanes is not None:
-            self.waveform_generator.lanes_ready()
-            support = self._hann.lane_support(self._lanes_host[:len(params)].numpy(), S.shape[1])
         self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib, lanes,
-                                 support)
+                                 self._lane_support(S, lanes))
         self._status(cw, single)
         return out
 
