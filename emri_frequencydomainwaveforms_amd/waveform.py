@@ -195,6 +195,15 @@ class FastSchwarzschildEccentricFlux:
         group's own walkers are done, while the pool works on the next groups (the fused
         likelihood's half-step)."""
         calls = [tuple(c) for c in calls]
+        # calls whose upstream is already in flight or held (an earlier prefetch of the same
+        # batch, e.g. the likelihood's asynchronous one before spectrum_batch's) are not run
+        # again: prepare() takes those results
+        with self._lock:
+            calls = [c for c in calls
+                     if (k := tuple(float(v) for v in c[:11]) + (True,)) not in self._inflight
+                     and k not in self._prefetched]
+        if not calls:
+            return 0
         for c in calls:                       # Ylm per viewing angle before the threads start
             self._ylms(c[4], c[5])
         pool = _pool()

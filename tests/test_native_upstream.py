@@ -110,6 +110,7 @@ def test_prepare_native_vs_numpy_and_prefetch():
         assert dn["teuk"].shape[1] == dp["teuk"].shape[1]
     serial = [wn.prepare(*c) for c in calls]
     assert wn.prefetch(calls) == len(calls)
+    assert wn.prefetch(calls[:3]) == 0             # held already: not run again
     for c, ref in zip(calls, serial):
         got = wn.prepare(*c)                       # taken from the prefetched results
         for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
@@ -125,6 +126,10 @@ def test_prepare_native_vs_numpy_and_prefetch():
     wn._prefetched.clear()
     wn._prefetched_bytes = 0
     assert wn.prefetch(calls, wait=False) == len(calls) and len(wn._inflight) == len(calls)
+    # a second prefetch of the same batch (spectrum_batch's after the likelihood's) runs
+    # nothing again: the in-flight results serve it
+    assert wn.prefetch(calls) == 0 and wn.prefetch(calls, wait=False) == 0
+    assert len(wn._inflight) == len(calls) and not wn._prefetched
     for c, ref in zip(calls, serial):
         got = wn.prepare(*c)
         for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
