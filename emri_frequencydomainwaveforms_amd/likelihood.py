@@ -217,12 +217,15 @@ class Likelihood:
             # and the windowed templates' logL reduced in place (efd_hann_loglike, at most
             # EFD_HANN_ROWS_MAX rows a call). The batch takes keyword waveform arguments only;
             # extra positional ones go to the per-walker fill below, which forwards them
-            G = min(max(1, int(getattr(tm, "WINDOW_GROUP", 8))), _lib.EFD_HANN_ROWS_MAX)
+            G = min(max(1, int(os.environ.get("EFD_WINDOW_GROUP", 0))
+                        or int(getattr(tm, "WINDOW_GROUP", 8))), _lib.EFD_HANN_ROWS_MAX)
             scr = getattr(self, "_wscratch", None)
             if scr is None or scr.numel() < G * _lib.EFD_LOGLIKE_SCRATCH:
                 scr = self._wscratch = torch.empty(G * _lib.EFD_LOGLIKE_SCRATCH,
                                                    dtype=torch.float64, device=self.device)
-            _prefetch(tm, params, args, kwargs)
+            # the upstream G walkers at a time, in order: the first group's device work then
+            # overlaps the later walkers' upstream
+            _prefetch(tm, params, args, kwargs, concurrency=G if G < num_likes else None)
             for g0 in range(0, num_likes, G):
                 rows = params[g0:g0 + G]
                 tm.loglike_batch(out[g0:g0 + len(rows)], rows, self._d, self._w_templ, scr,
@@ -470,14 +473,18 @@ class Likelihood:
         return np.concatenate(out_ll, axis=0)
 
 
-def _prefetch(tm, params, args, kwargs):
+def _prefetch(tm, params, args, kwargs, concurrency=None):
     """The batch's host upstream on the pool. Without waiting when the template supports it
     (PREFETCH_ASYNC): each walker's template then waits for its own upstream only, so the first
-    groups' device work runs while the pool computes the later walkers'."""
+    groups' device work runs while the pool computes the later walkers' (concurrency: at most
+    that many walkers' upstream at once, in order)."""
     if not hasattr(tm, "prefetch"):
         return
     if getattr(tm, "PREFETCH_ASYNC", False) and os.environ.get("EFD_PREFETCH_ASYNC", "1") != "0":
-        tm.prefetch(params, *args, wait=False, **kwargs)
+        if concurrency:
+            tm.prefetch(params, *args, wait=False, concurrency=concurrency, **kwargs)
+        else:
+            tm.prefetch(params, *args, wait=False, **kwargs)
     else:
         tm.prefetch(params, *args, **kwargs)
 

@@ -183,7 +183,7 @@ class FastSchwarzschildEccentricFlux:
                     f_phi=om_phi / (2.0 * np.pi * M * MTSUN_SI),
                     f_r=om_r / (2.0 * np.pi * M * MTSUN_SI))
 
-    def prefetch(self, calls, wait=True):
+    def prefetch(self, calls, wait=True, concurrency=None):
         """Run the host upstream of several sources at once: `calls` are prepare() argument
         tuples (M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps). The native parts
         release the GIL, so a thread pool works a walker batch in parallel; the results are held
@@ -193,7 +193,10 @@ class FastSchwarzschildEccentricFlux:
         the prepare() call with its parameters waits for that one result only, so a caller
         working through the batch in groups starts a group's device work as soon as the
         group's own walkers are done, while the pool works on the next groups (the fused
-        likelihood's half-step)."""
+        likelihood's half-step). concurrency (wait=False): at most that many calls run at once,
+        started in `calls` order, each with the pool's threads / concurrency OpenMP threads, so
+        a caller taking the batch in groups of that size gets its first group early (the
+        windowed likelihood's groups then overlap the later walkers' upstream)."""
         calls = [tuple(c) for c in calls]
         # calls whose upstream is already in flight or held (an earlier prefetch of the same
         # batch, e.g. the likelihood's asynchronous one before spectrum_batch's) are not run
@@ -209,7 +212,9 @@ class FastSchwarzschildEccentricFlux:
         pool = _pool()
         # a batch smaller than the pool gives each walker's mode selection several OpenMP
         # threads (efd_host_set_threads is per calling thread; bitwise the same result)
-        per = max(1, pool._max_workers // max(1, len(calls)))
+        limit = len(calls) if (wait or not concurrency) else max(1, min(int(concurrency),
+                                                                        len(calls)))
+        per = max(1, pool._max_workers // max(1, limit))
         if os.environ.get("EFD_PREFETCH_SPLIT", "1") == "0":
             per = 1
         lib = _lib.load()
@@ -217,6 +222,33 @@ class FastSchwarzschildEccentricFlux:
         def run(c):
             lib.efd_host_set_threads(per)
             return self._upstream(*c, None, True)
+
+        if limit < len(calls):
+            # start the calls in order, `limit` at a time (a task waits for its turn and a
+            # free slot; every task releases its slot however it ends)
+            cond = threading.Condition()
+            state = {"next": 0, "running": 0}
+
+            def run_ordered(i, c):
+                with cond:
+                    cond.wait_for(lambda: state["next"] == i and state["running"] < limit)
+                    state["next"] += 1
+                    state["running"] += 1
+                    cond.notify_all()
+                try:
+                    return run(c)
+                finally:
+                    with cond:
+                        state["running"] -= 1
+                        cond.notify_all()
+
+            with self._lock:
+                if len(self._inflight) > self.INFLIGHT_MAX:
+                    self._inflight.clear()
+                for i, c in enumerate(calls):
+                    self._inflight[tuple(float(v) for v in c[:11]) + (True,)] = \
+                        pool.submit(run_ordered, i, c)
+            return len(calls)
 
         if not wait:
             with self._lock:
@@ -598,7 +630,7 @@ class GenerateEMRIWaveform:
     PREFETCH_ASYNC = True
 
     def prefetch(self, params, T=1.0, dt=10.0, eps=1e-5, mode_selection=None,
-                 include_minus_m=True, wait=True, **kwargs):
+                 include_minus_m=True, wait=True, concurrency=None, **kwargs):
         """The host upstream of a batch of 14-parameter sets at once (thread pool; see
         FastSchwarzschildEccentricFlux.prefetch); later calls with the same parameters and
         kwargs take the results. Only for the FD generator without an explicit mode list."""
@@ -610,7 +642,8 @@ class GenerateEMRIWaveform:
             M, mu, a, p0, e0, x0, dist, qS, phiS, qK, phiK, Phi_phi0, Phi_theta0, Phi_r0 = prm
             theta, phi, _ = self._angles(qS, phiS, qK, phiK)
             calls.append((M, mu, p0, e0, theta, phi, dist, Phi_phi0, Phi_r0, T, eps))
-        return gen.prefetch(calls) if wait else gen.prefetch(calls, wait=False)
+        return (gen.prefetch(calls) if wait
+                else gen.prefetch(calls, wait=False, concurrency=concurrency))
 
     def fill_channels(self, out, *params, k0=None, **kwargs):
         """Write [h+, hx] over f >= 0 into the rows of out (complex128 [2][N_pos], device).

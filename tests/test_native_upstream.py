@@ -135,11 +135,24 @@ def test_prepare_native_vs_numpy_and_prefetch():
         for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
             np.testing.assert_array_equal(got[k], ref[k])
     assert not wn._inflight and not wn._prefetched
+    # concurrency: two at a time, in order; the same arrays
+    assert wn.prefetch(calls, wait=False, concurrency=2) == len(calls)
+    for c, ref in zip(calls, serial):
+        got = wn.prepare(*c)
+        for k in ("t", "teuk", "ylms", "m", "f_phi", "Phi_r"):
+            np.testing.assert_array_equal(got[k], ref[k])
+    assert not wn._inflight
     bad = calls[0][:2] + (3.0,) + calls[0][3:]     # p0 inside the separatrix buffer
     wn.prefetch([bad], wait=False)
     with pytest.raises(ValueError):
         wn.prepare(*bad)
     assert not wn._inflight
+    # a failing call releases its slot: the calls after it still run
+    wn.prefetch([bad] + calls[:2], wait=False, concurrency=1)
+    with pytest.raises(ValueError):
+        wn.prepare(*bad)
+    for c, ref in zip(calls[:2], serial[:2]):
+        np.testing.assert_array_equal(wn.prepare(*c)["teuk"], ref["teuk"])
 
 
 def test_host_modes_threads_bitwise():
