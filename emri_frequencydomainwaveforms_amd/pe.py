@@ -130,7 +130,7 @@ class MemoizedUpstream:
         self.host_s = 0.0
         wg.prepare = self
         if hasattr(wg, "prefetch"):
-            wg.prefetch = lambda calls, wait=True: 0   # the memo holds the upstream: nothing to prefetch
+            wg.prefetch = lambda calls, wait=True, concurrency=None: 0   # the memo holds it
 
     def __call__(self, *args, **kwargs):
         # submit_batch calls positionally with plain floats (and None / bool flags): the args
