@@ -4620,6 +4620,26 @@ __device__ __forceinline__ void fc_twiddle_pow(fcv* v, float theta) {
         b = a == 0 ? w8 : cmulf(b, w8);
     }
 }
+// v[j] *= w0 w^j, j = 0 .. N-1, w = exp(i theta): fc_twiddle_pow with the constant factor w0
+// folded into the powers (8 products instead of N)
+template <int N>
+__device__ __forceinline__ void fc_twiddle_pow_from(fcv* v, fcv w0, float theta) {
+    float s1, c1, s8, c8;
+    __sincosf(theta, &s1, &c1);
+    __sincosf(8.0f * theta, &s8, &c8);
+    const fcv w1 = {c1, s1}, w8 = {c8, s8};
+    fcv p[8];
+    p[0] = w0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) p[j] = cmulf(p[j - 1], w1);
+    fcv b = (fcv){1.0f, 0.0f};
+#pragma unroll
+    for (int a = 0; a < N / 8; ++a) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[8 * a + j] = cmulf(v[8 * a + j], a == 0 ? p[j] : cmulf(b, p[j]));
+        b = a == 0 ? w8 : cmulf(b, w8);
+    }
+}
 __global__ __launch_bounds__(FR_NT)
 void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
     static_assert(FC_C == 32 * 16 * 16 && FR_NT == 256, "row transform: 8192 = 32 x 16 x 16");
@@ -4893,11 +4913,8 @@ void k_fc_rows16k_h(const float2* __restrict__ kfpv, int64_t m, int rows, float2
     {
         float s0, c0;
         __sincosf(W16K * (float)(nb * kb), &s0, &c0);
-        const fcv w0 = {c0, s0};
-#pragma unroll
-        for (int n2b = 0; n2b < 32; ++n2b) u[n2b] = cmulf(u[n2b], w0);
+        fc_twiddle_pow_from<32>(u, (fcv){c0, s0}, W16K * 16.0f * (float)kb);
     }
-    fc_twiddle_pow<32>(u, W16K * 16.0f * (float)kb);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {   // exchange 1 back -> inverse (A): n2 = t
 #pragma unroll
