@@ -308,3 +308,23 @@ def test_generate_batch_matches_calls(setup):
         assert torch.equal(S[b], refS[b]), b
     with pytest.raises(ValueError):
         gen_list.spectrum_batch(rows, S[:4], **kw)
+    # lane ranges over several groups, gathered beside the sums and copied to the host early
+    # (lanes_host, lanes_ready), with the status read afterwards (check=False, check_batch)
+    lanes = torch.empty((5, 2), dtype=torch.int32, device="cuda")
+    lh = torch.full((5, 2), -7, dtype=torch.int32, pin_memory=True)
+    S.fill_(complex(np.nan, np.nan))
+    gen_list.BATCH_GROUP = 2
+    try:
+        gen_list.spectrum_batch(rows, S, lanes=lanes, lanes_host=lh, check=False, **kw)
+        gen_list.lanes_ready()
+        got = lh.numpy().copy()
+        gen_list.check_batch()
+    finally:
+        del gen_list.BATCH_GROUP
+    torch.cuda.synchronize()
+    assert np.array_equal(got, lanes.cpu().numpy()) and (got[:, 1] > got[:, 0]).all()
+    for b in range(5):
+        assert torch.equal(S[b], refS[b]), b
+    with pytest.raises(ValueError):   # lanes_host must be pinned
+        gen_list.spectrum_batch(rows, S, lanes=lanes, lanes_host=torch.empty((5, 2),
+                                dtype=torch.int32), **kw)
