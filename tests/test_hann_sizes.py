@@ -35,3 +35,29 @@ def test_size_for(n, support, m):
     # without the four-step pipeline: the smallest of either family
     alt = HannConvolution.size_for(n, support, four_step=False)
     assert alt >= need and alt <= got
+
+
+def test_lane_support_bounds_the_support():
+    """HannConvolution.lane_support (the host's transform-length input from the rows' lane
+    ranges, no synchronisation): for random paired-grid rows whose nonzero bins lie in
+    {l, n-1-l : lo <= l < hi}, the bound is at least every row's support (last + 1 - first) and
+    the span the extent scan covers; empty rows count as support 1; one all-empty batch gives 1."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    n = 100001
+    lanes = []
+    worst = 0
+    for _ in range(64):
+        lo = int(rng.integers(0, n // 2))
+        hi = int(rng.integers(lo, n // 2 + 1))
+        lanes.append((lo, hi))
+        if hi > lo:
+            # nonzero bins: a random subset of the lanes and their mirrors
+            ls = rng.integers(lo, hi, size=5)
+            bins = np.concatenate([ls, n - 1 - ls])
+            worst = max(worst, int(bins.max()) + 1 - int(bins.min()))
+            span = min(n, max(hi, n - lo)) - max(0, min(lo, n - hi))
+            assert HannConvolution.lane_support(np.array([(lo, hi)], dtype=np.int32), n) == span
+    bound = HannConvolution.lane_support(np.array(lanes, dtype=np.int32), n)
+    assert bound >= worst
+    assert HannConvolution.lane_support(np.array([(5, 5), (9, 3)], dtype=np.int32), n) == 1
