@@ -253,9 +253,6 @@ class Likelihood:
     # 43-tile grids) ran 54-60 k logL/s in 4 groups against 40-51 k in 8 (5 interleaved rounds);
     # config 4's 8 walkers are one group either way (groups of 4 or 3: -5 to -10%)
     FUSED_GROUP = min(max(1, int(os.environ.get("EFD_FUSED_GROUP", "16"))), 64)
-    # the batch's last group split in two when there are several (EFD_FUSED_SPLIT_LAST=1; an
-    # experiment switch for paired A/B runs)
-    FUSED_SPLIT_LAST = os.environ.get("EFD_FUSED_SPLIT_LAST", "0") == "1"
     FUSED_DEPTH = 2
     # each group's sum on the group's own stream, right behind its preparation: no
     # cross-stream wait between the two (~12 us of idle device per group on config 4's chain,
@@ -285,13 +282,6 @@ class Likelihood:
             return np.empty(0, dtype=np.float64)
         ngroups = -(-n // self.FUSED_GROUP)
         G = -(-n // ngroups)                       # balanced groups of at most FUSED_GROUP
-        bounds = [(g0, min(n, g0 + G)) for g0 in range(0, n, G)]
-        if self.FUSED_SPLIT_LAST and len(bounds) > 1 and bounds[-1][1] - bounds[-1][0] >= 8:
-            # the last group in two halves: the half-step ends on that group's device chain,
-            # which a smaller group shortens
-            a, b = bounds[-1]
-            bounds[-1:] = [(a, a + (b - a) // 2), (a + (b - a) // 2, b)]
-        ngroups = len(bounds)
         caustic = getattr(getattr(getattr(tm.waveform_generator, "waveform_generator", None),
                                   "create_waveform", None), "caustic", "uniform")
         F = self._fused
@@ -332,11 +322,11 @@ class Likelihood:
         used = []
         try:
             batch = getattr(tm, "submit_batch", None)
-            for g0, g1 in bounds:
+            for g0 in range(0, n, G):
                 if batch is not None:
-                    batch(B, params[g0:g1], *args, **kwargs)
+                    batch(B, params[g0:g0 + G], *args, **kwargs)
                 else:
-                    for i in range(g0, g1):
+                    for i in range(g0, min(n, g0 + G)):
                         tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
                                   **kwargs)
                 gi, jobs = B.flush()
