@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_status",
     "efd_modesum_contributions",
     "efd_modesum_stats",
+    "efd_modesum_env_evaluations",
     "efd_td_workspace_bytes",
     "efd_td_modesum",
     "efd_upload",
@@ -210,6 +211,9 @@ def load(path=None):
         lib.efd_modesum_stats.restype = ctypes.c_int
         lib.efd_modesum_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
                                           ctypes.POINTER(i32), vp]
+    if hasattr(lib, "efd_modesum_env_evaluations"):
+        lib.efd_modesum_env_evaluations.restype = ctypes.c_int
+        lib.efd_modesum_env_evaluations.argtypes = [vp, ctypes.POINTER(i64), vp]
     if hasattr(lib, "efd_td_modesum"):   # absent only in older experiment builds
         lib.efd_td_workspace_bytes.restype = sz
         lib.efd_td_workspace_bytes.argtypes = [i32, i32]

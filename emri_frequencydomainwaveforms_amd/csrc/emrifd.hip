@@ -117,6 +117,12 @@ constexpr double FAST_Y = 153.0;
 // smallest J whose bound holds on the whole interval (a lower bound of |y| there).
 #define EFD_TABLE __constant__
 #include "spa_tables.inc"
+// the K_{1/3} factor's polar phase, leading coefficient TH_0 (see KTHN at its use in spa_fast_m)
+constexpr double KTH0 = -0.069444444444444444444;   // TH_0
+// envelope records (k_items: A(w) polynomial, theta folded into the phase cubic)
+#define EFD_HD __device__
+#include "env_fit.inc"
+#undef EFD_HD
 
 thread_local std::string g_err;
 
@@ -163,6 +169,20 @@ struct __attribute__((aligned(16))) Item {
     int32_t klo[2], khi[2];  // lane ranges per sub-branch s (see k_items)
 };
 static_assert(sizeof(Item) == 288, "Item must be 288 B");
+// Envelope records (k_items, env_fit.inc; Item::jser = 0): the fd, dtj, fdd slots hold the
+// ENV_DEG + 1 coefficients of A(w) instead, highest power first, and ph holds Phi - theta. Only
+// certified-safe records become envelope records, so nothing that reads fd / dtj / fdd (the
+// masked body's tests, the general path) ever meets one.
+static_assert(offsetof(Item, dtj) == offsetof(Item, fd) + 24 &&
+              offsetof(Item, fdd) == offsetof(Item, fd) + 32 &&
+              offsetof(Item, jser) == offsetof(Item, fd) + 8 * (ENV_DEG + 1),
+              "envelope coefficients: fd, dtj, fdd contiguous");
+__host__ __device__ __forceinline__ double* env_of(Item* it) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(it) + offsetof(Item, fd));
+}
+__host__ __device__ __forceinline__ const double* env_of(const Item* it) {
+    return reinterpret_cast<const double*>(reinterpret_cast<const char*>(it) + offsetof(Item, fd));
+}
 static_assert(offsetof(Item, ph) % 16 == 0 && offsetof(Item, fd) % 16 == 0 &&
               offsetof(Item, fdd) % 16 == 0, "the fast path's coefficient pairs are 16-B aligned");
 constexpr int PIECES = (int)sizeof(Item) / 16;  // 16-B pieces per record
@@ -188,7 +208,7 @@ struct Header {
     int32_t lane_lo, lane_hi;   // union [lo, hi) of the segments' lane ranges (k_segment_compact)
     int32_t nitems;             // sparse sum's work items (k_segments_one's split plan), -1: none
     int32_t nsplit;             // split tiles of the plan
-    int64_t pad;                // 64 B
+    int64_t env_evaluations;    // evaluations on envelope records (k_items; 64 B)
 };
 static_assert(sizeof(Header) == 64, "Header must be 64 B");
 
@@ -273,6 +293,7 @@ struct PrepDesc {
     int32_t pcr;     // bit 0: k_prep_pcr_b builds the trajectory and inverse splines, bit 1:
                      // and the amplitude splines (else k_prep_b's roles); set per waveform from
                      // its own (N_t, K), so a workspace never depends on its batch
+    int32_t env;     // k_items makes envelope records (uniform caustic mode; EFD_ENV=0: none)
 };
 struct PrepBatch {
     PrepDesc d[EFD_BATCH_MAX];
@@ -560,6 +581,7 @@ __device__ __forceinline__ void header_init(Header* hdr) {
     const bool init = hdr->magic == HDR_MAGIC;
     hdr->contributions = 0;
     hdr->evaluations = 0;
+    hdr->env_evaluations = 0;
     hdr->groups = 0;
     hdr->lane_lo = INT32_MAX;   // empty until k_segment_compact's blocks widen it
     hdr->lane_hi = INT32_MIN;
@@ -569,7 +591,6 @@ __device__ __forceinline__ void header_init(Header* hdr) {
         hdr->runs_overflow = 0;
         hdr->bad_mn = 0;
         hdr->bad_tile = 0;
-        hdr->pad = 0;
         hdr->magic = HDR_MAGIC;
     }
 }
@@ -1459,13 +1480,13 @@ __device__ int64_t grid_bound(const double* __restrict__ f, int64_t nf, double v
     return lo;
 }
 
-__device__ void build_item(
+__device__ bool build_item(
     const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
     const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int ni, int K,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
     int64_t nl, int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges, int h, int j,
-    unsigned long long& evals);
+    unsigned long long& evals, bool env);
 
 // K4: one thread per (group g, knot interval j). Counts both the SPA evaluations the kernel
 // makes (per group) and the reference formulation's contributions C (per (l, m, n) harmonic:
@@ -1477,37 +1498,42 @@ __device__ __forceinline__ void items_body(const double* __restrict__ t, const d
                         const double* __restrict__ coefT, const int32_t* __restrict__ runs,
                         const double* __restrict__ freq, int64_t nf, int paired, int64_t nl,
                         int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges,
-                        Header* __restrict__ hdr, bool runs_mark) {
+                        Header* __restrict__ hdr, bool runs_mark, bool env) {
     const int ni = nt - 1;
     const int G = hdr->groups;
     // the grid is sized for K >= G groups: whole blocks past the records leave at once
     if ((int64_t)blockIdx.x * blockDim.x >= (int64_t)ni * G) return;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    __shared__ unsigned long long red[2][4];
-    unsigned long long ev = 0, contrib = 0;
+    __shared__ unsigned long long red[3][4];
+    unsigned long long ev = 0, contrib = 0, eev = 0;
     if (gid < (int64_t)ni * G) {
         const int g = (int)(gid % G), j = (int)(gid / G);
         // the PCR inverse splines' run-overflow marker (rr[3]) into the header's sticky flag
         if (runs_mark && j == 0 && runs[(size_t)g * 4 * MAXRUNS + 3] != 0)
             atomicOr(&hdr->runs_overflow, 1);
-        build_item(t, f_phi, f_r, gm, gn, ni, K, coefA, coefT, runs, freq, nf, paired, nl, nl1,
-                   items, ranges, g, j, ev);
+        const bool envr = build_item(t, f_phi, f_r, gm, gn, ni, K, coefA, coefT, runs, freq, nf,
+                                     paired, nl, nl1, items, ranges, g, j, ev, env);
         contrib = ev * (unsigned long long)(gstart[g + 1] - gstart[g]);
+        eev = envr ? ev : 0;
     }
     for (int o = 32; o > 0; o >>= 1) {
         ev += __shfl_xor(ev, o);
         contrib += __shfl_xor(contrib, o);
+        eev += __shfl_xor(eev, o);
     }
     if ((threadIdx.x & 63) == 0) {
         red[0][threadIdx.x >> 6] = contrib;
         red[1][threadIdx.x >> 6] = ev;
+        red[2][threadIdx.x >> 6] = eev;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long c = red[0][0] + red[0][1] + red[0][2] + red[0][3];
         const unsigned long long e = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        const unsigned long long x = red[2][0] + red[2][1] + red[2][2] + red[2][3];
         if (c) atomicAdd((unsigned long long*)&hdr->contributions, c);
         if (e) atomicAdd((unsigned long long*)&hdr->evaluations, e);
+        if (x) atomicAdd((unsigned long long*)&hdr->env_evaluations, x);
     }
 }
 __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
@@ -1516,7 +1542,7 @@ __global__ __launch_bounds__(256) void k_items(const PrepBatch B) {
                ws_at<int32_t>(W, L.gstart), D.nt, D.K, ws_at<double>(W, L.coefA),
                ws_at<double>(W, L.coefT), ws_at<int32_t>(W, L.runs), D.freq, B.nf, B.paired, B.nl,
                B.nl1, ws_at<Item>(W, L.items), ws_at<int4>(W, L.ranges),
-               ws_at<Header>(W, L.header), (D.pcr & 1) != 0);
+               ws_at<Header>(W, L.header), (D.pcr & 1) != 0, D.env != 0);
 }
 
 // One interval record of group h; `evals` = its (branch x bin) evaluation count.
@@ -1581,13 +1607,13 @@ __device__ bool record_safe(const Item& it, FAT fat, int64_t lo0, int64_t hi0, i
     return fmn > 1e-12 * scale && isfinite(scale);
 }
 
-__device__ void build_item(
+__device__ bool build_item(
     const double* __restrict__ t, const double* __restrict__ f_phi, const double* __restrict__ f_r,
     const int32_t* __restrict__ gm, const int32_t* __restrict__ gn, int ni, int K,
     const double* __restrict__ coefA, const double* __restrict__ coefT,
     const int32_t* __restrict__ runs, const double* __restrict__ freq, int64_t nf, int paired,
     int64_t nl, int64_t nl1, Item* __restrict__ items, int4* __restrict__ ranges, int h, int j,
-    unsigned long long& evals) {
+    unsigned long long& evals, bool env) {
     Item& it = items[(size_t)h * ni + j];
     const int m = gm[h], n = gn[h];
     const int32_t* rr = runs + (size_t)h * 4 * MAXRUNS;
@@ -1601,7 +1627,7 @@ __device__ void build_item(
     if (run < 0) {  // flat interval (F_{j+1} == F_j): no support; place empty ranges at 0
         it.klo[0] = it.khi[0] = it.klo[1] = it.khi[1] = 0;
         ranges[(size_t)h * ni + j] = make_int4(0, 0, 0, 0);
-        return;
+        return false;
     }
     const int a = rr[4 * run], sg = rr[4 * run + 2];
     it.tj = t[j];
@@ -1617,6 +1643,7 @@ __device__ void build_item(
         it.ph[c] = dm * ct[0] + dn * ct[1];
     }
     // F' = derivative of (m f_phi + n f_r) piece; F'' = derivative of (m f_phi' + n f_r') piece
+    double gq[3], ymin_rec;   // F'' quadratic (unscaled) and the |y| bound, for the envelope
     {
         const double* ct = coefT + (size_t)j * 32;
         const double F0 = dm * ct[0 * 8 + 2] + dn * ct[0 * 8 + 3];
@@ -1658,6 +1685,8 @@ __device__ void build_item(
         for (int jj = 1; jj < FAST_J; ++jj)
             if (ymin >= JSER_Y[jj]) { J = jj; break; }
         it.jser = J;
+        gq[0] = 3.0 * G0; gq[1] = 2.0 * G1; gq[2] = G2;
+        ymin_rec = ymin;
     }
     // g-interval of this record: [x_lo, x_hi), lower end open at the run's first knot
     const double Fj = knotF(f_phi, f_r, m, n, j), Fj1 = knotF(f_phi, f_r, m, n, j + 1);
@@ -1732,6 +1761,20 @@ __device__ void build_item(
     // branch x bin evaluations (on a paired grid one lane serves both the branch and its partner)
     const int mult = paired ? 1 + partner : 1;
     evals = (unsigned long long)((hi0 - lo0) + (hi1 - lo1)) * mult;
+    // envelope record (env_fit.inc): a certified-safe record with |y| >= ENV_MIN_Y everywhere
+    // whose A(w) and theta(w) polynomials pass the check; its F' / F'' / dtj slots then hold
+    // A's coefficients, its phase cubic Phi - theta, and jser = 0 marks it for the sum
+    if (env && (it.fdneg & 2) && ymin_rec >= ENV_MIN_Y && evals > 0) {
+        EnvFit E;
+        if (env_fit(it.fd, gq, it.dtj, (it.fdneg & 1) != 0, E)) {
+            double* e = env_of(&it);
+            for (int c = 0; c <= ENV_DEG; ++c) e[c] = E.a[c];
+            for (int c = 0; c < 4; ++c) it.ph[c] -= E.th[c];
+            it.jser = 0;
+            return true;
+        }
+    }
+    return false;
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2444,8 +2487,6 @@ __device__ __forceinline__ double cubic(const double* __restrict__ c, double w) 
 //     rho, an amplitude factor: for J <= 2 records (|y| >= 8.7e3, 82% of records) the KTHN1 term
 //     is at most 0.0694 * 0.512 |w|^3 = 5.4e-14 rad and theta = TH_0 w; for J >= 3 the KTHN3
 //     term is at most 4.2e-16 rad (|y| >= 153).
-constexpr double KTH0 = -0.069444444444444444444;   // TH_0
-
 // Lane predicates as wave masks in scalar registers: every VALU instruction issues in 4 cycles
 // per wave64, an FP64 FMA's cost, so the fast path's per-lane booleans (lane range: 2 integer
 // compares per bin; the |y| test of a series-length-4 record; the any-lane test of the general
@@ -2562,6 +2603,30 @@ __device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double 
     sincos_tab(psi0, rs.shift, sct, sn, cs, thn, true, rs.kth, COS_A);
     wr = am * cs;
     wi = am * sn;
+}
+// Envelope records (k_items, env_fit.inc; Item::jser = 0, always certified safe): the phase with
+// theta already in the record's phase cubic and the amplitude A(w) = rho / sqrt|F'| from its
+// degree-ENV_DEG polynomial. 28 FP64 operations per bin instead of spa_simple's 36: no F', F''
+// quadratics, no 1/sqrt|F'| Newton step, no 1/|y| and no angle or rho fold in the sin/cos.
+// MASK: the record covers the wave's chunk only partly; lanes outside actm get A = +0 (flushed).
+template <bool MASK>
+__device__ __forceinline__ void spa_env(const Item* __restrict__ it, double sfk, double stfk,
+                                        const double2* __restrict__ sct, const RecSign& rs,
+                                        uint64_t actm, double& wr, double& wi, double& w) {
+    const double u = sfk - it->gx;
+    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+    w = tt - it->tj;
+    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
+    const double psi0 = fma(stfk, tt, -ph);
+    const double* e = env_of(it);
+    double amp = e[0];
+#pragma unroll
+    for (int c = 1; c <= ENV_DEG; ++c) amp = fma(amp, w, e[c]);
+    if (MASK) amp = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm), amp);
+    double sn, cs;
+    sincos_tab(psi0, rs.shift, sct, sn, cs);
+    wr = amp * cs;
+    wi = amp * sn;
 }
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
@@ -3227,6 +3292,25 @@ __device__ __forceinline__ void modesum_tile(
                         if (!((ha >> (HDR_FD + 1)) & 1u)) atomicAdd(&g_exp_count[39], 1ull);
                     }
 #endif
+                    // envelope records (series length field 0): the straight envelope body when
+                    // the record covers the wave's whole chunk, else the same with a lane mask
+                    if (CAUSTIC == EFD_CAUSTIC_UNIFORM && !hdr_test(ha, 7u << HDR_J)) {
+                        if (!hdr_test((uint32_t)((e_lo - klo) | (khi - e_hi)) >> 31, 1u)) {
+#pragma unroll
+                            for (int i = 0; i < NB; ++i) {
+                                spa_env<false>(it, fk[i], tfk[i], sctab, rs, 0ull, wr[i], wi[i], w[i]);
+                                need[i] = false;
+                            }
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < NB; ++i) {
+                                const int32_t base = e_lo + 64 * i;
+                                const uint64_t am = lane_range_mask(klo - base, khi - base);
+                                spa_env<true>(it, fk[i], tfk[i], sctab, rs, am, wr[i], wi[i], w[i]);
+                                need[i] = false;
+                            }
+                        }
+                    } else
                     // certified safe, J <= 2 and covering the whole chunk: the straight-line
                     // evaluation (no lane masks, amplitude selects or series branch); the
                     // amplitude cubics and accumulation below are shared
@@ -5539,6 +5623,16 @@ static int32_t lists_min_k() {
     return v;
 }
 static bool use_prebuilt(int32_t K) { return K >= lists_min_k(); }
+// Envelope records (k_items, env_fit.inc) in the uniform caustic mode; EFD_ENV=0 (read once per
+// process) builds none: the A/B and parity switch of DESIGN.md's round-6 study. prepare decides
+// per waveform and the sum follows the records (Item::jser = 0), so they always agree.
+static bool env_records() {
+    static const bool v = [] {
+        const char* e = std::getenv("EFD_ENV");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 static bool use_cost_order(const Layout& L, int32_t K) {
     return use_prebuilt(K) && K >= ORDER_MIN_K &&
            L.ntiles > resident_tile_slots();
@@ -5602,6 +5696,7 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         d.sc_re = ai->scale_re; d.sc_im = ai->scale_im;
         d.nt = ai->nt; d.K = ai->K;
         d.lists = use_prebuilt(ai->K) ? (use_cost_order(L, ai->K) ? 3 : 1) : 0;
+        d.env = (ai->caustic == EFD_CAUSTIC_UNIFORM && env_records()) ? 1 : 0;
         any_lists |= d.lists != 0;
         any_order |= d.lists == 3;
 #ifdef EFD_EXP_NO_PCR   // experiment: every waveform on the Thomas kernels (the twin's solve order)
@@ -6061,6 +6156,15 @@ int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* ev
     if (contributions) *contributions = h.contributions;
     if (evaluations) *evaluations = h.evaluations;
     if (groups) *groups = h.groups;
+    return EFD_OK;
+}
+
+int efd_modesum_env_evaluations(const void* workspace, int64_t* env_evaluations, void* stream) {
+    if (!workspace || !env_evaluations) return fail(EFD_ERR_ARG, "NULL argument");
+    Header h{};
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(&h, workspace, sizeof(Header), hipMemcpyDeviceToHost));
+    *env_evaluations = h.env_evaluations;
     return EFD_OK;
 }
 

@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -59,10 +60,25 @@ constexpr double KTH0 = -0.069444444444444444444;
 constexpr double COS_A = 1.000000000029531;
 constexpr double COS_B = -0.5;
 constexpr double KTAB_WMIN = 0x1p-8, KTAB_WMAX = 0x1p10;
+using std::fabs;
+using std::fma;
+using std::fmax;
+using std::sqrt;
+#define EFD_HD
+#include "env_fit.inc"
+#undef EFD_HD
 
 thread_local std::string g_err;
 thread_local int64_t g_stats[3];    // contributions, evaluations, groups of the last call
 int g_threads = 0;                  // 0: all of omp_get_max_threads()
+int g_env = -1;                     // envelope records: -1 unset (EFD_ENV, default on), 0 off, 1 on
+bool env_enabled() {
+    if (g_env < 0) {
+        const char* e = std::getenv("EFD_ENV");
+        g_env = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_env != 0;
+}
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -143,6 +159,11 @@ struct Rec {
     int32_t klo[2], khi[2];
     int32_t jser, fdneg;
     int32_t h, j;          // group, interval (general path)
+    // envelope record (env_fit.inc, as k_items): A(w) of degree ENV_DEG and the phase cubic with
+    // theta folded in; the general path keeps ph, fd, fdd
+    int32_t envc;
+    double env[ENV_DEG + 1];
+    double phE[4];
 };
 
 struct Prep {
@@ -249,6 +270,7 @@ int prepare(const efd_modesum_args* a, Prep& P, bool paired, int64_t nl, int64_t
     const double* freq = a->freq;
     const int64_t nf = a->nf;
     const int64_t lim0 = paired ? nl : nf;
+    const bool env_on = a->caustic == EFD_CAUSTIC_UNIFORM && env_enabled();
     int bad = 0;
     int64_t evals_total = 0, contrib_total = 0;
 #pragma omp parallel num_threads(nthreads()) reduction(+ : evals_total, contrib_total) reduction(| : bad)
@@ -349,6 +371,16 @@ int prepare(const efd_modesum_args* a, Prep& P, bool paired, int64_t nl, int64_t
                     for (int jj = 1; jj < FAST_J; ++jj)
                         if (ymin >= JSER_Y[jj]) { J = jj; break; }
                     it.jser = J;
+                    it.envc = 0;
+                    if (env_on && ymin >= ENV_MIN_Y) {
+                        const double gq[3] = {3.0 * G0, 2.0 * G1, G2};
+                        EnvFit E;
+                        if (env_fit(it.fd, gq, it.dtj, (it.fdneg & 1) != 0, E)) {
+                            it.envc = 1;
+                            for (int c = 0; c <= ENV_DEG; ++c) it.env[c] = E.a[c];
+                            for (int c = 0; c < 4; ++c) it.phE[c] = it.ph[c] - E.th[c];
+                        }
+                    }
                     // lane ranges per sub-branch (open at the run's first knot)
                     const double Fj = knotF(a->f_phi, a->f_r, m, n, j);
                     const double Fj1 = knotF(a->f_phi, a->f_r, m, n, j + 1);
@@ -584,6 +616,47 @@ void spa_fast(const Rec& it, int s, const double* fk, int n, double* wr, double*
     }
 }
 
+// An envelope record's evaluations (k_modesum's spa_env): phase with theta folded into the phase
+// cubic, A(w) from its polynomial, no F' / F'' / K_{1/3} arithmetic. Lanes outside the knot
+// interval take the general path (the kernel certifies its envelope records have none).
+void spa_fast_env(const Rec& it, int s, const double* fk, int n, double* wr, double* wi,
+                  double* wv, unsigned char* need) {
+    const SinCosTable& T = sctab();
+    const double sgn = s ? 1.0 : -1.0;
+    const int shift = (it.fdneg & 1) ? -192 : 192;
+    constexpr double INV_STEP = 81.48733086305042;
+    constexpr double STEP_1 = 0.01227184630308513;
+    constexpr double SHIFTER = 6755399441055744.0;
+#pragma omp simd
+    for (int i = 0; i < n; ++i) {
+        const double g = sgn * fk[i];
+        const double u = g - it.gx;
+        const double tt = std::fma(std::fma(std::fma(it.ic[0], u, it.ic[1]), u, it.ic[2]), u, it.ic[3]);
+        const double w = tt - it.tj;
+        const bool good = (w >= 0.0) & (w < it.dtj);
+        const double ph = std::fma(std::fma(std::fma(it.phE[0], w, it.phE[1]), w, it.phE[2]), w, it.phE[3]);
+        const double psi0 = std::fma(TWO_PI * g, tt, -ph);
+        double A = it.env[0];
+        for (int c = 1; c <= ENV_DEG; ++c) A = std::fma(A, w, it.env[c]);
+        const double am = good ? A : 0.0;
+        const double qs = std::fma(psi0, INV_STEP, SHIFTER);
+        const double q = qs - SHIFTER;
+        const double r = std::fma(-q, STEP_1, psi0);
+        const int64_t qi = (int64_t)q;
+        const int off = (int)((qi + shift) & 511);
+        const double ts = T.s[off], tc = T.c[off];
+        const double z = r * r;
+        const double sr = std::fma(r * z, -1.6666666666666666e-01, r);
+        const double cr = std::fma(z, COS_B, COS_A);
+        const double sn = std::fma(ts, cr, tc * sr);
+        const double cs = std::fma(tc, cr, -ts * sr);
+        wr[i] = am * cs;
+        wi[i] = am * sn;
+        wv[i] = w;
+        need[i] = !good;
+    }
+}
+
 struct TileLists {
     std::vector<int64_t> off;    // [ntiles + 1]
     std::vector<uint32_t> ent;   // (record << 1) | s
@@ -667,7 +740,8 @@ int modesum(const efd_modesum_args* a) {
                 if (hi <= lo) continue;
                 const int n = hi - lo;
                 if (caustic == EFD_CAUSTIC_UNIFORM) {
-                    if (it.jser >= 3) spa_fast<EFD_CAUSTIC_UNIFORM, true>(it, s, fk + lo, n, wr, wi, wv, need);
+                    if (it.envc) spa_fast_env(it, s, fk + lo, n, wr, wi, wv, need);
+                    else if (it.jser >= 3) spa_fast<EFD_CAUSTIC_UNIFORM, true>(it, s, fk + lo, n, wr, wi, wv, need);
                     else spa_fast<EFD_CAUSTIC_UNIFORM, false>(it, s, fk + lo, n, wr, wi, wv, need);
                 } else {
                     spa_fast<EFD_CAUSTIC_SPA, false>(it, s, fk + lo, n, wr, wi, wv, need);

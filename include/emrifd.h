@@ -232,6 +232,11 @@ int efd_modesum_contributions(const void* workspace, int64_t* contributions, voi
 int efd_modesum_stats(const void* workspace, int64_t* contributions, int64_t* evaluations,
                       int32_t* groups, void* stream);
 
+/* Of those evaluations, the ones made on envelope records (the records whose SPA amplitude and
+ * K_{1/3} phase k_items carries as polynomials in t); synchronises `stream`.
+ * An extension for the roofline accounting, not part of the reference's interface. */
+int efd_modesum_env_evaluations(const void* workspace, int64_t* env_evaluations, void* stream);
+
 /* Input of one time-domain mode sum (one waveform). */
 typedef struct efd_td_args {
     /* sparse trajectory knots, length nt (device); as efd_modesum_args */
