@@ -9,9 +9,12 @@ the launcher's `OMP_NUM_THREADS=1` (torchrun sets it) nor a whole node's cores p
 them:
 
   - the process's affinity set is split into `LOCAL_WORLD_SIZE` contiguous, disjoint shares and
-    rank `LOCAL_RANK` takes its own (a single process keeps the whole set). A set that already
-    looks per-rank (at most the node's cores / LOCAL_WORLD_SIZE: the launcher or scheduler
-    bound each rank) is kept as it is, and `EFD_HOST_SPLIT=0` turns the split off;
+    rank `LOCAL_RANK` takes its own (a single process keeps the whole set). A set the launcher
+    or scheduler already bound per rank -- a strict subset of the cores the process's cgroup
+    allows (cpuset.cpus.effective), which torchrun never narrows -- is kept as it is. The
+    number of cores is no evidence either way: 8 ranks sharing a 16-core allocation of a
+    128-core node hold 16 = 128 / 8 cores each and still have to split them.
+    `EFD_HOST_SPLIT=0` never splits, `EFD_HOST_SPLIT=1` always does;
   - `pin()` restricts every thread of the process to that share (os.sched_setaffinity on each
     task of /proc/self/task: the call is per thread on Linux, so threads torch or HIP started
     earlier would otherwise keep the whole node; threads started later inherit it), so ranks
@@ -30,23 +33,47 @@ def local_rank_world(env=None):
     return int(env.get("LOCAL_RANK", "0")), int(env.get("LOCAL_WORLD_SIZE", "1"))
 
 
-def rank_cores(affinity=None, local_rank=None, local_world=None, node_cores=None):
+def allowed_cores():
+    """The cores this process's cgroup allows (cgroup v2 cpuset.cpus.effective, else v1
+    cpuset.effective_cpus), or None when neither can be read."""
+    for path in ("/sys/fs/cgroup/cpuset.cpus.effective",
+                 "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"):
+        try:
+            text = open(path).read().strip()
+        except OSError:
+            continue
+        out = set()
+        try:
+            for part in text.split(","):
+                if not part:
+                    continue
+                a, _, b = part.partition("-")
+                out.update(range(int(a), int(b or a) + 1))
+        except ValueError:
+            continue
+        return out or None
+    return None
+
+
+def rank_cores(affinity=None, local_rank=None, local_world=None, allowed="auto"):
     """This rank's disjoint share of `affinity` (default: the process's affinity set), split
     into `local_world` contiguous chunks of equal size (the remainder goes to the first ranks).
-    With fewer cores than ranks every rank keeps one core (round-robin). A set of at most
-    node_cores // local_world cores (default node: os.cpu_count()) is already per-rank and is
-    returned whole."""
+    With fewer cores than ranks every rank keeps one core (round-robin). An affinity set that is
+    a strict subset of `allowed` (default: allowed_cores(), the cgroup's cpuset) was bound per
+    rank by the launcher and is returned whole; EFD_HOST_SPLIT=0 / 1 forces no split / a split."""
     cores = sorted(os.sched_getaffinity(0) if affinity is None else affinity)
     lr, lw = local_rank_world()
     lr = lr if local_rank is None else int(local_rank)
     lw = lw if local_world is None else int(local_world)
     if lw > 1 and not 0 <= lr < lw:
         raise ValueError(f"local rank {lr} outside a local world of {lw}")
-    if lw <= 1 or not cores or os.environ.get("EFD_HOST_SPLIT", "1") == "0":
+    mode = os.environ.get("EFD_HOST_SPLIT", "")
+    if lw <= 1 or not cores or mode == "0":
         return cores
-    node = node_cores if node_cores is not None else (os.cpu_count() or len(cores))
-    if len(cores) <= node // lw:
-        return cores   # already a per-rank set (bound by the launcher): not split again
+    if mode != "1":
+        allowed = allowed_cores() if allowed == "auto" else allowed
+        if allowed is not None and set(cores) < set(allowed):
+            return cores   # narrowed below the cgroup's cores: bound per rank, not split again
     if len(cores) < lw:
         return [cores[lr % len(cores)]]
     base, extra = divmod(len(cores), lw)

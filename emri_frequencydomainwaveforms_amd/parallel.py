@@ -229,7 +229,7 @@ class ShardedScan:
         k = torch.tensor([rec.shape[1]], dtype=torch.int64, device=self.comm_device)
         dist.all_reduce(k, op=dist.ReduceOp.MAX, group=self.group)
         k = int(k)
-        width = -(-n // self.world)
+        width = max(1, -(-n // self.world))   # one row even for an empty scan (its time)
         pad = torch.zeros((width, k + 1), dtype=torch.float64, device=self.comm_device)
         if len(mine):
             pad[:len(mine), :k] = torch.as_tensor(rec, dtype=torch.float64)

@@ -200,8 +200,10 @@ class FastSchwarzschildEccentricFlux:
         calls = [tuple(c) for c in calls]
         # calls whose upstream is already in flight or held (an earlier prefetch of the same
         # batch, e.g. the likelihood's asynchronous one before spectrum_batch's) are not run
-        # again: prepare() takes those results
+        # again: prepare() takes those results. Eviction first, and never of this batch's own
+        # entries (which would then be recomputed serially in prepare())
         with self._lock:
+            self._evict_inflight({tuple(float(v) for v in c[:11]) + (True,) for c in calls})
             calls = [c for c in calls
                      if (k := tuple(float(v) for v in c[:11]) + (True,)) not in self._inflight
                      and k not in self._prefetched]
@@ -243,8 +245,6 @@ class FastSchwarzschildEccentricFlux:
                         cond.notify_all()
 
             with self._lock:
-                if len(self._inflight) > self.INFLIGHT_MAX:
-                    self._inflight.clear()
                 for i, c in enumerate(calls):
                     self._inflight[tuple(float(v) for v in c[:11]) + (True,)] = \
                         pool.submit(run_ordered, i, c)
@@ -252,8 +252,6 @@ class FastSchwarzschildEccentricFlux:
 
         if not wait:
             with self._lock:
-                if len(self._inflight) > self.INFLIGHT_MAX:
-                    self._inflight.clear()   # results nobody took: dropped when they finish
                 for c in calls:
                     self._inflight[tuple(float(v) for v in c[:11]) + (True,)] = pool.submit(run, c)
             return len(calls)
@@ -277,6 +275,27 @@ class FastSchwarzschildEccentricFlux:
 
     PREFETCH_MAX_BYTES = 1 << 30
     INFLIGHT_MAX = 4096
+
+    def _evict_inflight(self, keep):
+        """Drop in-flight entries nobody took (the caller holds self._lock), keeping the keys in
+        `keep` (the batch being prefetched): finished ones first once they hold more than
+        PREFETCH_MAX_BYTES of host memory or the table exceeds INFLIGHT_MAX entries, then the
+        oldest unfinished ones past INFLIGHT_MAX (dropped when they finish)."""
+        done = [(k, f) for k, f in self._inflight.items()
+                if k not in keep and f.done() and not f.cancelled()]
+        held = 0
+        for _, f in done:
+            try:
+                held += _nbytes(f.result())
+            except Exception:
+                pass
+        if held > self.PREFETCH_MAX_BYTES or len(self._inflight) > self.INFLIGHT_MAX:
+            for k, _ in done:
+                del self._inflight[k]
+        over = len(self._inflight) - self.INFLIGHT_MAX
+        if over > 0:
+            for k in [k for k in self._inflight if k not in keep][:over]:
+                del self._inflight[k]
 
     def spectrum(self, M, mu, p0, e0, theta, phi, dist, Phi_phi0=0.0, Phi_r0=0.0, dt=10.0,
                  T=1.0, eps=1e-5, mode_selection=None, include_minus_m=True, f_arr=None,
@@ -589,6 +608,10 @@ class GenerateEMRIWaveform:
                 rows = params[g0:g0 + G]
                 self.submit_batch(prep, rows, T=T, dt=dt, eps=eps, f_arr=f_arr, **kwargs)
                 gi, jobs = prep.flush()
+                # joined at the end however the rest of the group's queueing ends (its
+                # preparation is on the stream already)
+                if gi not in used:
+                    used.append(gi)
                 gs = prep.stream(gi)
                 if lanes_host is not None:
                     pev = st["prep_ev"][gi]
@@ -616,12 +639,12 @@ class GenerateEMRIWaveform:
                 ev = st["ev"][gi]
                 ev.record(gs)
                 prep.release(gi, ev)
-                if gi not in used:
-                    used.append(gi)
         finally:
             prep._pending = []
             for gi in used:
                 cur.wait_stream(prep.stream(gi))
+            if lanes_host is not None and used:
+                cur.wait_stream(st["lstream"])
         if check:
             prep.wait()   # device-side errors of the groups' workspaces raise here
         return out

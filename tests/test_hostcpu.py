@@ -110,14 +110,33 @@ def test_two_ranks_pin_disjoint_shares():
 
 
 def test_per_rank_set_not_split_again(monkeypatch):
-    """A launcher that already bound each rank to its own cores (a set of at most node / LW
-    cores) keeps that set whole; EFD_HOST_SPLIT=0 turns the split off."""
-    own = set(range(32, 48))                  # 16 cores of a 128-core node, 8 ranks
-    assert hostcpu.rank_cores(own, 3, 8, node_cores=128) == sorted(own)
-    whole = set(range(128))
-    assert hostcpu.rank_cores(whole, 3, 8, node_cores=128) == list(range(48, 64))
+    """A launcher that already bound each rank to its own cores (a strict subset of the cgroup's
+    cpuset) keeps that set whole; ranks that all report the allocation's whole set split it,
+    whatever its size against the node (advisor r05: 8 ranks sharing a 16-core allocation of a
+    128-core node hold node / LW cores each and must still split); EFD_HOST_SPLIT forces either
+    way."""
+    monkeypatch.delenv("EFD_HOST_SPLIT", raising=False)
+    node = set(range(128))
+    own = set(range(32, 48))                  # 16 cores of a 128-core node, 8 ranks, bound
+    assert hostcpu.rank_cores(own, 3, 8, allowed=node) == sorted(own)
+    assert hostcpu.rank_cores(node, 3, 8, allowed=node) == list(range(48, 64))
+    alloc = set(range(16, 32))                # one 16-core allocation shared by 8 ranks
+    shares = [hostcpu.rank_cores(alloc, r, 8, allowed=alloc) for r in range(8)]
+    assert [len(x) for x in shares] == [2] * 8
+    assert sorted(c for x in shares for c in x) == sorted(alloc)
+    wide = set(range(20, 40))                 # a 20-core per-rank binding is kept, not re-split
+    assert hostcpu.rank_cores(wide, 5, 8, allowed=node) == sorted(wide)
+    assert hostcpu.rank_cores(alloc, 3, 8, allowed=None) == [22, 23]   # cpuset unreadable
     monkeypatch.setenv("EFD_HOST_SPLIT", "0")
-    assert hostcpu.rank_cores(whole, 3, 8, node_cores=128) == sorted(whole)
+    assert hostcpu.rank_cores(node, 3, 8, allowed=node) == sorted(node)
+    monkeypatch.setenv("EFD_HOST_SPLIT", "1")
+    assert hostcpu.rank_cores(own, 3, 8, allowed=node) == [38, 39]
+
+
+def test_allowed_cores_parses_cpuset():
+    a = hostcpu.allowed_cores()
+    if a is not None:
+        assert set(os.sched_getaffinity(0)) <= a
 
 
 _PIN_CHILD = r"""

@@ -148,11 +148,12 @@ def _scan_worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [100, 7, 1])
+@pytest.mark.parametrize("n", [100, 7, 1, 0])
 def test_sharded_scan_gloo(n):
     """Config 3's scan over 2 gloo ranks: the shards are disjoint, round-robin and cover the
     grid; every rank gets every point's record in point order; each rank generated exactly its
-    own points (after its own p0 solves); a rank with no point (n = 1) still joins the gather."""
+    own points (after its own p0 solves); a rank with no point (n = 1) still joins the gather,
+    and an empty scan (n = 0) returns empty records on every rank (advisor r05)."""
     import torch.multiprocessing as mp
     from emri_frequencydomainwaveforms_amd.parallel import scan_points
     ctx = mp.get_context("spawn")
@@ -174,6 +175,12 @@ def test_sharded_scan_gloo(n):
     params = np.array([[M, 1e-5 * M, 0.0, 10.0, e0, 1.0, 1.0, 0.2, 0.2, 0.8, 0.8, 1.0, 0.0, 3.0]
                        for M in Ms for e0 in e0s])[:n]
     params[:, 3] = 10.0 + params[:, 4]
+    if n == 0:
+        for r in range(world):
+            summary, owner, seconds, points, rows, out = res[r]
+            assert summary.shape[0] == 0 and len(owner) == 0 and len(points) == 0
+            assert seconds.shape == (world,) and np.all(seconds >= 0)
+        return
     expect = _scan_expect(params)
     owned = [res[r][3] for r in range(world)]
     allpts = np.concatenate(owned)
