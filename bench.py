@@ -241,6 +241,96 @@ def cpu_baseline(w, seconds=10.0):
                               "on the host, C++17 + OpenMP, -O3 -march=x86-64-v4"}
 
 
+def _host_threads():
+    threads = len(os.sched_getaffinity(0))
+    return min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+
+
+def twin_job_rate(jobs, unit, seconds=10.0, what=""):
+    """The host twin over a list of jobs (BASELINE.md section 2's CPU column for configs 1, 3, 4
+    and 5), each job one waveform or one walker's log-likelihood: job() runs it on the host
+    (efd_modesum_cpu writing h+/hx over f >= 0 as the device path does, + efd_loglike_cpu for a
+    likelihood). All of this rank's cores (the twin's OpenMP over tiles; one warm-up job, then
+    the jobs in order until `seconds` or the list ends) and 1 thread (the jobs in order until
+    seconds / 2, at least one). The reference's CPU path is the same per-walker loop
+    (likelihood.py:246-248), there under mp.Pool(4) (emri_pe.py:545)."""
+    from emri_frequencydomainwaveforms_amd import cputwin
+    threads = _host_threads()
+
+    def timed(budget):
+        n, t0 = 0, time.perf_counter()
+        for job in jobs:
+            job()
+            n += 1
+            if time.perf_counter() - t0 > budget:
+                break
+        return n, time.perf_counter() - t0
+    prev = cputwin.set_threads(threads)
+    try:
+        jobs[0]()
+        n_all, t_all = timed(seconds)
+        cputwin.set_threads(1)
+        n_one, t_one = timed(0.5 * seconds)
+    finally:
+        cputwin.set_threads(prev)
+    return {"value": n_all / t_all, "unit": unit, "cores": threads, "kind": "twin",
+            "sample": f"{n_all} of {len(jobs)} {what} in {t_all:.2f} s on {threads} threads",
+            "single_thread": {"value": n_one / t_one, "unit": unit, "cores": 1,
+                              "sample": f"{n_one} of {len(jobs)} {what} in {t_one:.2f} s on "
+                                        f"1 thread"},
+            "implementation": "efd_modesum_cpu (+ efd_loglike_cpu): the HIP path's algorithm "
+                              "on the host (csrc/emrifd_cpu.cpp, C++17 + OpenMP, -O3 "
+                              "-march=x86-64-v4), host upstream prepared beforehand"}
+
+
+def twin_waveform_job(w):
+    """One waveform of a workload dict (build_workload) on the twin: h+/hx over f >= 0."""
+    from emri_frequencydomainwaveforms_amd import cputwin
+    k0 = int(np.searchsorted(w["freq"], 0.0))
+
+    def job():
+        cputwin.modesum(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"], w["f_r"],
+                        w["m"], w["n"], w["ylm_p"], w["ylm_m"], w["freq"], w["prefactor"],
+                        polarizations=True, k0=k0)
+    return job
+
+
+def twin_likelihood_jobs(s, rows):
+    """One job per walker of `rows` (sampled coordinates) for pe.setup's likelihood `s`: the
+    walker's template on the twin (its host upstream prepared here, untimed, as the device
+    rate's memoised one) and efd_loglike_cpu against the likelihood's own d and w. Returns
+    (jobs, logL list the jobs fill)."""
+    from emri_frequencydomainwaveforms_amd import cputwin
+    from emri_frequencydomainwaveforms_amd.constants import Gpc, MRSUN_SI
+    from emri_frequencydomainwaveforms_amd.summation import fd_grid
+    from emri_frequencydomainwaveforms_amd.waveform import get_viewing_angles, polarization_angle
+    kw = s.kwargs
+    grid = np.asarray(kw["f_arr"]) if kw.get("f_arr") is not None else fd_grid(kw["T"], kw["dt"])
+    k0 = int(np.searchsorted(grid, 0.0))
+    d = s.like._d.cpu().numpy()
+    w = s.like._w_templ.cpu().numpy()
+    few = s.few
+    wg = few.waveform_generator
+    out = [None] * len(rows)
+    jobs = []
+    for i, p14 in enumerate(s.transform.both_transforms(np.asarray(rows))):
+        M, mu, _a, p0, e0, _x0, dist, qS, phiS, qK, phiK, pp0, _pt0, pr0 = (float(v) for v in p14)
+        theta, phi = get_viewing_angles(qS, phiS, qK, phiK)
+        rot = (np.exp(-2j * polarization_angle(qS, phiS, qK, phiK))
+               if getattr(few, "frame", None) == "detector" else 1.0)
+        u = wg.prepare(M, mu, p0, e0, theta, phi, dist, pp0, pr0, kw["T"], kw["eps"])
+        K = len(u["m"])
+        scale = complex(rot) * (mu * MRSUN_SI / (dist * Gpc))
+
+        def job(i=i, u=u, K=K, scale=scale):
+            hp, hc = cputwin.modesum(u["t"], u["teuk"], u["Phi_phi"], u["Phi_r"], u["f_phi"],
+                                     u["f_r"], u["m"], u["n"], u["ylms"][:K], u["ylms"][K:],
+                                     grid, scale, polarizations=True, k0=k0)
+            out[i] = cputwin.loglike(np.stack([hp, hc]), d, w)
+        jobs.append(job)
+    return jobs, out
+
+
 def few_gen_timing(w, reps=10, caustic="uniform"):
     """The drivers' whole call (events around the full few_gen-equivalent
     call; check_mode_by_mode.py:221-229 times `few_gen(*injection_in, **kw)`): the
@@ -498,8 +588,15 @@ def main():
     C = sum(s_[0] for s_ in st_all)
     n_eval = sum(s_[1] for s_ in st_all)
     n_groups = [s_[2] for s_ in st_all]
+    n_env = sum(x["eng"].env_evaluations(s_sum.cuda_stream) for x in slots[0]["wf"])
 
+    rank_elapsed = [elapsed]
     if world > 1:
+        # every rank's own timed region (the line's value takes the slowest: max over ranks)
+        mine = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rank_elapsed = [float(x) for x in allr]
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(tt[0]), float(tt[1])
@@ -539,6 +636,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "rank_ms_per_step": {"min": min(rank_elapsed) / args.steps * 1e3,
+                                 "max": max(rank_elapsed) / args.steps * 1e3,
+                                 "per_rank": [x / args.steps * 1e3 for x in rank_elapsed]},
             "waveforms_per_step": B,
             "higher_is_better": True,
             "scaling": "weak",
@@ -552,6 +652,8 @@ def main():
                                    else "B copies of config 2's source"),
                        "harmonics": Ks, "mn_groups": n_groups, "N_t": nts, "N_f": nf,
                        "contributions_per_launch": C, "spa_evaluations_per_launch": n_eval,
+                       "envelope_evaluations_per_launch": n_env,
+                       "envelope_share": n_env / n_eval if n_eval else 0.0,
                        "p0": w["params"]["p0"], "parallelism": f"walkers x{world} (no exchange)",
                        "pipeline": args.pipeline + (" (diagnostic: sum only)"
                                                     if args.diag_sum_only else ""),
@@ -633,6 +735,23 @@ def bench_scan(args):
         res = scan(params, T=T, dt=dt, eps=eps, p0_solver=p0_of, mapper=pool.map)
         times.append(float(res.seconds.max()))
     sweep = float(np.median(times))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the host twin over the same 100 points (inputs from the same stand-in upstream,
+        # prepared beforehand; the upstream's own cost is reported beside it)
+        try:
+            from emri_frequencydomainwaveforms_amd.waveform import get_viewing_angles
+            th, ph = get_viewing_angles(*params[0][7:11])
+            t0 = time.perf_counter()
+            ws = [build_workload(T=T, dt=dt, eps=eps, M=row[0], mu=row[1], e0=row[4],
+                                 p0=float(p0_of(row)), Phi_phi0=row[11], Phi_r0=row[13],
+                                 theta=th, phi=ph, dist=row[6]) for row in params]
+            up = time.perf_counter() - t0
+            cpu = twin_job_rate([twin_waveform_job(w) for w in ws], "waveforms/s",
+                                seconds=args.cpu_seconds, what="grid points")
+            cpu["host_upstream_s_per_grid_serial"] = up
+        except Exception as exc:
+            cpu = {"value": None, "error": repr(exc)}
     if rank == 0:
         line = {
             "metric": "FD waveforms/sec (config 3: 10x10 (M, e0) scan, Tobs=1yr, dt=10s, "
@@ -652,6 +771,7 @@ def bench_scan(args):
             "rank_seconds_last_sweep": res.seconds.tolist(),
             "sweep_seconds": times,
             "record_checksum": float(np.sum(res.summary[:, :2])),
+            "cpu_baseline": cpu,
             "note": "value: 100 points / the max over ranks of one sweep (p0 solves on the "
                     "rank's upstream pool, generate_batch's host upstream and device groups of "
                     "16, per-point records); median over steps",
@@ -729,6 +849,7 @@ def bench_likelihood(args):
     mine = dict(rank=rank, walkers_per_step=hi - lo, api_s=api,
                 api_loglikes_per_s=args.api_steps * (hi - lo) / api, host_threads=host_threads,
                 host_cores=len(share), host_core_range=[min(share), max(share)] if share else None)
+    mine["ms_per_step"] = elapsed / args.steps * 1e3
     per_rank = [mine]
     rccl_world = 1
     if world > 1:
@@ -738,6 +859,20 @@ def bench_likelihood(args):
         tt = torch.tensor([elapsed, api], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, api = float(tt[0]), float(tt[1])
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the host twin on the same walkers (all of the start's for config 4, the first
+        # half-step's 64 for config 5) against the device logL of the same rows
+        try:
+            rows = np.concatenate(batches)[:max(B, 16)]
+            ll_dev = np.concatenate([np.asarray(sl(rows[i:i + B])) for i in range(0, len(rows), B)])
+            jobs, ll_twin = twin_likelihood_jobs(s, rows)
+            cpu = twin_job_rate(jobs, "logL/s", seconds=args.cpu_seconds, what="walkers")
+            done = [i for i, v in enumerate(ll_twin) if v is not None]
+            cpu["twin_vs_device_max_rel_logL"] = float(max(
+                abs(ll_twin[i] - ll_dev[i]) / max(1.0, abs(ll_dev[i])) for i in done))
+        except Exception as exc:  # the baseline must not kill the GPU measurement
+            cpu = {"value": None, "error": repr(exc)}
     if rank == 0:
         line = {
             "metric": f"FD log-likelihoods/sec (emri_pe {args.likelihood}: "
@@ -756,9 +891,12 @@ def bench_likelihood(args):
                        "tile_constants": bool(s.like.fused_tile_constants)},
             "api_loglikes_per_s": args.api_steps * B / api,
             "api_per_rank": per_rank,
+            "rank_ms_per_step": {"min": min(r["ms_per_step"] for r in per_rank),
+                                 "max": max(r["ms_per_step"] for r in per_rank)},
             "world_size_rccl": rccl_world,
             "host_upstream_ms_per_walker": memo.host_s / max(1, len(memo.memo)) * 1e3,
             "ll_truth_walker_sample": float(np.asarray(ll)[0]),
+            "cpu_baseline": cpu,
             "note": "value: device path with each walker's host upstream memoised after the "
                     "warm-up (inputs resident); api_loglikes_per_s: the same calls with the "
                     "host stand-in upstream (C++ trajectory, amplitudes, selection on a thread "

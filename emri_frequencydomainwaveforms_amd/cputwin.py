@@ -53,12 +53,14 @@ def modesum(t, amp, phi_phi, phi_r, f_phi, f_r, m, n, ylm_p, ylm_m, freq, scale=
     if grid_symmetric is None:
         grid_symmetric = bool(np.array_equal(freq, -freq[::-1]))
     hp = hc = None
+    # (the twin writes every output bin, so a fresh output needs no zeroing unless accumulating)
+    new = np.zeros if accumulate else np.empty
     if polarizations:
-        hp = np.zeros(nf - k0, dtype=np.complex128)
-        hc = np.zeros(nf - k0, dtype=np.complex128)
+        hp = new(nf - k0, dtype=np.complex128)
+        hc = new(nf - k0, dtype=np.complex128)
         S = None
     else:
-        S = out if out is not None else np.zeros(nf, dtype=np.complex128)
+        S = out if out is not None else new(nf, dtype=np.complex128)
     p = lambda x: x.ctypes.data if x is not None else None  # noqa: E731
     sc = complex(scale)
     a = _lib.ModesumArgs(

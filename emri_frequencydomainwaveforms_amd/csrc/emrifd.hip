@@ -1770,7 +1770,7 @@ __device__ bool build_item(
             double* e = env_of(&it);
             for (int c = 0; c <= ENV_DEG; ++c) e[c] = E.a[c];
             for (int c = 0; c < 4; ++c) it.ph[c] -= E.th[c];
-            it.jser = 0;
+            it.jser = 0;   // the sum's envelope class
             return true;
         }
     }
@@ -2606,27 +2606,32 @@ __device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double 
 }
 // Envelope records (k_items, env_fit.inc; Item::jser = 0, always certified safe): the phase with
 // theta already in the record's phase cubic and the amplitude A(w) = rho / sqrt|F'| from its
-// degree-ENV_DEG polynomial. 28 FP64 operations per bin instead of spa_simple's 36: no F', F''
-// quadratics, no 1/sqrt|F'| Newton step, no 1/|y| and no angle or rho fold in the sin/cos.
-// MASK: the record covers the wave's chunk only partly; lanes outside actm get A = +0 (flushed).
-template <bool MASK>
-__device__ __forceinline__ void spa_env(const Item* __restrict__ it, double sfk, double stfk,
-                                        const double2* __restrict__ sct, const RecSign& rs,
-                                        uint64_t actm, double& wr, double& wi, double& w) {
-    const double u = sfk - it->gx;
-    const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
-    w = tt - it->tj;
-    const double ph = fma(fma(fma(it->ph[0], w, it->ph[1]), w, it->ph[2]), w, it->ph[3]);
-    const double psi0 = fma(stfk, tt, -ph);
+// degree-ENV_DEG polynomial, for the NB bins of the lane. 28 FP64 operations per bin instead of
+// spa_simple's 36: no F', F'' quadratics, no 1/sqrt|F'| Newton step, no 1/|y| and no angle or rho
+// fold in the sin/cos.
+// MASK: the record covers the wave's chunk only partly; lanes outside am[i] get A = +0 (flushed).
+template <bool MASK, int NB>
+__device__ __forceinline__ void env_record(const Item* __restrict__ it, const double* fk,
+                                           const double* tfk, const double2* __restrict__ sct,
+                                           const RecSign& rs, const uint64_t* am, double* wr,
+                                           double* wi, double* w) {
     const double* e = env_of(it);
-    double amp = e[0];
 #pragma unroll
-    for (int c = 1; c <= ENV_DEG; ++c) amp = fma(amp, w, e[c]);
-    if (MASK) amp = ftz_select(__builtin_amdgcn_inverse_ballot_w64(actm), amp);
-    double sn, cs;
-    sincos_tab(psi0, rs.shift, sct, sn, cs);
-    wr = amp * cs;
-    wi = amp * sn;
+    for (int i = 0; i < NB; ++i) {
+        const double u = fk[i] - it->gx;
+        const double tt = fma(fma(fma(it->ic[0], u, it->ic[1]), u, it->ic[2]), u, it->ic[3]);
+        w[i] = tt - it->tj;
+        const double ph = fma(fma(fma(it->ph[0], w[i], it->ph[1]), w[i], it->ph[2]), w[i], it->ph[3]);
+        const double psi0 = fma(tfk[i], tt, -ph);
+        double amp = e[0];
+#pragma unroll
+        for (int c = 1; c <= ENV_DEG; ++c) amp = fma(amp, w[i], e[c]);
+        if (MASK) amp = ftz_select(__builtin_amdgcn_inverse_ballot_w64(am[i]), amp);
+        double sn, cs;
+        sincos_tab(psi0, rs.shift, sct, sn, cs);
+        wr[i] = amp * cs;
+        wi[i] = amp * sn;
+    }
 }
 template <int CAUSTIC>
 __device__ __forceinline__ void spa_fast_m(const Item* __restrict__ it, double sfk, double stfk,
@@ -3296,20 +3301,18 @@ __device__ __forceinline__ void modesum_tile(
                     // the record covers the wave's whole chunk, else the same with a lane mask
                     if (CAUSTIC == EFD_CAUSTIC_UNIFORM && !hdr_test(ha, 7u << HDR_J)) {
                         if (!hdr_test((uint32_t)((e_lo - klo) | (khi - e_hi)) >> 31, 1u)) {
-#pragma unroll
-                            for (int i = 0; i < NB; ++i) {
-                                spa_env<false>(it, fk[i], tfk[i], sctab, rs, 0ull, wr[i], wi[i], w[i]);
-                                need[i] = false;
-                            }
+                            env_record<false, NB>(it, fk, tfk, sctab, rs, nullptr, wr, wi, w);
                         } else {
+                            uint64_t am[NB];
 #pragma unroll
                             for (int i = 0; i < NB; ++i) {
                                 const int32_t base = e_lo + 64 * i;
-                                const uint64_t am = lane_range_mask(klo - base, khi - base);
-                                spa_env<true>(it, fk[i], tfk[i], sctab, rs, am, wr[i], wi[i], w[i]);
-                                need[i] = false;
+                                am[i] = lane_range_mask(klo - base, khi - base);
                             }
+                            env_record<true, NB>(it, fk, tfk, sctab, rs, am, wr, wi, w);
                         }
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) need[i] = false;
                     } else
                     // certified safe, J <= 2 and covering the whole chunk: the straight-line
                     // evaluation (no lane masks, amplitude selects or series branch); the
@@ -4819,99 +4822,15 @@ void k_fc_rows(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __r
     }
 }
 
-// (B) for rows of C = 16384 (m = 2^24 as 1024 x 16384, EFD_FC_C16: wider column segments, 128 B
-// of S and 64 B of Y per row of a column block), register-staged as k_fc_rows with 512 threads
-// of 32 elements (16384 = 32 x 32 x 16; n = n2 + 512 n1, n2 = n2a + 16 n2b; k = k1 + 32 k2a +
-// 1024 k2b): forward (A) thread n2: DFT-32 over n1, times w_16384^(n2 k1); (B) task (k1, n2a):
-// DFT-32 over n2b, times w_512^(n2a k2a); (C) task (k1, k2a), two per thread: DFT-16 over n2a;
-// the kernel's spectrum; the transposed steps back. Exchange 1 [k1][n2] (stride 513),
-// exchange 2 [k2a][n2a][k1]: conflict-free as k_fc_rows'. 128.3 KB of LDS, one workgroup per CU.
+// (B) for rows of C = 16384 (m = 2^24 as 1024 x 16384: wider column segments, 128 B of S and 64 B
+// of Y per row of a column block), register-staged as k_fc_rows with 512 threads of 32 elements
+// (16384 = 32 x 32 x 16; n = n2 + 512 n1, n2 = n2a + 16 n2b; k = k1 + 32 k2a + 1024 k2b): forward
+// (A) thread n2: DFT-32 over n1, times w_16384^(n2 k1); (B) task (k1, n2a): DFT-32 over n2b,
+// times w_512^(n2a k2a); (C) task (k1, k2a), two per thread: DFT-16 over n2a; the kernel's
+// spectrum; the transposed steps back. (Round 5 also kept complex exchanges with 128 KB of LDS,
+// one workgroup per CU: 650 against 575-579 us, r05z; deleted in round 6.)
 constexpr int FC_C16 = 16384;
-constexpr int FR16_S1 = 513;
-__global__ __launch_bounds__(FC_NT)
-void k_fc_rows16k(const float2* __restrict__ kfpv, int64_t m, int rows, float2* __restrict__ Yv) {
-    static_assert(FC_NT == 512 && FC_C16 == 32 * 32 * 16, "16384 = 32 x 32 x 16, 512 threads");
-    __shared__ fcv sm[32 * FR16_S1];
-    const fcv* kfp = reinterpret_cast<const fcv*>(kfpv);
-    fcv* Y = reinterpret_cast<fcv*>(Yv);
-    const int64_t npair = (int64_t)gridDim.x;
-    const int64_t p = (int64_t)(blockIdx.x & 7) * (npair >> 3) + (blockIdx.x >> 3);
-    const int fr = (int)(p / rows), wk = (int)(p - (int64_t)fr * rows);
-    fcv* y = Y + (int64_t)wk * m + (int64_t)fr * FC_C16;
-    const fcv* kr = kfp + (int64_t)fr * FC_C16;
-    const int t = threadIdx.x;
-    constexpr float W16K = FC_2PI / 16384.0f, W512 = FC_2PI / 512.0f;
-    {   // forward (A): n2 = t
-        fcv v[32];
-#pragma unroll
-        for (int n1 = 0; n1 < 32; ++n1) v[n1] = y[t + 512 * n1];
-        fc_dft32<-1>(v);
-        fc_twiddle_pow<32>(v, -W16K * (float)t);
-#pragma unroll
-        for (int k1 = 0; k1 < 32; ++k1) sm[k1 * FR16_S1 + t] = v[k1];
-    }
-    __syncthreads();
-    const int kb = t & 31, nb = t >> 5;   // (B) task (k1 = kb, n2a = nb)
-    {
-        fcv u[32];
-#pragma unroll
-        for (int n2b = 0; n2b < 32; ++n2b) u[n2b] = sm[kb * FR16_S1 + nb + 16 * n2b];
-        __syncthreads();
-        fc_dft32<-1>(u);
-        fc_twiddle_pow<32>(u, -W512 * (float)nb);
-#pragma unroll
-        for (int k2a = 0; k2a < 32; ++k2a) sm[(k2a * 16 + nb) * 32 + kb] = u[k2a];
-    }
-    __syncthreads();
-    fcv w[2][16];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // forward (C), the kernel's spectrum, inverse (C): (k1, k2a)
-        const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
-#pragma unroll
-        for (int n2a = 0; n2a < 16; ++n2a) w[h][n2a] = sm[(k2a * 16 + n2a) * 32 + k1];
-        fc_dft16<-1>(w[h]);
-#pragma unroll
-        for (int k2b = 0; k2b < 16; ++k2b)
-            w[h][k2b] = cmulf(w[h][k2b], kr[k1 + 32 * k2a + 1024 * k2b]);
-        fc_dft16<1>(w[h]);
-        fc_twiddle_pow<16>(w[h], W512 * (float)k2a);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int q = t + 512 * h, k1 = q & 31, k2a = q >> 5;
-#pragma unroll
-        for (int n2a = 0; n2a < 16; ++n2a) sm[(k2a * 16 + n2a) * 32 + k1] = w[h][n2a];
-    }
-    __syncthreads();
-    {   // inverse (B): task (k1 = kb, n2a = nb) -> n2b, times w_16384^(-n2 k1)
-        fcv u[32];
-#pragma unroll
-        for (int k2a = 0; k2a < 32; ++k2a) u[k2a] = sm[(k2a * 16 + nb) * 32 + kb];
-        __syncthreads();
-        fc_dft32<1>(u);
-        float s0, c0;
-        __sincosf(W16K * (float)(nb * kb), &s0, &c0);
-        const fcv w0 = {c0, s0};
-#pragma unroll
-        for (int n2b = 0; n2b < 32; ++n2b) u[n2b] = cmulf(u[n2b], w0);
-        fc_twiddle_pow<32>(u, W16K * 16.0f * (float)kb);
-#pragma unroll
-        for (int n2b = 0; n2b < 32; ++n2b) sm[kb * FR16_S1 + nb + 16 * n2b] = u[n2b];
-    }
-    __syncthreads();
-    {   // inverse (A): n2 = t -> x[n2 + 512 n1]
-        fcv v[32];
-#pragma unroll
-        for (int k1 = 0; k1 < 32; ++k1) v[k1] = sm[k1 * FR16_S1 + t];
-        fc_dft32<1>(v);
-#pragma unroll
-        for (int n1 = 0; n1 < 32; ++n1) y[t + 512 * n1] = v[n1];
-    }
-}
-
-// k_fc_rows16k with every exchange in two passes (real parts, then imaginary parts) through a
-// float array: 69.6 KB of LDS and at most 128 VGPRs, so two workgroups share a CU and one's
+// Every exchange in two passes (real parts, then imaginary parts) through a float array: 69.6 KB of LDS and at most 128 VGPRs, so two workgroups share a CU and one's
 // loads and stores overlap the other's transforms (one per CU leaves HBM idle while it
 // computes). Exchange 1 [k1][n2] stride 513, exchange 2 [k2a][n2a][k1] unpadded: every b32
 // access of a 32-lane bank group hits 32 distinct banks (ds_read_b32 / ds_write_b32 bank
@@ -5020,148 +4939,15 @@ void k_fc_rows16k_h(const float2* __restrict__ kfpv, int64_t m, int rows, float2
     for (int n1 = 0; n1 < 32; ++n1) y[to + 512 * n1] = v[n1];
 }
 
-// (A) and (C) for R = 2048 (m = 2^24, test.sh's transform), NCOL = 4 columns per workgroup, as
-// register stages with two LDS exchanges (2048 = 16 x 16 x 8; n = n2 + 128 n1, n2 = n2a + 8 n2b;
-// k = k1 + 16 k2a + 256 k2b): forward (A) task (j, n2): DFT-16 over n1, times w_2048^(n2 k1);
-// (B) task (j, k1, n2a): DFT-16 over n2b, times w_128^(n2a k2a); (C) task (j, k1, k2a): DFT-8
-// over n2a -> f_r = k. The inverse runs the transposed steps in reverse. Exchange 1 is
-// [k1][n2][j], exchange 2 [k1][k2a][n2a (pad to 9)][j]: every LDS access of a half-wave covers
-// 64 distinct banks. Two exchanges per direction instead of the Stockham form's four passes and
-// the staging round trip (the other R keep it).
-constexpr int FCC_R = 2048, FCC_NCOL = 4, FCC_S2 = 9;
-template <bool FWD>
-__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
-void k_fc_cols2048(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
-                   float2* __restrict__ Yv) {
-    static_assert(FC_NT == 512 && FCC_R * FCC_NCOL == 16 * FC_NT, "16 elements per thread");
-    constexpr int64_t M = (int64_t)FCC_R * FC_C;
-    // exchange 1: 16 x 128 x 4 = 8192; exchange 2: 16 x 16 x 9 x 4 = 9216 elements (73.7 KB)
-    __shared__ fcv sm[16 * 16 * FCC_S2 * FCC_NCOL];
-    fcv* Y = reinterpret_cast<fcv*>(Yv);
-    const int row = blockIdx.y;
-    constexpr int G = FC_C / FCC_NCOL;
-    static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
-    const int c0 = ((blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3)) * FCC_NCOL;
-    fcv* y = Y + (int64_t)row * M;
-    const int t = threadIdx.x;
-    const int j = t & 3;
-    constexpr float W2048 = FC_2PI / 2048.0f, W128 = FC_2PI / 128.0f;
-    auto e1 = [](int k1, int n2, int jj) { return (k1 * 128 + n2) * FCC_NCOL + jj; };
-    auto e2 = [](int k1, int k2a, int n2a, int jj) {
-        return ((k1 * 16 + k2a) * FCC_S2 + n2a) * FCC_NCOL + jj;
-    };
-    if (FWD) {
-        const HannRow h = hann_row(info, row);
-        const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;
-        const double2* src = S + (int64_t)row * stride + h.first;
-        const bool bad = h.len > M;
-        {   // (A): task (j, n2)
-            const int n2 = t >> 2;
-            fcv v[16];
-#pragma unroll
-            for (int n1 = 0; n1 < 16; ++n1) {
-                const int64_t s = (int64_t)(n2 + 128 * n1) * FC_C + c0 + j;
-                fcv x = {0.f, 0.f};
-                if (bad) {
-                    x = (fcv){__int_as_float(0x7fc00000), 0.f};
-                } else if (s < h.len) {
-                    const double2 d = src[s];
-                    x = (fcv){(float)(d.x * inv), (float)(d.y * inv)};
-                }
-                v[n1] = x;
-            }
-            fc_dft16<-1>(v);
-            fc_twiddle_pow<16>(v, -W2048 * (float)n2);
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) sm[e1(k1, n2, j)] = v[k1];
-        }
-        __syncthreads();
-        fcv u[16];
-        const int n2a = (t >> 2) & 7, k1b = t >> 5;
-#pragma unroll
-        for (int n2b = 0; n2b < 16; ++n2b) u[n2b] = sm[e1(k1b, n2a + 8 * n2b, j)];
-        __syncthreads();
-        fc_dft16<-1>(u);
-        fc_twiddle_pow<16>(u, -W128 * (float)n2a);
-#pragma unroll
-        for (int k2a = 0; k2a < 16; ++k2a) sm[e2(k1b, k2a, n2a, j)] = u[k2a];
-        __syncthreads();
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {   // (C): tasks (j, k2a, k1), two per thread
-            const int q = t + FC_NT * hh;
-            const int k2a = (q >> 2) & 15, k1 = q >> 6;
-            fcv w[8];
-#pragma unroll
-            for (int a = 0; a < 8; ++a) w[a] = sm[e2(k1, k2a, a, j)];
-            fc_dft8<-1>(w);
-#pragma unroll
-            for (int k2b = 0; k2b < 8; ++k2b) {
-                const int fr = k1 + 16 * k2a + 256 * k2b;
-                const int c = c0 + j;
-                const uint32_t pp = (uint32_t)c * (uint32_t)fr;   // < C R = M: no reduction
-                float sn, cs;
-                __sincosf(-FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
-                y[(int64_t)fr * FC_C + c] = cmulf(w[k2b], (fcv){cs, sn});
-            }
-        }
-    } else {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {   // inverse (C): tasks (j, k2a, k1)
-            const int q = t + FC_NT * hh;
-            const int k2a = (q >> 2) & 15, k1 = q >> 6;
-            fcv w[8];
-#pragma unroll
-            for (int k2b = 0; k2b < 8; ++k2b) {
-                const int fr = k1 + 16 * k2a + 256 * k2b;
-                const int c = c0 + j;
-                const uint32_t pp = (uint32_t)c * (uint32_t)fr;
-                float sn, cs;
-                __sincosf(FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
-                w[k2b] = cmulf(y[(int64_t)fr * FC_C + c], (fcv){cs, sn});
-            }
-            fc_dft8<1>(w);   // -> n2a
-            fc_twiddle_pow<8>(w, W128 * (float)k2a);
-#pragma unroll
-            for (int a = 0; a < 8; ++a) sm[e2(k1, k2a, a, j)] = w[a];
-        }
-        __syncthreads();
-        fcv u[16];
-        const int n2a = (t >> 2) & 7, k1b = t >> 5;
-#pragma unroll
-        for (int k2a = 0; k2a < 16; ++k2a) u[k2a] = sm[e2(k1b, k2a, n2a, j)];
-        __syncthreads();
-        fc_dft16<1>(u);   // -> n2b
-        {   // times w_2048^(-n2 k1), n2 = n2a + 8 n2b
-            float s0, cz;
-            __sincosf(W2048 * (float)(n2a * k1b), &s0, &cz);
-            const fcv w0 = {cz, s0};
-#pragma unroll
-            for (int n2b = 0; n2b < 16; ++n2b) u[n2b] = cmulf(u[n2b], w0);
-            fc_twiddle_pow<16>(u, W2048 * 8.0f * (float)k1b);
-        }
-#pragma unroll
-        for (int n2b = 0; n2b < 16; ++n2b) sm[e1(k1b, n2a + 8 * n2b, j)] = u[n2b];
-        __syncthreads();
-        {   // inverse (A): task (j, n2) -> r = n2 + 128 n1
-            const int n2 = t >> 2;
-            fcv v[16];
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) v[k1] = sm[e1(k1, n2, j)];
-            fc_dft16<1>(v);
-#pragma unroll
-            for (int n1 = 0; n1 < 16; ++n1) y[(int64_t)(n2 + 128 * n1) * FC_C + c0 + j] = v[n1];
-        }
-    }
-}
-
-// (A) and (C) for R = 1024 with rows of C = 16384 (m = 2^24 as 1024 x 16384), NCOL = 8 columns
-// per workgroup, register-staged as k_fc_cols2048 (1024 = 16 x 8 x 8; n = n2 + 64 n1,
-// n2 = n2a + 8 n2b; k = k1 + 16 k2a + 128 k2b): forward (A) task (j, n2): DFT-16 over n1, times
-// w_1024^(n2 k1); (B) tasks (j, k1, n2a), two per thread: DFT-8 over n2b, times w_64^(n2a k2a);
-// (C) tasks (j, k1, k2a), two per thread: DFT-8 over n2a -> f_r = k. Exchange 1 [k1][n2][j],
-// exchange 2 [k1][k2a][n2a (pad to 9)][j]: lanes along j then n2a / k2a, conflict-free.
+// (A) for R = 1024 with rows of C = 16384 (m = 2^24 as 1024 x 16384), NCOL = 8 columns per
+// workgroup, register-staged (1024 = 16 x 8 x 8; n = n2 + 64 n1, n2 = n2a + 8 n2b; k = k1 + 16 k2a
+// + 128 k2b): task (j, n2): DFT-16 over n1, times w_1024^(n2 k1); (B) tasks (j, k1, n2a), two per
+// thread: DFT-8 over n2b, times w_64^(n2a k2a); (C) tasks (j, k1, k2a), two per thread: DFT-8
+// over n2a -> f_r = k. Exchange 1 [k1][n2][j], exchange 2 [k1][k2a][n2a (pad to 9)][j]: lanes
+// along j then n2a / k2a, conflict-free. 252 against the Stockham kernel's 369 us (r05z3). The
+// inverse columns stay on the Stockham kernel k_fc_cols<false, 1024, 16384>: the staged inverse
+// measured 549 against 476 us (r05z3; deleted in round 6).
 constexpr int FCD_R = 1024, FCD_NCOL = 8, FCD_S2 = 9;
-template <bool FWD>
 __global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
                    float2* __restrict__ Yv) {
@@ -5184,7 +4970,7 @@ void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t
     auto e2 = [](int k1, int k2a, int n2a, int jj) {
         return ((k1 * 8 + k2a) * FCD_S2 + n2a) * FCD_NCOL + jj;
     };
-    if (FWD) {
+    {
         const HannRow h = hann_row(info, row);
         const double inv = h.scale == 0.0 ? 0.0 : 1.0 / h.scale;
         const double2* src = S + (int64_t)row * stride + h.first;
@@ -5244,65 +5030,6 @@ void k_fc_cols1024(const double2* __restrict__ S, int64_t stride, const uint64_t
                 __sincosf(-FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
                 y[(int64_t)fr * C + c] = cmulf(w[k2b], (fcv){cs, sn});
             }
-        }
-    } else {
-        fcv r[2][8];   // all 16 loads in flight before any arithmetic
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int q = t + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
-#pragma unroll
-            for (int k2b = 0; k2b < 8; ++k2b) r[hh][k2b] = y[(int64_t)(k1 + 16 * k2a + 128 * k2b) * C + c];
-        }
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {   // inverse (C): tasks (j, k2a, k1)
-            const int q = t + FC_NT * hh, k2a = (q >> 3) & 7, k1 = q >> 6;
-            fcv w[8];
-#pragma unroll
-            for (int k2b = 0; k2b < 8; ++k2b) {
-                const int fr = k1 + 16 * k2a + 128 * k2b;
-                const uint32_t pp = (uint32_t)c * (uint32_t)fr;
-                float sn, cs;
-                __sincosf(FC_2PI * ((float)pp * (1.0f / (float)M)), &sn, &cs);
-                w[k2b] = cmulf(r[hh][k2b], (fcv){cs, sn});
-            }
-            fc_dft8<1>(w);   // -> n2a
-            fc_twiddle_pow<8>(w, W64 * (float)k2a);
-#pragma unroll
-            for (int a = 0; a < 8; ++a) sm[e2(k1, k2a, a, j)] = w[a];
-        }
-        __syncthreads();
-        fcv u[2][8];
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {   // inverse (B): tasks (j, n2a, k1)
-            const int q = t + FC_NT * hh, n2a = (q >> 3) & 7, k1 = q >> 6;
-#pragma unroll
-            for (int k2a = 0; k2a < 8; ++k2a) u[hh][k2a] = sm[e2(k1, k2a, n2a, j)];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int q = t + FC_NT * hh, n2a = (q >> 3) & 7, k1 = q >> 6;
-            fc_dft8<1>(u[hh]);   // -> n2b; times w_1024^(-n2 k1), n2 = n2a + 8 n2b
-            float s0, cz;
-            __sincosf(W1024 * (float)(n2a * k1), &s0, &cz);
-            const fcv w0 = {cz, s0};
-#pragma unroll
-            for (int n2b = 0; n2b < 8; ++n2b) u[hh][n2b] = cmulf(u[hh][n2b], w0);
-            fc_twiddle_pow<8>(u[hh], W1024 * 8.0f * (float)k1);
-#pragma unroll
-            for (int n2b = 0; n2b < 8; ++n2b) sm[e1(k1, n2a + 8 * n2b, j)] = u[hh][n2b];
-        }
-        __syncthreads();
-        {   // inverse (A): task (j, n2) -> r = n2 + 64 n1
-            int to = t;   // opaque: no store address kept live from inverse (C)
-            __asm__ volatile("" : "+v"(to));
-            const int n2 = to >> 3, jo = to & 7;
-            fcv v[16];
-#pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) v[k1] = sm[e1(k1, n2, jo)];
-            fc_dft16<1>(v);
-#pragma unroll
-            for (int n1 = 0; n1 < 16; ++n1) y[(int64_t)(n2 + 64 * n1) * C + c0 + jo] = v[n1];
         }
     }
 }
@@ -5625,7 +5352,7 @@ static int32_t lists_min_k() {
 static bool use_prebuilt(int32_t K) { return K >= lists_min_k(); }
 // Envelope records (k_items, env_fit.inc) in the uniform caustic mode; EFD_ENV=0 (read once per
 // process) builds none: the A/B and parity switch of DESIGN.md's round-6 study. prepare decides
-// per waveform and the sum follows the records (Item::jser = 0), so they always agree.
+// per waveform and the sum follows the records (Item::jser), so they always agree.
 static bool env_records() {
     static const bool v = [] {
         const char* e = std::getenv("EFD_ENV");
@@ -6346,42 +6073,10 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
 }
 // the four-step split's row length C for a transform length m (the lag kernel's spectrum is
 // laid out [f_r][f_c], R = m / C): 16384 at m = 2^24 (1024 x 16384: the column kernels read
-// 128 B segments, r05z), else 8192; EFD_FC_C16=0 keeps 8192 at 2^24 too (an experiment switch
-// for paired A/B runs, read once)
+// 128 B segments, r05z; the 2048 x 8192 split measured 1.08 against 0.73 ms of column passes and
+// was deleted in round 6), else 8192
 int efd_hann_four_step_cols(int64_t m) {
-    static const bool c16 = [] {
-        const char* e = getenv("EFD_FC_C16");
-        return !(e && e[0] == '0');
-    }();
-    return (c16 && m == ((int64_t)1 << 24)) ? FC_C16 : FC_C;
-}
-// the register-staged column kernels at R = 2048 (EFD_FC_COLS=0: the Stockham ones, an
-// experiment switch for paired A/B runs; read once)
-static bool fc_cols_staged() {
-    static const bool v = [] {
-        const char* e = getenv("EFD_FC_COLS");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-// the column kernels at 1024 x 16384: the register-staged forward and the Stockham inverse
-// (r05z3: staged forward 252 against 369 us, staged inverse 549 against 476 us); EFD_FC_COLS16
-// = 0 both Stockham, 2 both staged (an experiment switch; read once)
-static int fc_cols1024_mode() {
-    static const int v = [] {
-        const char* e = getenv("EFD_FC_COLS16");
-        return (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
-    }();
-    return v;
-}
-// the 16384-point rows with two-pass exchanges, two workgroups per CU (EFD_FC_R16H=0: one
-// workgroup per CU with complex exchanges, an experiment switch; read once)
-static bool fc_rows16k_half() {
-    static const bool v = [] {
-        const char* e = getenv("EFD_FC_R16H");
-        return !(e && e[0] == '0');
-    }();
-    return v;
+    return m == ((int64_t)1 << 24) ? FC_C16 : FC_C;
 }
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream) {
@@ -6390,20 +6085,17 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         return fail(EFD_ERR_ARG, "efd_hann_convolve: bad arguments (m: a power of two in "
                                  "[2^21, 2^25], >= nf)");
     hipStream_t st = (hipStream_t)stream;
-    if (m == ((int64_t)1 << 24) && efd_hann_four_step_cols(m) == FC_C16) {
+    if (m == ((int64_t)1 << 24)) {
         constexpr int R16 = (1 << 24) / FC_C16;
         constexpr int NC16 = FcCols<R16>::NCOL;
         static_assert(NC16 == FCD_NCOL && R16 == FCD_R, "1024 x 16384: 8 columns per block");
-        hipLaunchKernelGGL((fc_cols1024_mode() >= 1 ? k_fc_cols1024<true> : k_fc_cols<true, R16, FC_C16>),
-                           dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
+        hipLaunchKernelGGL(k_fc_cols1024, dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
                            (const double2*)S, stride, info, (float2*)Y);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(fc_rows16k_half() ? k_fc_rows16k_h : k_fc_rows16k,
-                           dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st, (const float2*)kfp, m,
-                           (int)rows, (float2*)Y);
+        hipLaunchKernelGGL(k_fc_rows16k_h, dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st,
+                           (const float2*)kfp, m, (int)rows, (float2*)Y);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL((fc_cols1024_mode() == 2 ? k_fc_cols1024<false>
-                                                 : k_fc_cols<false, R16, FC_C16>),
+        hipLaunchKernelGGL((k_fc_cols<false, R16, FC_C16>),
                            dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
                            (const double2*)nullptr, (int64_t)0, (const uint64_t*)nullptr,
                            (float2*)Y);
@@ -6430,25 +6122,9 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
         case 256: EFD_FC(256); break;
         case 512: EFD_FC(512); break;
         case 1024: EFD_FC(1024); break;
-        case 2048:
-            if (fc_cols_staged()) {
-                hipLaunchKernelGGL((k_fc_cols2048<true>), dim3(FC_C / FCC_NCOL, (unsigned)rows),
-                                   dim3(FC_NT), 0, st, (const double2*)S, stride, info, y);
-                HIP_TRY(hipGetLastError());
-                hipLaunchKernelGGL(k_fc_rows, dim3(2048 * (unsigned)rows), dim3(FR_NT), 0, st,
-                                   (const float2*)kfp, m, (int)rows, y);
-                HIP_TRY(hipGetLastError());
-                // the inverse pass stays on the Stockham kernel: its staged form measured 649
-                // against 611 us (r05l; both at ~0.6 of HBM, bound by the 32-B column segments)
-                hipLaunchKernelGGL((k_fc_cols<false, 2048>), dim3(FC_C / FcCols<2048>::NCOL,
-                                   (unsigned)rows), dim3(FC_NT), 0, st, (const double2*)nullptr,
-                                   (int64_t)0, (const uint64_t*)nullptr, y);
-                HIP_TRY(hipGetLastError());
-            } else {
-                EFD_FC(2048);
-            }
-            break;
-        default: EFD_FC(4096); break;
+        case 4096: EFD_FC(4096); break;
+        default:   // R = 2048 is m = 2^24, the 1024 x 16384 split above
+            return fail(EFD_ERR_ARG, "efd_hann_convolve: no four-step split for this m");
     }
 #undef EFD_FC
     return EFD_OK;
@@ -6480,12 +6156,9 @@ int efd_hann_loglike(const double* S, int64_t stride, const float* Y, const uint
                                           ((nb + threads - 1) / threads + 7) / 8 * 8);
     hipStream_t st = (hipStream_t)stream;
     static_assert(EFD_LOGLIKE_SCRATCH % 8 == 0, "chunks: whole rounds of the 8 XCDs");
-    // two rows a workgroup when the rows pair up (EFD_HANN_RPT=1: one, an experiment switch)
-    static const int rpt_env = [] {
-        const char* e = getenv("EFD_HANN_RPT");
-        return e && e[0] == '1' ? 1 : 2;
-    }();
-    const int rpt = (rows % 2 == 0) ? rpt_env : 1;
+    // two rows a workgroup when the rows pair up (d and w read once for both: 362 -> 318 us,
+    // r05zr; an odd row count takes one row a workgroup)
+    const int rpt = (rows % 2 == 0) ? 2 : 1;
     hipLaunchKernelGGL(rpt == 2 ? k_hann_loglike_partial<2> : k_hann_loglike_partial<1>,
                        dim3((unsigned)(np * (rows / rpt))), dim3(threads), 0, st,
                        (const double2*)S, stride, (const float2*)Y, info, m, nf, k0,

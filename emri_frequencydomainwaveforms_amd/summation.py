@@ -259,6 +259,17 @@ class ModeSumEngine:
                    "efd_modesum_stats", self.lib)
         return int(c.value), int(e.value), int(g.value)
 
+    def env_evaluations(self, stream=None):
+        """SPA evaluations of the last launch made on envelope records (k_items' per-record
+        amplitude / K_1/3-phase polynomials)."""
+        import ctypes
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        e = ctypes.c_int64(0)
+        _lib.check(self.lib.efd_modesum_env_evaluations(self._ws.data_ptr(), ctypes.byref(e), st),
+                   "efd_modesum_env_evaluations", self.lib)
+        return int(e.value)
+
     def run(self, inp, freq, out=None, grid_symmetric=None, scale=1.0 + 0.0j, accumulate=False,
             check=True):
         """Launch on the current stream; with check=True synchronise and surface device errors."""

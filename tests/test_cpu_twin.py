@@ -178,3 +178,37 @@ def test_loglike_and_inner_product_cpu_vs_oracle():
                                      out.ctypes.data, None, None) == 0
     ref = 4.0 * np.sum(np.conj(h) * d * w)
     assert abs(out[0] - ref.real) <= 1e-12 * abs(ref) and abs(out[1] - ref.imag) <= 1e-12 * abs(ref)
+
+
+_ENV_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import bench
+from emri_frequencydomainwaveforms_amd import cputwin
+w = bench.build_workload(T=0.25, eps=1e-3)
+S = cputwin.modesum(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"], w["f_r"], w["m"],
+                    w["n"], w["ylm_p"], w["ylm_m"], w["freq"], w["prefactor"])
+np.save(sys.argv[2], S)
+"""
+
+
+def test_twin_envelope_records_on_and_off(tmp_path):
+    """The twin's envelope records (env_fit.inc, as k_items: A(w) of degree 6 and theta(w)
+    folded into the phase cubic on records whose polynomials pass the 1e-11 / 1e-10 check)
+    against the per-bin arithmetic (EFD_ENV=0, a child process each): within 1e-10 of max|S|
+    on a 0.25-yr eps = 1e-3 source, identical support."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    S = {}
+    for env in ("1", "0"):
+        path = str(tmp_path / f"S{env}.npy")
+        r = subprocess.run([sys.executable, "-c", _ENV_CHILD, root, path], capture_output=True,
+                           text=True, timeout=300, env=dict(os.environ, EFD_ENV=env), cwd=root)
+        assert r.returncode == 0, r.stderr[-3000:]
+        S[env] = np.load(path)
+    mx = np.abs(S["0"]).max()
+    np.testing.assert_array_equal(S["1"] != 0, S["0"] != 0)
+    assert 0.0 < np.abs(S["1"] - S["0"]).max() <= 1e-10 * mx

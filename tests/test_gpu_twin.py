@@ -81,3 +81,68 @@ def test_hip_equals_twin_config2_full_size():
     record_parity("config2_hip_vs_twin", stats)
     assert ok, stats
     np.testing.assert_array_equal(S != 0, T != 0)
+
+
+_NOENV_CHILD = r"""
+import os, sys, json
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch
+import bench
+from emri_frequencydomainwaveforms_amd.summation import DeviceInputs, ModeSumEngine
+w = bench.build_workload(T=0.25, eps=1e-3)
+inp = DeviceInputs.from_host(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"], w["f_r"],
+                             w["m"], w["n"], w["ylm_p"], w["ylm_m"])
+eng = ModeSumEngine()
+S = eng.run(inp, torch.as_tensor(w["freq"], device="cuda"), grid_symmetric=True,
+            scale=w["prefactor"]).cpu().numpy()
+np.save(sys.argv[2], S)
+print(json.dumps(dict(stats=eng.stats(), env=eng.env_evaluations())))
+"""
+
+
+def test_envelope_records_on_and_off(tmp_path):
+    """The mode sum with envelope records (the default: A(w) and theta(w) as per-record
+    polynomials, k_items / env_fit.inc) and without (EFD_ENV=0, read once per process: a child
+    process each), on a 0.25-yr eps = 1e-3 source: the same support, contributions and
+    evaluations; most evaluations on envelope records with them and none without; spectra
+    within 1e-10 of max|S| of each other, and each within 1e-10 of the host twin run the same
+    way (the twin follows EFD_ENV too)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for env in ("1", "0"):
+        path = str(tmp_path / f"S{env}.npy")
+        r = subprocess.run([sys.executable, "-c", _NOENV_CHILD, root, path], capture_output=True,
+                           text=True, timeout=240, env=dict(os.environ, EFD_ENV=env), cwd=root)
+        assert r.returncode == 0, r.stderr[-3000:]
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        tpath = str(tmp_path / f"T{env}.npy")
+        tw = subprocess.run([sys.executable, "-c", _TWIN_CHILD, root, tpath], capture_output=True,
+                            text=True, timeout=240, env=dict(os.environ, EFD_ENV=env), cwd=root)
+        assert tw.returncode == 0, tw.stderr[-3000:]
+        out[env] = (np.load(path), j, np.load(tpath))
+    (S1, j1, T1), (S0, j0, T0) = out["1"], out["0"]
+    assert j1["stats"] == j0["stats"]
+    ev = j1["stats"][1]
+    assert j0["env"] == 0 and j1["env"] > 0.5 * ev, (j1["env"], ev)
+    mx = np.abs(S0).max()
+    np.testing.assert_array_equal(S1 != 0, S0 != 0)
+    assert np.abs(S1 - S0).max() <= 1e-10 * mx
+    assert np.abs(S1 - T1).max() <= 1e-10 * mx and np.abs(S0 - T0).max() <= 1e-10 * mx
+
+
+_TWIN_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import bench
+from emri_frequencydomainwaveforms_amd import cputwin
+w = bench.build_workload(T=0.25, eps=1e-3)
+T = cputwin.modesum(w["t"], w["amp"], w["phi_phi"], w["phi_r"], w["f_phi"], w["f_r"], w["m"],
+                    w["n"], w["ylm_p"], w["ylm_m"], w["freq"], w["prefactor"])
+np.save(sys.argv[2], T)
+"""

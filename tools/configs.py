@@ -39,6 +39,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 SUM_KW = dict(pad_output=True, output_type="fd", odd_len=True)
+NO_CPU = False       # --no-cpu-baseline
+CPU_SECONDS = 8.0    # --cpu-seconds: the host twin's time budget per configuration
 # injection angles of emri_pe.py:603-617 (qS, phiS, qK, phiK) and dist = 2.4539 Gpc (:612)
 ANGLES = dict(dist=2.4539, qS=0.2, phiS=0.2, qK=0.8, phiK=0.8)
 
@@ -88,7 +90,19 @@ def config1(reps):
     dev = (time.perf_counter() - t0) / reps
     nf = len(few.waveform_generator.create_waveform.frequency)
     K = len(few.waveform_generator.last_modes[0])
+    cpu = None
+    if not NO_CPU:
+        # the host twin on the same waveform (BASELINE.md section 2's CPU column): the same
+        # stand-in upstream, prepared beforehand, then efd_modesum_cpu writing h+/hx
+        import bench
+        from emri_frequencydomainwaveforms_amd.waveform import get_viewing_angles
+        th, ph = get_viewing_angles(ANGLES["qS"], ANGLES["phiS"], ANGLES["qK"], ANGLES["phiK"])
+        w = bench.build_workload(T=T, dt=dt, eps=eps, M=1e6, mu=10.0, e0=0.35, p0=p0,
+                                 Phi_phi0=1.0, Phi_r0=3.0, theta=th, phi=ph, dist=ANGLES["dist"])
+        cpu = bench.twin_job_rate([bench.twin_waveform_job(w)] * 64, "waveforms/s",
+                                  seconds=CPU_SECONDS, what="config-1 waveforms")
     return {"config": "config1: M=1e6 mu=10 e0=0.35 Tobs=1yr dt=10s eps=1e-2", "p0": p0,
+            "cpu_baseline": cpu,
             "harmonics": K, "N_f": nf, "device_waveforms_per_s": 1.0 / dev,
             "device_ms": dev * 1e3, "api_waveforms_per_s": 1.0 / api, "api_ms": api * 1e3,
             "host_upstream_ms": cache.host_s * 1e3,
@@ -165,6 +179,11 @@ def config3(reps, slots=4):
     prep.wait()
     dev = (time.perf_counter() - t0) / reps
     K = [len(w["m"]) for w in ws]
+    cpu = None
+    if not NO_CPU:   # the host twin over the same 100 points' inputs
+        cpu = bench.twin_job_rate([bench.twin_waveform_job(w) for w in ws], "waveforms/s",
+                                  seconds=CPU_SECONDS, what="grid points")
+        cpu["host_upstream_s_per_grid_serial"] = host_s
     # the drivers' scan (check_mode_by_mode.py:183-229): per point the p0 root solve
     # (get_p_at_t) and the whole few_gen call, one at a time, native upstream
     from emri_frequencydomainwaveforms_amd.trajectory import EMRIInspiral, get_p_at_t
@@ -210,7 +229,7 @@ def config3(reps, slots=4):
     api_b = float(np.median(tb))
     return {"config": "config3: 10x10 grid M=logspace(5,7) e0=linspace(0.1,0.6) mu=1e-5 M "
                       "Tobs=1yr dt=10s eps=1e-2", "waveforms": len(ws), "N_f": nf,
-            "harmonics_min_max": [min(K), max(K)],
+            "harmonics_min_max": [min(K), max(K)], "cpu_baseline": cpu,
             "device_waveforms_per_s": len(ws) / dev, "device_ms_per_grid": dev * 1e3,
             "pipeline_waveforms_per_s": len(ws) / dev_pipe,
             "api_waveforms_per_s": len(ws) / api,
@@ -273,7 +292,15 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
         ll2 = like.get_ll(walkers, **kw)
     _sync()
     dev = (time.perf_counter() - t0) / reps
-    return {"config": name, "walkers_per_half_step": B, "N_pos": nbins,
+    cpu = None
+    if not NO_CPU and not windowed:
+        # the host twin on the same walkers against the likelihood's own d and w
+        import bench
+        from emri_frequencydomainwaveforms_amd import pe
+        st = pe.setup(Tobs=T, eps=eps, downsample=downsample, nwalkers=nwalkers, **extra)
+        jobs, ll_twin = bench.twin_likelihood_jobs(st, st.half_steps()[0])
+        cpu = bench.twin_job_rate(jobs, "logL/s", seconds=CPU_SECONDS, what="walkers")
+    return {"config": name, "walkers_per_half_step": B, "N_pos": nbins, "cpu_baseline": cpu,
             "device_loglikes_per_s": B / dev, "device_ms_per_half_step": dev * 1e3,
             "api_loglikes_per_s": B / api, "api_ms_per_half_step": api * 1e3,
             "host_upstream_ms_per_walker": cache.host_s / B * 1e3,
@@ -308,7 +335,11 @@ def main():
                     "a buffer + efd_loglike instead of the fused batched likelihood")
     ap.add_argument("--fused-group", type=int, default=0, help="walkers per fused launch "
                     "(Likelihood.FUSED_GROUP; 0 = its default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the host twin rates")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     args = ap.parse_args()
+    global NO_CPU, CPU_SECONDS
+    NO_CPU, CPU_SECONDS = args.no_cpu_baseline, args.cpu_seconds
     which = set(args.only.split(","))
     out = []
     if "1" in which:
