@@ -433,6 +433,9 @@ def main():
     ap.add_argument("--sum-priority", type=int, default=0,
                     help="overlap pipeline: torch stream priority of the sum stream (negative = "
                          "higher; the preparation stream keeps the default)")
+    ap.add_argument("--prep-priority", type=int, default=0,
+                    help="overlap pipeline: torch stream priority of the preparation stream "
+                         "(negative = higher)")
     ap.add_argument("--diag-sum-only", action="store_true",
                     help="diagnostic, not the metric: each slot is prepared once in the warm-up, "
                          "then every step runs only the mode sum (the sum-stream ceiling)")
@@ -509,7 +512,7 @@ def main():
                            fS=None if overlap else torch.view_as_real(
                                torch.empty(nf, dtype=torch.complex128, device=dev))))
         slots.append(dict(wf=wf, prep_done=torch.cuda.Event(), sum_done=None))
-    s_prep = torch.cuda.Stream(dev)
+    s_prep = torch.cuda.Stream(dev, priority=args.prep_priority)
     s_sums = [torch.cuda.Stream(dev, priority=args.sum_priority)
               for _ in range(max(1, args.sum_streams))] if overlap else [s_prep]
     s_sum = s_sums[0]

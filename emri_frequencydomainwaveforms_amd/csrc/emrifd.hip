@@ -119,7 +119,13 @@ constexpr double FAST_Y = 153.0;
 #include "spa_tables.inc"
 // the K_{1/3} factor's polar phase, leading coefficient TH_0 (see KTHN at its use in spa_fast_m)
 constexpr double KTH0 = -0.069444444444444444444;   // TH_0
-// envelope records (k_items: A(w) polynomial, theta folded into the phase cubic)
+// envelope records (k_items: A(w) polynomial, theta folded into the phase cubic); 1/sqrt from
+// the hardware estimate and two Newton steps (~1 ulp; the fit's check needs 1e-11)
+__device__ __forceinline__ double env_rsqrt(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = y * fma(-0.5 * x * y, y, 1.5);
+    return y * fma(-0.5 * x * y, y, 1.5);
+}
 #define EFD_HD __device__
 #include "env_fit.inc"
 #undef EFD_HD

@@ -64,6 +64,7 @@ using std::fabs;
 using std::fma;
 using std::fmax;
 using std::sqrt;
+inline double env_rsqrt(double x) { return 1.0 / std::sqrt(x); }
 #define EFD_HD
 #include "env_fit.inc"
 #undef EFD_HD
