@@ -20,6 +20,7 @@ EFD_LOGLIKE_SCRATCH = 1024
 EFD_INNER_SCRATCH = 2048
 EFD_BATCH_MAX = 16
 EFD_HANN_ROWS_MAX = 16   # efd_hann_loglike's rows per call (include/emrifd.h)
+EFD_HANN_LOCAL_PARTIALS = 4096   # efd_hann_loglike_local's scratch doubles per row
 
 # every symbol include/emrifd.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = (
@@ -56,6 +57,8 @@ EXPORTED_SYMBOLS = (
     "efd_hann_four_step_cols",
     "efd_hann_polarizations",
     "efd_hann_loglike",
+    "efd_hann_loglike_local",
+    "efd_hann_loglike_local_partials",
     "efd_loglike",
     "efd_inner_product",
     "efd_modesum_cpu",
@@ -243,6 +246,11 @@ def load(path=None):
     lib.efd_hann_polarizations.argtypes = [vp, vp, vp, i64, i64, i64, vp, vp, vp]
     lib.efd_hann_loglike.restype = ctypes.c_int
     lib.efd_hann_loglike.argtypes = [vp, i64, vp, vp, i64, i32, i64, i64, vp, vp, vp, vp, vp]
+    lib.efd_hann_loglike_local.restype = ctypes.c_int
+    lib.efd_hann_loglike_local.argtypes = [vp, i64, i64, i32, vp, i64, vp, vp, vp, vp, i64, vp,
+                                           vp, vp, vp]
+    lib.efd_hann_loglike_local_partials.restype = ctypes.c_int
+    lib.efd_hann_loglike_local_partials.argtypes = [i64]
     lib.efd_loglike.restype = ctypes.c_int
     lib.efd_loglike.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp]
     lib.efd_inner_product.restype = ctypes.c_int

@@ -5147,6 +5147,141 @@ __global__ __launch_bounds__(256) void k_hann_loglike_partial(
     }
 }
 
+// (C) with the windowed logL fused in (efd_hann_loglike_local). Per bin the two channels' terms
+// of a bin k and of its mirror k' = nf-1-k combine into one term on each (with the same weight
+// w on both channels, p = d0 - w h+, q = d1 - w hx: |p|^2 + |q|^2 = (|p - iq|^2 + |p + iq|^2)/2,
+// p - iq = (d0 - i d1) - w S_w[k], p + iq = (d0 + i d1) - w conj(S_w[k'])), so the logL is
+//   (1/2) sum_j |dl[j] - wl[j] S_w[j]|^2 over the whole grid
+// with dl[k] = d0 - i d1 (k >= k0), dl[k'] = conj(d0 + i d1), wl = w at both (the caller's
+// layout: fdutils.HannConvolution.local_data; the self-mirror bin kself takes its second term
+// from dl[nf]). Every term is local to its bin, so the inverse column pass reduces them as it
+// produces the correction: the correction array is neither written nor read back.
+// The pipeline's kernel spectrum carries the difference factor 2i sin(2 pi f / m), so the
+// transform yields Dc[s] = Y[s+1] - Y[s-1] directly (no neighbour column needed): valid for
+// s in [m - nf, m - 1) when m >= nf + len, and at s = m - 1 (bin u = nf - 1, whose +1 neighbour
+// wraps to u = 0) Y[m] = Y[0] differs from C(u = 0) = Y[m - nf] by y[0] (K[(-(m-nf)) mod nf] -
+// K[0]) alone (kfix = K[0] - K[(-(m-nf)) mod nf], added back). emit (one row): write
+// dl[j] = wl[j] S_w[j] (and dl[nf] = dl[kself]) instead, the data of an injection made by this
+// same arithmetic (its logL against itself is then exactly 0).
+// Workgroups: 1-D, b -> XCD b mod 8; XCD x takes column blocks [x G/8, (x+1) G/8) and on it the
+// rows of one column block are consecutive, so dl / wl (24 B a bin, the same for every row) come
+// from HBM once and from the XCD's L2 for the other rows. part[row * G + column block], halved.
+template <int R, int C>
+__global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void k_fc_cols_ll(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
+                  const float2* __restrict__ Yv, int64_t nf, const double2* __restrict__ dl,
+                  const double* __restrict__ wl, int64_t kself, double2 kfix, int rows,
+                  double* __restrict__ part, double2* __restrict__ emit) {
+#pragma clang fp contract(off)
+    constexpr int NCOL = FcCols<R>::NCOL, LOGL = FcCols<R>::LOGL;
+    constexpr int64_t M = (int64_t)R * C;
+    constexpr int NQ = R * NCOL / FC_NT;
+    static_assert(R * NCOL % FC_NT == 0, "whole rounds of elements per thread");
+    constexpr int G = C / NCOL;
+    static_assert(G % 8 == 0, "column blocks: a multiple of the 8 XCDs");
+    __shared__ fcv sm[R * FcColIdx<NCOL>::STRIDE];
+    __shared__ double red[FC_NT / 64];
+    const fcv* Y = reinterpret_cast<const fcv*>(Yv);
+    const FcColIdx<NCOL> idx;
+    const int q8 = (int)(blockIdx.x >> 3);
+    const int row = q8 % rows, cb = (int)(blockIdx.x & 7) * (G / 8) + q8 / rows;
+    const int c0 = cb * NCOL;
+    const fcv* y = Y + (int64_t)row * M;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int i = threadIdx.x + q * FC_NT;
+        const int e = i / NCOL, j = i % NCOL;
+        const uint32_t p = (uint32_t)(c0 + j) * (uint32_t)e;
+        float sn, cs;
+        __sincosf(FC_2PI * ((float)p * (1.0f / (float)M)), &sn, &cs);
+        sm[idx(j, e)] = cmulf(y[(int64_t)e * C + c0 + j], (fcv){cs, sn});
+    }
+    __syncthreads();
+    fc_fft<1, R, LOGL>(sm, idx);
+    const HannRow h = hann_row(info, row);
+    const int64_t off = M - nf;
+    // a support longer than m - nf leaves Y[m - nf - 1] aliased: the row's logL is NaN
+    const double cc = h.len > off ? __longlong_as_double(0x7ff8000000000000ll)
+                                  : h.scale / (4.0 * (double)(nf - 1));
+    const double2* Sr = S + (int64_t)row * stride;
+    const double2 z = make_double2(0.0, 0.0);
+    // the elements' data (dl, wl) requested QH at a time before any of them is used: QH loads
+    // of each in flight per thread (the epilogue is latency-bound otherwise, one round trip per
+    // few elements; all 16 at once spill past 128 VGPRs); indices fit 32 bits (nf < 2^31,
+    // m <= 2^25)
+    const int nfi = (int)nf, offi = (int)off, first = (int)h.first, len = (int)h.len;
+    constexpr int QH = NQ >= 8 ? 8 : NQ;
+    static_assert(NQ % QH == 0, "whole rounds of prefetched elements");
+    double acc = 0.0;
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += QH) {
+        double2 dv[QH];
+        double wv[QH];
+#pragma unroll
+        for (int t = 0; t < QH; ++t) {
+            const int i = threadIdx.x + (q0 + t) * FC_NT;
+            const int u = (i / NCOL) * C + c0 + i % NCOL - offi;
+            int k = u + first;
+            k -= k >= nfi ? nfi : 0;
+            dv[t] = z;
+            wv[t] = 0.0;
+            if (u >= 0) {
+                wv[t] = wl[k];
+                if (emit == nullptr) dv[t] = dl[k];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < QH; ++t) {
+            const int i = threadIdx.x + (q0 + t) * FC_NT;
+            const int e = i / NCOL, j = i % NCOL;
+            const int u = e * C + c0 + j - offi;   // the correction's bin offset from first
+            if (u < 0) continue;
+            const fcv dvf = sm[idx(j, e)];
+            double dx = (double)dvf.x, dy = (double)dvf.y;
+            if (u == nfi - 1 && len > 0) {   // the +1 neighbour wraps: Y[0] -> C(u = 0)
+                const double inv = 1.0 / h.scale;
+                const double2 s0 = Sr[first];
+                const double yx = s0.x * inv, yy = s0.y * inv;
+                dx += yx * kfix.x - yy * kfix.y;
+                dy += yx * kfix.y + yy * kfix.x;
+            }
+            int k = u + first;
+            k -= k >= nfi ? nfi : 0;
+            const int kp = k + 1 < nfi ? k + 1 : 0, km = k > 0 ? k - 1 : nfi - 1;
+            const int qp = u + 1 < nfi ? u + 1 : 0, qm = u > 0 ? u - 1 : nfi - 1;
+            const double2 s = u < len ? Sr[k] : z, sp = qp < len ? Sr[kp] : z,
+                          sn2 = qm < len ? Sr[km] : z;
+            const double wx = 0.5 * s.x - 0.25 * (sp.x + sn2.x) - cc * dx;
+            const double wy = 0.5 * s.y - 0.25 * (sp.y + sn2.y) - cc * dy;
+            const double w = wv[t];
+            if (emit != nullptr) {
+                const double2 o = make_double2(wx * w, wy * w);
+                emit[k] = o;
+                if (k == kself) emit[nf] = o;
+                continue;
+            }
+            const double rx = dv[t].x - wx * w, ry = dv[t].y - wy * w;
+            acc = fma(rx, rx, fma(ry, ry, acc));
+            if (k == kself) {
+                const double2 d2 = dl[nf];
+                const double tx = d2.x - wx * w, ty = d2.y - wy * w;
+                acc = fma(tx, tx, fma(ty, ty, acc));
+            }
+        }
+    }
+    if (emit != nullptr) return;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int wv = 0; wv < FC_NT / 64; ++wv) t += red[wv];
+        part[(int64_t)row * G + cb] = 0.5 * t;
+    }
+}
+
 // fused log-likelihood partials: one workgroup per chunk, then a second pass
 __global__ void k_loglike_partial(const double2* __restrict__ h, const double2* __restrict__ d,
                                   const double* __restrict__ w, int64_t total,
@@ -6084,55 +6219,115 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
 int efd_hann_four_step_cols(int64_t m) {
     return m == ((int64_t)1 << 24) ? FC_C16 : FC_C;
 }
+// the four-step pipeline for power-of-two m in [2^21, 2^25]: forward columns (staging folded
+// in) and rows (the kernel spectrum kfp between the row transforms), then either the inverse
+// columns (Y = the correction, efd_hann_convolve) or the inverse columns with the windowed logL
+// reduced in place (ll != nullptr: efd_hann_loglike_local)
+}  // extern "C"
+struct HannLocal {
+    const double2* dl;
+    const double* wl;
+    int64_t kself;
+    double2 kfix;
+    double* part;
+    double2* emit;
+};
+template <int RR, int CC>
+static int hann_pipeline(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                         const uint64_t* info, const float* kfp, float* Y, const HannLocal* ll,
+                         hipStream_t st) {
+    constexpr int NC = FcCols<RR>::NCOL;
+    constexpr int64_t M = (int64_t)RR * CC;
+    float2* y = (float2*)Y;
+    if constexpr (CC == FC_C16) {
+        static_assert(RR == FCD_R && NC == FCD_NCOL, "1024 x 16384 split");
+        hipLaunchKernelGGL(k_fc_cols1024, dim3(CC / NC, (unsigned)rows), dim3(FC_NT), 0, st,
+                           (const double2*)S, stride, info, y);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_fc_rows16k_h, dim3(RR * (unsigned)rows), dim3(FC_NT), 0, st,
+                           (const float2*)kfp, M, (int)rows, y);
+    } else {
+        hipLaunchKernelGGL((k_fc_cols<true, RR, CC>), dim3(CC / NC, (unsigned)rows), dim3(FC_NT),
+                           0, st, (const double2*)S, stride, info, y);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_fc_rows, dim3(RR * (unsigned)rows), dim3(FR_NT), 0, st,
+                           (const float2*)kfp, M, (int)rows, y);
+    }
+    HIP_TRY(hipGetLastError());
+    if (ll == nullptr) {
+        hipLaunchKernelGGL((k_fc_cols<false, RR, CC>), dim3(CC / NC, (unsigned)rows),
+                           dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,
+                           (const uint64_t*)nullptr, y);
+    } else {
+        hipLaunchKernelGGL((k_fc_cols_ll<RR, CC>), dim3((CC / NC) * (unsigned)rows), dim3(FC_NT),
+                           0, st, (const double2*)S, stride, info, (const float2*)y, nf, ll->dl,
+                           ll->wl, ll->kself, ll->kfix, (int)rows, ll->part, ll->emit);
+    }
+    HIP_TRY(hipGetLastError());
+    return EFD_OK;
+}
+static int hann_pipeline_m(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                           const uint64_t* info, int64_t m, const float* kfp, float* Y,
+                           const HannLocal* ll, hipStream_t st) {
+    if (m == ((int64_t)1 << 24))
+        return hann_pipeline<(1 << 24) / FC_C16, FC_C16>(S, stride, nf, rows, info, kfp, Y, ll, st);
+    switch (m / FC_C) {   // R = 2048 is m = 2^24, the 1024 x 16384 split above
+        case 256: return hann_pipeline<256, FC_C>(S, stride, nf, rows, info, kfp, Y, ll, st);
+        case 512: return hann_pipeline<512, FC_C>(S, stride, nf, rows, info, kfp, Y, ll, st);
+        case 1024: return hann_pipeline<1024, FC_C>(S, stride, nf, rows, info, kfp, Y, ll, st);
+        case 4096: return hann_pipeline<4096, FC_C>(S, stride, nf, rows, info, kfp, Y, ll, st);
+        default: return fail(EFD_ERR_ARG, "efd_hann_convolve: no four-step split for this m");
+    }
+}
+extern "C" {
+static bool hann_four_step_m(int64_t m, int64_t nf) {
+    return m >= nf && m >= ((int64_t)1 << 21) && m <= ((int64_t)1 << 25) && (m & (m - 1)) == 0;
+}
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream) {
     if (!hann_rows_ok("efd_hann_convolve", S, stride, nf, rows) || !info || !kfp || !Y ||
-        m < nf || m < ((int64_t)1 << 21) || m > ((int64_t)1 << 25) || (m & (m - 1)) != 0)
+        !hann_four_step_m(m, nf))
         return fail(EFD_ERR_ARG, "efd_hann_convolve: bad arguments (m: a power of two in "
                                  "[2^21, 2^25], >= nf)");
+    return hann_pipeline_m(S, stride, nf, rows, info, m, kfp, Y, nullptr, (hipStream_t)stream);
+}
+int efd_hann_loglike_local_partials(int64_t m) {
+    if (m == ((int64_t)1 << 24)) return FC_C16 / FcCols<(1 << 24) / FC_C16>::NCOL;
+    switch (m / FC_C) {
+        case 256: return FC_C / FcCols<256>::NCOL;
+        case 512: return FC_C / FcCols<512>::NCOL;
+        case 1024: return FC_C / FcCols<1024>::NCOL;
+        case 4096: return FC_C / FcCols<4096>::NCOL;
+        default: return 0;
+    }
+}
+int efd_hann_loglike_local(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                           const uint64_t* info, int64_t m, const float* kfd, float* Y,
+                           const double* dl, const double* wl, int64_t kself, double* out,
+                           double* scratch, double* emit, void* stream) {
+    const int np = hann_four_step_m(m, nf) ? efd_hann_loglike_local_partials(m) : 0;
+    if (!hann_rows_ok("efd_hann_loglike_local", S, stride, nf, rows) || !info || !kfd || !Y ||
+        !wl || np == 0 || kself < -1 || kself >= nf ||
+        (emit ? rows != 1 : (!dl || !out || !scratch || rows > HANN_ROWS_MAX)))
+        return fail(EFD_ERR_ARG, "efd_hann_loglike_local: bad arguments (m: a power of two in "
+                                 "[2^21, 2^25], >= nf; rows <= 16, or 1 with emit)");
+    // kfix = K[0] - K[(-(m - nf)) mod nf], K[j] = -i pi/nf + (pi/nf) cot(pi j/nf), K[0] = i pi
+    // (nf - 1)/nf (fdutils.HannConvolution.kernel_spectrum's lag kernel)
+    const double pn = M_PI / (double)nf;
+    const int64_t jw = ((-(m - nf)) % nf + nf) % nf;
+    double2 kfix = make_double2(0.0, pn * (double)(nf - 1));
+    if (jw != 0) {
+        kfix.x -= pn / std::tan(pn * (double)jw);
+        kfix.y += pn;
+    } else {
+        kfix = make_double2(0.0, 0.0);
+    }
     hipStream_t st = (hipStream_t)stream;
-    if (m == ((int64_t)1 << 24)) {
-        constexpr int R16 = (1 << 24) / FC_C16;
-        constexpr int NC16 = FcCols<R16>::NCOL;
-        static_assert(NC16 == FCD_NCOL && R16 == FCD_R, "1024 x 16384: 8 columns per block");
-        hipLaunchKernelGGL(k_fc_cols1024, dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
-                           (const double2*)S, stride, info, (float2*)Y);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_fc_rows16k_h, dim3(R16 * (unsigned)rows), dim3(FC_NT), 0, st,
-                           (const float2*)kfp, m, (int)rows, (float2*)Y);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL((k_fc_cols<false, R16, FC_C16>),
-                           dim3(FC_C16 / NC16, (unsigned)rows), dim3(FC_NT), 0, st,
-                           (const double2*)nullptr, (int64_t)0, (const uint64_t*)nullptr,
-                           (float2*)Y);
-        HIP_TRY(hipGetLastError());
-        return EFD_OK;
-    }
-    const int R = (int)(m / FC_C);
-    float2* y = (float2*)Y;
-#define EFD_FC(RR)                                                                            \
-    do {                                                                                      \
-        constexpr int NC = FcCols<RR>::NCOL;                                                  \
-        hipLaunchKernelGGL((k_fc_cols<true, RR>), dim3(FC_C / NC, (unsigned)rows), dim3(FC_NT), \
-                           0, st, (const double2*)S, stride, info, y);                        \
-        HIP_TRY(hipGetLastError());                                                           \
-        hipLaunchKernelGGL(k_fc_rows, dim3(RR * (unsigned)rows), dim3(FR_NT), 0, st,          \
-                           (const float2*)kfp, m, (int)rows, y);                              \
-        HIP_TRY(hipGetLastError());                                                           \
-        hipLaunchKernelGGL((k_fc_cols<false, RR>), dim3(FC_C / NC, (unsigned)rows),          \
-                           dim3(FC_NT), 0, st, (const double2*)nullptr, (int64_t)0,           \
-                           (const uint64_t*)nullptr, y);                                      \
-        HIP_TRY(hipGetLastError());                                                           \
-    } while (0)
-    switch (R) {
-        case 256: EFD_FC(256); break;
-        case 512: EFD_FC(512); break;
-        case 1024: EFD_FC(1024); break;
-        case 4096: EFD_FC(4096); break;
-        default:   // R = 2048 is m = 2^24, the 1024 x 16384 split above
-            return fail(EFD_ERR_ARG, "efd_hann_convolve: no four-step split for this m");
-    }
-#undef EFD_FC
+    const HannLocal ll{(const double2*)dl, wl, kself, kfix, scratch, (double2*)emit};
+    const int rc = hann_pipeline_m(S, stride, nf, rows, info, m, kfd, Y, &ll, st);
+    if (rc != EFD_OK || emit) return rc;
+    hipLaunchKernelGGL(k_loglike_final, dim3((unsigned)rows), dim3(256), 0, st, scratch, np, out);
+    HIP_TRY(hipGetLastError());
     return EFD_OK;
 }
 int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,

@@ -31,6 +31,7 @@ by dt, then masked like the FD template.
 """
 
 import os
+import weakref
 
 import numpy as np
 
@@ -117,7 +118,7 @@ class HannConvolution:
     hipFFT plans per (m, rows), _hipfft); efd_hann_loglike then reduces the windowed
     templates' logL without writing them."""
 
-    KEEP_KERNELS = 2   # lag-kernel spectra kept (one per m)
+    KEEP_KERNELS = 3   # lag-kernel spectra kept (per m: plain and the logL's differenced one)
     KEEP_PLANS = 2     # hipFFT plans kept (one per (m, rows); the lengths outside the four-step's)
     # The first-order form drops an O(e^2) term, ~3.5-5 / N^2 of max|S| (the test's 5 / N^2 bound:
     # 5e-10 at N = 1e5, 5e-6 at N = 1e3). The likelihood takes this path only where that is below
@@ -154,7 +155,9 @@ class HannConvolution:
         """The transform length for a support of `support` bins: >= n + support - 1, the power
         of two when efd_hann_convolve takes it (three passes over the rows beat hipFFT's ~11 on
         a length up to 4/3 shorter), else the smallest 2^a or 3 2^a."""
-        need = int(n) + max(int(support), 1) - 1
+        # (one bin more than the linear convolution needs: the fused logL's differenced
+        # correction reads Y one place below the window, efd_hann_loglike_local)
+        need = int(n) + max(int(support), 1)
         best = None
         for base in (1, 3):
             m = base
@@ -174,11 +177,12 @@ class HannConvolution:
         return (self.four_step and m & (m - 1) == 0
                 and self.FOUR_STEP_MIN <= m <= self.FOUR_STEP_MAX)
 
-    def kernel_spectrum(self, m, four=False):
+    def kernel_spectrum(self, m, four=False, diff=False):
         """fft(z) / m in complex64, z[t] = K[(t - (m - n)) mod n] (computed in complex128); with
         four=True in efd_hann_convolve's order: [f_r][f_c] = kf[f_r + R f_c], R = m / C with the
-        library's C for m (efd_hann_four_step_cols: 8192, or 16384 at m = 2^24)."""
-        kf = self._kf.get((m, four))
+        library's C for m (efd_hann_four_step_cols: 8192, or 16384 at m = 2^24). diff=True: times
+        2i sin(2 pi f / m), so the transforms give Y[s+1] - Y[s-1] (efd_hann_loglike_local)."""
+        kf = self._kf.get((m, four, diff))
         if kf is None:
             torch = require_gpu()
             n = self.n
@@ -188,14 +192,18 @@ class HannConvolution:
             re = torch.where(zero, torch.zeros_like(mm), (np.pi / n) / torch.tan(np.pi * mm / n))
             im = torch.where(zero, torch.full_like(mm, np.pi * (n - 1) / n),
                              torch.full_like(mm, -np.pi / n))
-            kf = (torch.fft.fft(torch.complex(re, im)) / m).to(torch.complex64)
+            kf = torch.fft.fft(torch.complex(re, im)) / m
+            if diff:
+                f = torch.arange(m, device=self.device, dtype=torch.float64)
+                kf = kf * torch.complex(torch.zeros_like(f), 2.0 * torch.sin((2.0 * np.pi / m) * f))
+            kf = kf.to(torch.complex64)
             if four:
                 from . import _lib
                 C = int(_lib.load().efd_hann_four_step_cols(m))
                 kf = kf.view(C, m // C).t().contiguous()
             while len(self._kf) >= self.KEEP_KERNELS:
                 self._kf.pop(next(iter(self._kf)))
-            self._kf[(m, four)] = kf
+            self._kf[(m, four, diff)] = kf
         return kf
 
     def _rows(self, S):
@@ -221,27 +229,8 @@ class HannConvolution:
         S = self._rows(S)
         rows, n = int(S.shape[0]), self.n
         st = torch.cuda.current_stream(S.device).cuda_stream
-        if self._info is None or self._info.shape[0] < rows:
-            self._info = torch.empty((rows, 4), dtype=torch.int64, device=S.device)
-        info = self._info[:rows]
         sp = torch.view_as_real(S).data_ptr()
-        lp = None
-        if lanes is not None:
-            if tuple(lanes.shape) != (rows, 2) or lanes.dtype != torch.int32:
-                raise ValueError("lanes: int32 [rows][2]")
-            lp = lanes.data_ptr()
-        _lib.check(lib.efd_hann_extent(sp, n, n, rows, lp, info.data_ptr(), st),
-                   "efd_hann_extent", lib)
-        if support is None:
-            ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
-            live = ext[:, 1] > 0
-            support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
-        m = self.size_for(n, max(int(support), 1), self.four_step)
-        need = rows * m
-        if self._ybuf is None or self._ybuf.numel() < need:
-            self._ybuf = None
-            self._ybuf = torch.empty(need, dtype=torch.complex64, device=S.device)
-        Y = self._ybuf[:need].view(rows, m)
+        m, info, Y = self._forward_setup(S, lib, lanes, support)
         yp = torch.view_as_real(Y).data_ptr()
         if self._four(m):
             kfp = self.kernel_spectrum(m, four=True)
@@ -328,6 +317,111 @@ class HannConvolution:
             w.data_ptr(), out.data_ptr(), scratch.data_ptr(), st), "efd_hann_loglike", lib)
         return out
 
+    # local logL data (efd_hann_loglike_local) --------------------------------------------
+    def local_ok(self, d, w, k0):
+        """Whether the windowed logL against d, w ([2][n - k0]) can take the per-bin form of
+        efd_hann_loglike_local: the same weight on both channels at every bin and every mirror
+        n-1-k of a kept bin k >= k0 outside the kept bins (or k itself)."""
+        torch = require_gpu()
+        n = self.n
+        return (2 * int(k0) >= n - 1 and tuple(d.shape) == (2, n - k0)
+                and tuple(w.shape) == (2, n - k0) and bool(torch.equal(w[0], w[1])))
+
+    def local_data(self, d, w, k0):
+        """(dl, wl, kself) of efd_hann_loglike_local from d, w ([2][n - k0], efd_loglike's
+        layout): dl complex128 [n + 1] with d0 - i d1 at each kept bin k, conj(d0 + i d1) at its
+        mirror n-1-k (at dl[n] when the mirror is k itself, kself = k), wl float64 [n] the
+        weight at both; bins neither kept nor mirrored hold 0 (no term)."""
+        torch = require_gpu()
+        n, k0 = self.n, int(k0)
+        dev = d.device
+        dl = torch.zeros(n + 1, dtype=torch.complex128, device=dev)
+        wl = torch.zeros(n, dtype=torch.float64, device=dev)
+        k = torch.arange(k0, n, device=dev)
+        j = (n - 1) - k
+        d0, d1 = d[0], d[1]
+        a = torch.complex(d0.real + d1.imag, d0.imag - d1.real)       # d0 - i d1
+        b = torch.complex(d0.real - d1.imag, -(d0.imag + d1.real))    # conj(d0 + i d1)
+        kself = n - 1 - k0 if 2 * k0 == n - 1 else -1
+        dl[j] = b
+        wl[j] = w[0]
+        if kself >= 0:
+            dl[n] = b[0]
+        dl[k] = a
+        wl[k] = w[0]
+        return dl, wl, kself
+
+    def local_emit(self, S, wl, kself, lib, lanes=None, support=None):
+        """dl = wl S_w over the grid (and dl[n] = dl[kself]) for one row S: the local data of an
+        injection made with this arithmetic (efd_hann_loglike_local's emit), whose logL against
+        a template of the same spectrum and transform length is exactly 0."""
+        from . import _lib
+        torch = require_gpu()
+        S = self._rows(S)
+        if S.shape[0] != 1:
+            raise ValueError("local_emit: one row")
+        m, info, Y = self._forward_setup(S, lib, lanes, support)
+        if not self._four(m):
+            return None
+        dl = torch.zeros(self.n + 1, dtype=torch.complex128, device=S.device)
+        st = torch.cuda.current_stream(S.device).cuda_stream
+        _lib.check(lib.efd_hann_loglike_local(
+            torch.view_as_real(S).data_ptr(), self.n, self.n, 1, info.data_ptr(), m,
+            torch.view_as_real(self.kernel_spectrum(m, four=True, diff=True)).data_ptr(),
+            torch.view_as_real(Y).data_ptr(), None, wl.data_ptr(), int(kself), None, None,
+            torch.view_as_real(dl).data_ptr(), st), "efd_hann_loglike_local", lib)
+        return dl
+
+    def _forward_setup(self, S, lib, lanes, support):
+        """efd_hann_extent, the transform length m and the Y buffer for the rows of S."""
+        from . import _lib
+        torch = require_gpu()
+        rows, n = int(S.shape[0]), self.n
+        st = torch.cuda.current_stream(S.device).cuda_stream
+        if self._info is None or self._info.shape[0] < rows:
+            self._info = torch.empty((rows, 4), dtype=torch.int64, device=S.device)
+        info = self._info[:rows]
+        lp = None
+        if lanes is not None:
+            if tuple(lanes.shape) != (rows, 2) or lanes.dtype != torch.int32:
+                raise ValueError("lanes: int32 [rows][2]")
+            lp = lanes.data_ptr()
+        _lib.check(lib.efd_hann_extent(torch.view_as_real(S).data_ptr(), n, n, rows, lp,
+                                       info.data_ptr(), st), "efd_hann_extent", lib)
+        if support is None:
+            ext = info[:, 1:3].cpu().numpy()          # first (-1: empty row), last + 1
+            live = ext[:, 1] > 0
+            support = int((ext[live, 1] - ext[live, 0]).max()) if live.any() else 1
+        m = self.size_for(n, max(int(support), 1), self.four_step)
+        need = rows * m
+        if self._ybuf is None or self._ybuf.numel() < need:
+            self._ybuf = None
+            self._ybuf = torch.empty(need, dtype=torch.complex64, device=S.device)
+        return m, info, self._ybuf[:need].view(rows, m)
+
+    def loglike_local(self, S, local, out, scratch, lib, lanes=None, support=None):
+        """efd_hann_loglike_local: every row's windowed logL against local = (dl, wl, kself)
+        into out (float64 device [rows]), the correction reduced inside the inverse column pass
+        (no correction array written or read back); scratch holds rows *
+        EFD_HANN_LOCAL_PARTIALS doubles. Returns False (nothing done) when the transform length
+        is not the four-step's: the caller takes loglike_batch."""
+        from . import _lib
+        torch = require_gpu()
+        S = self._rows(S)
+        rows = int(S.shape[0])
+        m, info, Y = self._forward_setup(S, lib, lanes, support)
+        if not self._four(m):
+            return False
+        dl, wl, kself = local
+        st = torch.cuda.current_stream(S.device).cuda_stream
+        _lib.check(lib.efd_hann_loglike_local(
+            torch.view_as_real(S).data_ptr(), self.n, self.n, rows, info.data_ptr(), m,
+            torch.view_as_real(self.kernel_spectrum(m, four=True, diff=True)).data_ptr(),
+            torch.view_as_real(Y).data_ptr(), torch.view_as_real(dl).data_ptr(), wl.data_ptr(),
+            int(kself), out.data_ptr(), scratch.data_ptr(), None, st),
+            "efd_hann_loglike_local", lib)
+        return True
+
     def __call__(self, S):
         torch = require_gpu()
         C = self.correction(S)
@@ -409,7 +503,14 @@ class get_fd_waveform_fromFD:
             self.fill(out, *args, **kwargs)
             if self.non_zero_mask is not None:
                 out[:, ~self.non_zero_mask] = 0.0
-            return [out[0], out[1]]
+            chans = [out[0], out[1]]
+            # what made these channels (made_by): weak references, the template is the caller's
+            try:
+                self._made = (np.asarray(args, dtype=np.float64).reshape(-1), dict(kwargs),
+                              [weakref.ref(c) for c in chans], out._version)
+            except (TypeError, ValueError):
+                self._made = None
+            return chans
         chans = self.waveform_generator(*args, **kwargs)
         p, c = get_fd_windowed(chans, self.window, window_in_fd=self.window_in_fd)
         p = torch.as_tensor(p)
@@ -538,18 +639,55 @@ class get_fd_waveform_fromFD:
         self.waveform_generator.lanes_ready()
         return self._hann.lane_support(self._lanes_host[:S.shape[0]].numpy(), S.shape[1])
 
-    def loglike_batch(self, out, params, d, w, scratch, **kwargs):
+    def loglike_batch(self, out, params, d, w, scratch, local=None, **kwargs):
         """The windowed templates' log-likelihoods of a batch of walkers into out (float64
         device [B]) against d, w (efd_loglike's operands, [2][num_bins]): the spectra as in
         fill_batch, then HannConvolution.loglike_batch (efd_hann_loglike: no template is
-        written). The same logL as fill_batch + efd_loglike up to the reduction order."""
+        written). The same logL as fill_batch + efd_loglike up to the reduction order.
+        local: hann_local's data for d, w: the logL reduced inside the transforms' last pass
+        (HannConvolution.loglike_local) where the transform length allows it."""
         if len(params) == 0:
             return out
         S, cw, single, lanes = self._spectra(params, **kwargs)
-        self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib, lanes,
-                                 self._lane_support(S, lanes))
+        support = self._lane_support(S, lanes)
+        if local is None or not self._hann.loglike_local(S, local, out, scratch, cw.engine.lib,
+                                                         lanes, support):
+            self._hann.loglike_batch(S, d, w, self._suffix_k0, out, scratch, cw.engine.lib,
+                                     lanes, support)
         self._status(cw, single)
         return out
+
+    def made_by(self, channels):
+        """(FEW parameters, waveform kwargs) of this model's call that returned `channels`, if
+        they are those very tensors, unmodified since (the drivers inject data = gen(*truth),
+        emri_pe.py:276), else None."""
+        made = getattr(self, "_made", None)
+        if made is None or not isinstance(channels, (list, tuple)) or len(channels) != 2:
+            return None
+        params, kw, refs, version = made
+        if any(r() is not c for r, c in zip(refs, channels)) or channels[0]._version != version:
+            return None
+        return params, kw
+
+    def hann_local(self, d, w, inj=None, **kwargs):
+        """The per-bin logL data of d, w (HannConvolution.local_data: the same weight on both
+        channels) for loglike_batch, or None where the windowed logL cannot take that form.
+        inj: the injection's FEW parameters when d is this model's template of them times w:
+        the data is then emitted by the logL's own arithmetic (HannConvolution.local_emit),
+        so the injection's logL against itself is exactly 0 as with efd_hann_loglike."""
+        if (self._hann is None or not self._windowed_s_path()
+                or not self._hann.local_ok(d, w, self._suffix_k0)):
+            return None
+        dl, wl, kself = self._hann.local_data(d, w, self._suffix_k0)
+        if inj is not None:
+            S, cw, single, lanes = self._spectra(np.asarray(inj, dtype=np.float64)[None, :],
+                                                 **kwargs)
+            e = self._hann.local_emit(S, wl, kself, cw.engine.lib, lanes,
+                                      self._lane_support(S, lanes))
+            self._status(cw, single)
+            if e is not None:
+                dl = e
+        return dl, wl, kself
 
     def fill(self, out, *args, **kwargs):
         """Write [ch1, ch2] into out (complex128 [2][num_bins], device) without copies.

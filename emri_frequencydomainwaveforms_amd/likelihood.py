@@ -85,14 +85,25 @@ class Likelihood:
     def inject_signal(self, data_stream=None, params=None, waveform_kwargs={}, noise_fn=None,
                       noise_kwargs={}, add_noise=False):
         torch = self.torch
+        # the injection's parameters when the data is exactly the template model's output for
+        # them (a single injection, no noise): the windowed logL's per-bin data is then made by
+        # the logL's own arithmetic (get_fd_waveform_fromFD.hann_local)
+        first = not hasattr(self, "injection_channels")
+        self._inj_call = None
         if params is not None:
             if self.parameter_transforms is not None:
                 key = list(self.parameter_transforms.keys())[0]
                 params = self.parameter_transforms[key].both_transforms(params)
             injection_channels = _to_numpy(self.template_model(*params, **waveform_kwargs))
+            if first:
+                self._inj_call = (np.asarray(params, dtype=np.float64).reshape(-1),
+                                  dict(waveform_kwargs))
         elif data_stream is not None:
             if isinstance(data_stream, list) is False:
                 raise ValueError("If data_stream is provided, it must be as a list.")
+            made_by = getattr(self.template_model, "made_by", None)
+            if first and made_by is not None:
+                self._inj_call = made_by(data_stream)
             injection_channels = _to_numpy(data_stream)
         else:
             raise ValueError("Must provide data_stream or params kwargs to inject signal.")
@@ -171,6 +182,7 @@ class Likelihood:
         self._d, self._w = d, w
         self._w_templ = w
         self._tile_const = None   # (their tile constants are made again on the next call)
+        self._hloc = None         # the windowed logL's per-bin data (made on the next call)
         tm = self.template_model
         mask = getattr(tm, "non_zero_mask", None)
         if mask is not None and getattr(tm, "can_fill", False):
@@ -220,16 +232,18 @@ class Likelihood:
             G = min(max(1, int(os.environ.get("EFD_WINDOW_GROUP", 0))
                         or int(getattr(tm, "WINDOW_GROUP", 8))), _lib.EFD_HANN_ROWS_MAX)
             scr = getattr(self, "_wscratch", None)
-            if scr is None or scr.numel() < G * _lib.EFD_LOGLIKE_SCRATCH:
-                scr = self._wscratch = torch.empty(G * _lib.EFD_LOGLIKE_SCRATCH,
-                                                   dtype=torch.float64, device=self.device)
+            per_row = max(_lib.EFD_LOGLIKE_SCRATCH, _lib.EFD_HANN_LOCAL_PARTIALS)
+            if scr is None or scr.numel() < G * per_row:
+                scr = self._wscratch = torch.empty(G * per_row, dtype=torch.float64,
+                                                   device=self.device)
+            local = self._hann_local(tm, kwargs)
             # the upstream G walkers at a time, in order: the first group's device work then
             # overlaps the later walkers' upstream
             _prefetch(tm, params, args, kwargs, concurrency=G if G < num_likes else None)
             for g0 in range(0, num_likes, G):
                 rows = params[g0:g0 + G]
                 tm.loglike_batch(out[g0:g0 + len(rows)], rows, self._d, self._w_templ, scr,
-                                 *args, **kwargs)
+                                 *args, local=local, **kwargs)
         elif getattr(tm, "can_fill", False):
             if self._buf is None or tuple(self._buf.shape) != (nch, nb):
                 self._buf = torch.empty((nch, nb), dtype=torch.complex128, device=self.device)
@@ -246,6 +260,26 @@ class Likelihood:
         if self.use_gpu and self.return_cupy:
             return out
         return out.cpu().numpy()
+
+    # the windowed logL in its per-bin form, reduced inside the transforms' last pass
+    # (efd_hann_loglike_local; False: efd_hann_loglike's mirror-pair form after the transforms)
+    HANN_LOCAL = True
+
+    def _hann_local(self, tm, kwargs):
+        """The template model's per-bin windowed-logL data for this likelihood's d, w (made once
+        per injection), or None."""
+        hloc = getattr(self, "_hloc", None)
+        if hloc is None:
+            make = getattr(tm, "hann_local", None) if self.HANN_LOCAL else None
+            inj = getattr(self, "_inj_call", None)
+            if make is None:
+                hloc = False
+            elif inj is not None:
+                hloc = make(self._d, self._w_templ, inj=inj[0], **inj[1]) or False
+            else:
+                hloc = make(self._d, self._w_templ, **kwargs) or False
+            self._hloc = hloc
+        return hloc or None
 
     # walkers per fused group (EFD_FUSED_GROUP overrides it: an experiment switch): one
     # efd_modesum_prepare_batch and one efd_modesum_sum_loglike each; FUSED_DEPTH groups rotate so group i+1's preparation runs beside group i's sum.

@@ -47,10 +47,15 @@ class PESetup:
 
 
 def setup(Tobs=2.0, dt=10.0, eps=1e-2, M=1e6, mu=10.0, e0=0.35, downsample=None, nwalkers=16,
-          ntemps=1, seed=SEED, caustic="uniform", subset=24, window_flag=False):
+          ntemps=1, seed=SEED, caustic="uniform", subset=24, window_flag=False, freeze_gc=True):
     """window_flag: the templates and the injection convolved with a Hann window of the grid's
     length (emri_pe.py:259-263, -window_flag 1 in test.sh: scipy.signal.windows.hann(N), N the
-    TD/FD length, odd_len); not with downsampling (emri_pe.py:330-331)."""
+    TD/FD length, odd_len); not with downsampling (emri_pe.py:330-331).
+    freeze_gc: collect, then move every object alive after the setup (torch's and scipy's
+    modules, the likelihood, its grids) out of the cyclic collector's reach (gc.freeze), as a
+    sampler process would once its setup is done: a full collection otherwise walks ~200 k
+    objects, 35 ms (130 ms with a dropped setup's garbage), inside whichever likelihood call
+    happens to trigger it (tools/api_trace.py, tools/gc_cycles.py)."""
     from .fdutils import get_fd_waveform_fromFD, get_sensitivity
     from .likelihood import Likelihood
     from .trajectory import EMRIInspiral, get_p_at_t
@@ -110,6 +115,10 @@ def setup(Tobs=2.0, dt=10.0, eps=1e-2, M=1e6, mu=10.0, e0=0.35, downsample=None,
     cov = np.load(_COV, allow_pickle=False) / (2.4 * 6)
     rng = np.random.default_rng(seed)
     start = rng.multivariate_normal(truth6, cov, size=nwalkers * ntemps)
+    if freeze_gc:
+        import gc
+        gc.collect()
+        gc.freeze()
     return PESetup(few=few, gen=gen, like=like, transform=tc, truth14=injection,
                    truth6=truth6, start=start, kwargs=kw, f_like=f_like,
                    half_step=max(1, nwalkers * ntemps // 2), info=info)

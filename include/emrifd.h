@@ -344,9 +344,28 @@ int efd_hann_stage(const double* S, int64_t stride, int64_t nf, int32_t rows,
 int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
                       const uint64_t* info, int64_t m, const float* kfp, float* Y, void* stream);
 /* The four-step split's row length C that efd_hann_convolve uses for transform length m
- * (R = m / C; kfp's layout above with 8192 replaced by C): 16384 at m = 2^24, else 8192
- * (EFD_FC_C16=0 in the environment keeps 8192 at 2^24 as well). */
+ * (R = m / C; kfp's layout above with 8192 replaced by C): 16384 at m = 2^24, else 8192. */
 int efd_hann_four_step_cols(int64_t m);
+/* The windowed logL with the correction reduced inside efd_hann_convolve's inverse column pass
+ * (no correction array written or read back). With the same weight w on both channels the two
+ * channels' terms of a kept bin k and of its mirror k' = nf-1-k recombine into one term per bin:
+ *   sum_k |d0 - w h+|^2 + |d1 - w hx|^2 = (1/2) sum_j |dl[j] - wl[j] S_w[j]|^2,
+ * dl[k] = d0[k] - i d1[k], dl[k'] = conj(d0[k] + i d1[k]), wl = w at both (complex128 [nf + 1]
+ * and float64 [nf]; the self-mirror bin kself, or -1, takes its second term from dl[nf]; other
+ * bins hold 0). kfd: kfp times 2i sin(2 pi f / m) (the transforms then give the correction's
+ * difference C[k+1] - C[k-1] directly); m >= nf + the rows' longest support (a longer support
+ * makes the row's logL NaN). out[r] = -2 sum (efd_hann_loglike's value, up to rounding);
+ * scratch: rows * efd_hann_loglike_local_partials(m) (<= 4096) doubles. emit (device complex128
+ * [nf + 1], rows = 1; dl, out, scratch unused): writes wl[j] S_w[j] (and emit[nf] at kself)
+ * instead, the dl of an injection made by this same arithmetic: the logL of the same spectrum
+ * against it is exactly 0. */
+int efd_hann_loglike_local(const double* S, int64_t stride, int64_t nf, int32_t rows,
+                           const uint64_t* info, int64_t m, const float* kfd, float* Y,
+                           const double* dl, const double* wl, int64_t kself, double* out,
+                           double* scratch, double* emit, void* stream);
+/* The partial sums per row efd_hann_loglike_local writes at transform length m (0: not a
+ * four-step length). */
+int efd_hann_loglike_local_partials(int64_t m);
 int efd_hann_polarizations(const double* S, const float* Y, const uint64_t* info, int64_t m,
                            int64_t nf, int64_t k0, double* hp, double* hc, void* stream);
 

@@ -77,7 +77,19 @@ def test_windowed_likelihood_test_sh_full_grid():
     gen.fill_batch([bufs[i] for i in range(len(batch))], params14, **s.kwargs)
     ll_w = np.array([float(like._red.loglike(bufs[i], like._d, like._w_templ)[0])
                      for i in range(len(batch))])
-    np.testing.assert_allclose(ll_w, ll, rtol=1e-12, atol=0.0)
+    # the per-bin form reduced inside the transforms (efd_hann_loglike_local, the default)
+    # against the mirror-pair form after them (efd_hann_loglike): the differenced correction's
+    # float rounding and the channel recombination only; the pair form against the written
+    # templates: the reduction order only
+    like.HANN_LOCAL, like._hloc = False, None
+    try:
+        ll_pair = like(batch, **s.kwargs)
+    finally:
+        del like.HANN_LOCAL
+        like._hloc = None
+    assert like._hann_local(gen, s.kwargs) is not None
+    np.testing.assert_allclose(ll_w, ll_pair, rtol=1e-12, atol=0.0)
+    np.testing.assert_allclose(ll, ll_pair, rtol=1e-10, atol=0.0)
     del bufs
 
     f = s.f_like
@@ -204,6 +216,65 @@ def test_hann_loglike_matches_templates():
     got = out.cpu().numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0.0)
     np.testing.assert_allclose(got[2], float(red.loglike(None, d, w)[0]), rtol=1e-12, atol=0.0)
+
+
+@pytest.mark.parametrize("n,m", [(1000001, 1 << 21), (12623261, 1 << 24)])
+def test_hann_loglike_local(n, m):
+    """efd_hann_loglike_local (the windowed logL in its per-bin form, reduced inside the inverse
+    column pass from the differenced correction) against efd_hann_loglike (the mirror-pair form
+    after the transforms) on the same rows and d, w (the same weight on both channels), rows of
+    different supports and an all-zero row: 1e-11 relative (the correction's float rounding,
+    ~1e-7 of a term ~1e-6 of max|S|, and the channel recombination). Its emit mode against
+    HannConvolution's own windowed spectrum (the plain pipeline, complex128 stencil) times the
+    weight, every bin (the wrapped bin nf-1 - first and the mirror layout included): within
+    2^-23 ln(n) / (n - 1) + 1e-14 of max|S| max w (tol_pol above); and the emitted data's logL
+    against the same spectrum is exactly 0."""
+    from emri_frequencydomainwaveforms_amd import _lib
+    from emri_frequencydomainwaveforms_amd.fdutils import HannConvolution
+    lib = _lib.load()
+    k0 = (n - 1) // 2
+    nb = n - k0
+    rng = np.random.default_rng(n % 997)
+    rows = 3
+    S = torch.zeros((rows, n), dtype=torch.complex128, device="cuda")
+    for r, (a, b) in enumerate([(0.45, 0.55), (0.43, 0.56)]):
+        lo_, hi_ = int(a * n), int(b * n)
+        S[r, lo_:hi_] = torch.complex(torch.randn(hi_ - lo_, dtype=torch.float64, device="cuda"),
+                                      torch.randn(hi_ - lo_, dtype=torch.float64,
+                                                  device="cuda")) * 1e-21
+    d = torch.as_tensor((rng.normal(size=(2, nb)) + 1j * rng.normal(size=(2, nb))) * 1e-20,
+                        device="cuda")
+    w1 = rng.uniform(0.5, 2.0, size=nb)
+    w1[0] = 0.0                                  # a masked bin (the likelihood's start_ind)
+    w = torch.as_tensor(np.stack([w1, w1]), device="cuda")
+    hcv = HannConvolution(n, S.device)
+    assert hcv.local_ok(d, w, k0)
+    assert not hcv.local_ok(d, torch.as_tensor(np.stack([w1, w1 * 1.5]), device="cuda"), k0)
+    local = hcv.local_data(d, w, k0)
+    assert local[2] == k0                        # odd grid: k0 is its own mirror
+    out = torch.empty(rows, dtype=torch.float64, device="cuda")
+    scr = torch.empty(rows * _lib.EFD_HANN_LOCAL_PARTIALS, dtype=torch.float64, device="cuda")
+    assert hcv.loglike_local(S, local, out, scr, lib)
+    assert lib.efd_hann_loglike_local_partials(m) <= _lib.EFD_HANN_LOCAL_PARTIALS
+    ref = torch.empty(rows, dtype=torch.float64, device="cuda")
+    scr2 = torch.empty(rows * _lib.EFD_LOGLIKE_SCRATCH, dtype=torch.float64, device="cuda")
+    hcv.loglike_batch(S, d, w, k0, ref, scr2, lib)
+    _, _, mm = hcv.transform(S, lib)
+    assert mm == m
+    np.testing.assert_allclose(out.cpu().numpy(), ref.cpu().numpy(), rtol=1e-11, atol=0.0)
+    # emit: wl S_w per bin, against the plain pipeline's windowed spectrum
+    tol = 2.0 ** -23 * np.log(n) / (n - 1) + 1e-14
+    wl, kself = local[1], local[2]
+    for r in range(2):
+        row = S[r:r + 1].contiguous()
+        e = hcv.local_emit(row, wl, kself, lib)
+        Sw = hcv(row)[0]
+        mx = float(row.abs().max()) * float(wl.max())
+        assert float((e[:n] - wl * Sw).abs().max()) <= tol * mx
+        assert complex(e[n]) == complex(e[kself])
+        zero = torch.empty(1, dtype=torch.float64, device="cuda")
+        assert hcv.loglike_local(row, (e, wl, kself), zero, scr, lib)
+        assert float(zero[0]) == 0.0
 
 
 @pytest.mark.parametrize("n,support,rows,m", [

@@ -10,6 +10,7 @@ how long the main thread waited) are recorded. Per call: wall ms, the pool's bus
 thread's waits, and recomputed misses. One JSON line per call, then a summary line.
 """
 
+import gc
 import json
 import os
 import sys
@@ -25,8 +26,20 @@ sys.path.insert(0, ROOT)
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "config5"
     calls = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    gc.callbacks.append(_gc_cb)
     for w in which.split(","):   # several in one process (tools/configs.py's order)
         trace(w, calls)
+
+
+GC = []       # (generation, seconds) of every collection
+_gc_t0 = [0.0]
+
+
+def _gc_cb(phase, info):
+    if phase == "start":
+        _gc_t0[0] = time.perf_counter()
+    else:
+        GC.append((info["generation"], time.perf_counter() - _gc_t0[0]))
 
 
 def trace(which, calls):
@@ -62,8 +75,13 @@ def trace(which, calls):
         like.get_ll(walkers, **kw)
     torch.cuda.synchronize()
     out = []
+    if os.environ.get("TRACE_GC_FREEZE"):
+        gc.freeze()
+    print(json.dumps({"setup": which, "gc_tracked_objects": len(gc.get_objects()),
+                      "gc_frozen": gc.get_freeze_count(), "gc_counts": gc.get_count()}), flush=True)
     for c in range(calls):
         rec.clear()
+        GC.clear()
         t0 = time.perf_counter()
         like.get_ll(walkers, **kw)
         torch.cuda.synchronize()
@@ -79,7 +97,8 @@ def trace(which, calls):
                 "recomputed_on_main": len(main_ups),
                 "main_wait_in_prepare_ms": 1e3 * sum(r[3] - r[2] for r in preps),
                 "last_upstream_end_ms": 1e3 * (max(r[3] for r in ups) - t0) if ups else None,
-                "first_prepare_ms": 1e3 * (min(r[2] for r in preps) - t0) if preps else None}
+                "first_prepare_ms": 1e3 * (min(r[2] for r in preps) - t0) if preps else None,
+                "gc": [[g, round(1e3 * d, 3)] for g, d in GC]}
         out.append(line)
         print(json.dumps(line), flush=True)
     w = [x["wall_ms"] for x in out]

@@ -40,6 +40,7 @@ sys.path.insert(0, ROOT)
 
 SUM_KW = dict(pad_output=True, output_type="fd", odd_len=True)
 NO_CPU = False       # --no-cpu-baseline
+HANN_PAIR = False    # --hann-pair: the windowed logL in its mirror-pair form (efd_hann_loglike)
 CPU_SECONDS = 8.0    # --cpu-seconds: the host twin's time budget per configuration
 # injection angles of emri_pe.py:603-617 (qS, phiS, qK, phiK) and dist = 2.4539 Gpc (:612)
 ANGLES = dict(dist=2.4539, qS=0.2, phiS=0.2, qK=0.8, phiK=0.8)
@@ -268,6 +269,8 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
     windowed = like.template_model.window is not None
     like.num_streams = slots
     like.fused_likelihood = fused
+    if HANN_PAIR:
+        like.HANN_LOCAL = False
     if group:
         like.FUSED_GROUP = group
     if os.environ.get("FUSED_DEPTH"):
@@ -279,11 +282,15 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
     for _ in range(3):
         ll = like.get_ll(walkers, **kw)
     _sync()
-    t0 = time.perf_counter()
+    # per-call times (get_ll returns host values: each call ends synchronised); the API rate is
+    # their median, with the spread reported beside it
+    calls = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         ll = like.get_ll(walkers, **kw)
+        calls.append(time.perf_counter() - t0)
     _sync()
-    api = (time.perf_counter() - t0) / reps
+    api = float(np.median(calls))
     cache = PrepareCache(few.waveform_generator)
     like.get_ll(walkers, **kw)
     _sync()
@@ -303,6 +310,7 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
     return {"config": name, "walkers_per_half_step": B, "N_pos": nbins, "cpu_baseline": cpu,
             "device_loglikes_per_s": B / dev, "device_ms_per_half_step": dev * 1e3,
             "api_loglikes_per_s": B / api, "api_ms_per_half_step": api * 1e3,
+            "api_ms_per_call_min_max": [min(calls) * 1e3, max(calls) * 1e3],
             "host_upstream_ms_per_walker": cache.host_s / B * 1e3,
             "ll_truth": float(ll[0]), "ll_min": float(np.min(ll)),
             "ll_bitwise_repeatable": bool(np.array_equal(ll, ll2)), "streams": slots,
@@ -337,9 +345,12 @@ def main():
                     "(Likelihood.FUSED_GROUP; 0 = its default)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the host twin rates")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--hann-pair", action="store_true", help="windowed config: the logL in "
+                    "its mirror-pair form after the transforms (efd_hann_loglike) instead of "
+                    "the per-bin form reduced inside them (efd_hann_loglike_local)")
     args = ap.parse_args()
-    global NO_CPU, CPU_SECONDS
-    NO_CPU, CPU_SECONDS = args.no_cpu_baseline, args.cpu_seconds
+    global NO_CPU, CPU_SECONDS, HANN_PAIR
+    NO_CPU, CPU_SECONDS, HANN_PAIR = args.no_cpu_baseline, args.cpu_seconds, args.hann_pair
     which = set(args.only.split(","))
     out = []
     if "1" in which:
