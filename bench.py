@@ -512,11 +512,11 @@ def main():
                            fS=None if overlap else torch.view_as_real(
                                torch.empty(nf, dtype=torch.complex128, device=dev))))
         slots.append(dict(wf=wf, prep_done=torch.cuda.Event(), sum_done=None))
+    lib = slots[0]["wf"][0]["eng"].lib
     s_prep = torch.cuda.Stream(dev, priority=args.prep_priority)
     s_sums = [torch.cuda.Stream(dev, priority=args.sum_priority)
               for _ in range(max(1, args.sum_streams))] if overlap else [s_prep]
     s_sum = s_sums[0]
-    lib = slots[0]["wf"][0]["eng"].lib
 
     def step(i, ev=None):
         sl = slots[i % len(slots)]

@@ -5166,6 +5166,85 @@ __global__ __launch_bounds__(256) void k_hann_loglike_partial(
 // Workgroups: 1-D, b -> XCD b mod 8; XCD x takes column blocks [x G/8, (x+1) G/8) and on it the
 // rows of one column block are consecutive, so dl / wl (24 B a bin, the same for every row) come
 // from HBM once and from the XCD's L2 for the other rows. part[row * G + column block], halved.
+// one element of the fused logL: bin offset u >= 0 from the row's first bin, its differenced
+// correction dvf (the transform's output), its prefetched data dv and weight w
+struct HannLl {
+    const double2* Sr;   // the row of S
+    int nfi, first, len;
+    double cc, scale;    // e / 4 times the row's scale (NaN: aliased row); the scale
+    double2 kfix;
+    const double2* dl;
+    int64_t kself, nf;
+    double2* emit;
+};
+__device__ __forceinline__ void hann_ll_elem(const HannLl& x, int u, fcv dvf, double2 dv, double w,
+                                             double& acc) {
+#pragma clang fp contract(off)
+    const double2 z = make_double2(0.0, 0.0);
+    double dx = (double)dvf.x, dy = (double)dvf.y;
+    if (u == x.nfi - 1 && x.len > 0) {   // the +1 neighbour wraps: Y[0] -> C(u = 0)
+        const double inv = 1.0 / x.scale;
+        const double2 s0 = x.Sr[x.first];
+        const double yx = s0.x * inv, yy = s0.y * inv;
+        dx += yx * x.kfix.x - yy * x.kfix.y;
+        dy += yx * x.kfix.y + yy * x.kfix.x;
+    }
+    int k = u + x.first;
+    k -= k >= x.nfi ? x.nfi : 0;
+    const int kp = k + 1 < x.nfi ? k + 1 : 0, km = k > 0 ? k - 1 : x.nfi - 1;
+    const int qp = u + 1 < x.nfi ? u + 1 : 0, qm = u > 0 ? u - 1 : x.nfi - 1;
+    const double2 s = u < x.len ? x.Sr[k] : z, sp = qp < x.len ? x.Sr[kp] : z,
+                  sn = qm < x.len ? x.Sr[km] : z;
+    const double wx = 0.5 * s.x - 0.25 * (sp.x + sn.x) - x.cc * dx;
+    const double wy = 0.5 * s.y - 0.25 * (sp.y + sn.y) - x.cc * dy;
+    if (x.emit != nullptr) {
+        const double2 o = make_double2(wx * w, wy * w);
+        x.emit[k] = o;
+        if (k == x.kself) x.emit[x.nf] = o;
+        return;
+    }
+    const double rx = dv.x - wx * w, ry = dv.y - wy * w;
+    acc = fma(rx, rx, fma(ry, ry, acc));
+    if (k == x.kself) {
+        const double2 d2 = x.dl[x.nf];
+        const double tx = d2.x - wx * w, ty = d2.y - wy * w;
+        acc = fma(tx, tx, fma(ty, ty, acc));
+    }
+}
+// the row's context (hann_row) for hann_ll_elem
+__device__ __forceinline__ HannLl hann_ll_ctx(const double2* S, int64_t stride,
+                                              const uint64_t* info, int row, int64_t M,
+                                              int64_t nf, const double2* dl, int64_t kself,
+                                              double2 kfix, double2* emit) {
+    const HannRow h = hann_row(info, row);
+    HannLl x;
+    x.Sr = S + (int64_t)row * stride;
+    x.nfi = (int)nf;
+    x.first = (int)h.first;
+    x.len = (int)h.len;
+    // a support longer than m - nf leaves Y[m - nf - 1] aliased: the row's logL is NaN
+    x.cc = h.len > M - nf ? __longlong_as_double(0x7ff8000000000000ll)
+                          : h.scale / (4.0 * (double)(nf - 1));
+    x.scale = h.scale;
+    x.kfix = kfix;
+    x.dl = dl;
+    x.kself = kself;
+    x.nf = nf;
+    x.emit = emit;
+    return x;
+}
+// the workgroup's partial (wave butterflies, then the waves in order): part[row G + cb], halved
+__device__ __forceinline__ void hann_ll_store(double acc, double* red, double* part, int64_t at) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) t += red[wv];
+        part[at] = 0.5 * t;
+    }
+}
 template <int R, int C>
 __global__ __launch_bounds__(FC_NT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_fc_cols_ll(const double2* __restrict__ S, int64_t stride, const uint64_t* __restrict__ info,
@@ -5198,18 +5277,12 @@ void k_fc_cols_ll(const double2* __restrict__ S, int64_t stride, const uint64_t*
     }
     __syncthreads();
     fc_fft<1, R, LOGL>(sm, idx);
-    const HannRow h = hann_row(info, row);
-    const int64_t off = M - nf;
-    // a support longer than m - nf leaves Y[m - nf - 1] aliased: the row's logL is NaN
-    const double cc = h.len > off ? __longlong_as_double(0x7ff8000000000000ll)
-                                  : h.scale / (4.0 * (double)(nf - 1));
-    const double2* Sr = S + (int64_t)row * stride;
-    const double2 z = make_double2(0.0, 0.0);
+    const HannLl x = hann_ll_ctx(S, stride, info, row, M, nf, dl, kself, kfix, emit);
+    const int offi = (int)(M - nf);
     // the elements' data (dl, wl) requested QH at a time before any of them is used: QH loads
     // of each in flight per thread (the epilogue is latency-bound otherwise, one round trip per
     // few elements; all 16 at once spill past 128 VGPRs); indices fit 32 bits (nf < 2^31,
     // m <= 2^25)
-    const int nfi = (int)nf, offi = (int)off, first = (int)h.first, len = (int)h.len;
     constexpr int QH = NQ >= 8 ? 8 : NQ;
     static_assert(NQ % QH == 0, "whole rounds of prefetched elements");
     double acc = 0.0;
@@ -5221,9 +5294,9 @@ void k_fc_cols_ll(const double2* __restrict__ S, int64_t stride, const uint64_t*
         for (int t = 0; t < QH; ++t) {
             const int i = threadIdx.x + (q0 + t) * FC_NT;
             const int u = (i / NCOL) * C + c0 + i % NCOL - offi;
-            int k = u + first;
-            k -= k >= nfi ? nfi : 0;
-            dv[t] = z;
+            int k = u + x.first;
+            k -= k >= x.nfi ? x.nfi : 0;
+            dv[t] = make_double2(0.0, 0.0);
             wv[t] = 0.0;
             if (u >= 0) {
                 wv[t] = wl[k];
@@ -5235,51 +5308,11 @@ void k_fc_cols_ll(const double2* __restrict__ S, int64_t stride, const uint64_t*
             const int i = threadIdx.x + (q0 + t) * FC_NT;
             const int e = i / NCOL, j = i % NCOL;
             const int u = e * C + c0 + j - offi;   // the correction's bin offset from first
-            if (u < 0) continue;
-            const fcv dvf = sm[idx(j, e)];
-            double dx = (double)dvf.x, dy = (double)dvf.y;
-            if (u == nfi - 1 && len > 0) {   // the +1 neighbour wraps: Y[0] -> C(u = 0)
-                const double inv = 1.0 / h.scale;
-                const double2 s0 = Sr[first];
-                const double yx = s0.x * inv, yy = s0.y * inv;
-                dx += yx * kfix.x - yy * kfix.y;
-                dy += yx * kfix.y + yy * kfix.x;
-            }
-            int k = u + first;
-            k -= k >= nfi ? nfi : 0;
-            const int kp = k + 1 < nfi ? k + 1 : 0, km = k > 0 ? k - 1 : nfi - 1;
-            const int qp = u + 1 < nfi ? u + 1 : 0, qm = u > 0 ? u - 1 : nfi - 1;
-            const double2 s = u < len ? Sr[k] : z, sp = qp < len ? Sr[kp] : z,
-                          sn2 = qm < len ? Sr[km] : z;
-            const double wx = 0.5 * s.x - 0.25 * (sp.x + sn2.x) - cc * dx;
-            const double wy = 0.5 * s.y - 0.25 * (sp.y + sn2.y) - cc * dy;
-            const double w = wv[t];
-            if (emit != nullptr) {
-                const double2 o = make_double2(wx * w, wy * w);
-                emit[k] = o;
-                if (k == kself) emit[nf] = o;
-                continue;
-            }
-            const double rx = dv[t].x - wx * w, ry = dv[t].y - wy * w;
-            acc = fma(rx, rx, fma(ry, ry, acc));
-            if (k == kself) {
-                const double2 d2 = dl[nf];
-                const double tx = d2.x - wx * w, ty = d2.y - wy * w;
-                acc = fma(tx, tx, fma(ty, ty, acc));
-            }
+            if (u >= 0) hann_ll_elem(x, u, sm[idx(j, e)], dv[t], wv[t], acc);
         }
     }
     if (emit != nullptr) return;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-#pragma unroll
-        for (int wv = 0; wv < FC_NT / 64; ++wv) t += red[wv];
-        part[(int64_t)row * G + cb] = 0.5 * t;
-    }
+    hann_ll_store(acc, red, part, (int64_t)row * G + cb);
 }
 
 // fused log-likelihood partials: one workgroup per chunk, then a second pass

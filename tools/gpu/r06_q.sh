@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU box, round 6: the register-staged fused inverse (m = 2^24): parity, profile, paired rates.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=$1; O=gpurun_out/$TAG; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_windowed.py -k "local or test_sh" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 7; }
+bash tools/gpu/windowed_prof.sh $TAG || exit 6
+run() { timeout -k 10 300 "$@" >> $O/$NAME.jsonl 2>> $O/$NAME.err || { tail -20 $O/$NAME.err; exit 8; }; }
+for i in 1 2; do
+NAME=w_local; run python tools/configs.py --only w --reps 7 --no-cpu-baseline
+NAME=w_pair; run python tools/configs.py --only w --reps 7 --no-cpu-baseline --hann-pair
+done
+echo q done
