@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "efd_modesum_prepare_batch",
     "efd_modesum_status_batch",
     "efd_stage_batch",
+    "efd_fused_group",
     "efd_modesum_sum",
     "efd_modesum_sum_batch",
     "efd_modesum_sum_loglike",
@@ -205,6 +206,11 @@ def load(path=None):
         lib.efd_stage_batch.restype = ctypes.c_int
         lib.efd_stage_batch.argtypes = [vp, sz, ctypes.c_uint64, i32, vp, vp, vp,
                                         ctypes.POINTER(ModesumArgs), vp, ctypes.POINTER(sz)]
+    if hasattr(lib, "efd_fused_group"):
+        lib.efd_fused_group.restype = ctypes.c_int
+        lib.efd_fused_group.argtypes = [vp, sz, vp, sz, i32, vp, vp, vp,
+                                        ctypes.POINTER(ModesumArgs), vp, vp, vp, vp, vp, vp, vp,
+                                        vp, vp, ctypes.POINTER(sz)]
     if hasattr(lib, "efd_modesum_status_batch"):
         lib.efd_modesum_status_batch.restype = ctypes.c_int
         lib.efd_modesum_status_batch.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(i32), vp]

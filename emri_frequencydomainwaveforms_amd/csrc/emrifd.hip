@@ -5965,6 +5965,45 @@ int efd_modesum_sum_loglike_ex(const efd_modesum_args* const* a, void* const* wo
                           w, out, stream, tile_const);
 }
 
+// One walker group of the fused likelihood in one call (Likelihood.get_ll's per-group host
+// path, likelihood.py:246-274 callers): efd_stage_batch into pin, the copy to dbuf, staged_event
+// recorded after it (the pinned buffer's reuse waits on it), efd_modesum_prepare_batch and
+// efd_modesum_sum_loglike_ex in launches of EFD_BATCH_MAX walkers, all on `stream`: the five
+// ctypes transitions and the argument handling of the Python steps in one.
+int efd_fused_group(void* pin, size_t pin_bytes, void* dbuf, size_t dbuf_bytes, int32_t count,
+                    const uint64_t* src, const int32_t* shape, const double* scale,
+                    const efd_modesum_args* tmpl, efd_modesum_args* args,
+                    void* const* workspace, const size_t* workspace_bytes, const double* d,
+                    const double* w, const double* tile_const, double* out, void* staged_event,
+                    void* stream, size_t* total) {
+    if (count < 1 || !args || !workspace || !workspace_bytes || !d || !w || !out || !total)
+        return fail(EFD_ERR_ARG, "efd_fused_group: bad arguments");
+    const int rs = efd_stage_batch(pin, pin_bytes, (uint64_t)(uintptr_t)dbuf, count, src, shape,
+                                   scale, tmpl, args, total);
+    if (rs == EFD_ERR_WORKSPACE || (rs == EFD_OK && (!dbuf || *total > dbuf_bytes)))
+        return EFD_ERR_WORKSPACE;   // the caller grows pin / dbuf to *total and calls again
+    if (rs != EFD_OK) return fail(rs, "efd_fused_group: staging failed (efd_stage_batch)");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(dbuf, pin, *total, hipMemcpyHostToDevice, st));
+    if (staged_event) HIP_TRY(hipEventRecord((hipEvent_t)staged_event, st));
+    const efd_modesum_args* ap[EFD_BATCH_MAX];
+    for (int32_t c0 = 0; c0 < count; c0 += EFD_BATCH_MAX) {
+        const int32_t cnt = std::min<int32_t>(EFD_BATCH_MAX, count - c0);
+        for (int32_t i = 0; i < cnt; ++i) ap[i] = &args[c0 + i];
+        const int rc = efd_modesum_prepare_batch(ap, workspace + c0, workspace_bytes + c0, cnt,
+                                                 stream);
+        if (rc != EFD_OK) return rc;
+    }
+    for (int32_t c0 = 0; c0 < count; c0 += EFD_BATCH_MAX) {
+        const int32_t cnt = std::min<int32_t>(EFD_BATCH_MAX, count - c0);
+        for (int32_t i = 0; i < cnt; ++i) ap[i] = &args[c0 + i];
+        const int rc = efd_modesum_sum_loglike_ex(ap, workspace + c0, workspace_bytes + c0, cnt,
+                                                  d, w, tile_const, out + c0, stream);
+        if (rc != EFD_OK) return rc;
+    }
+    return EFD_OK;
+}
+
 int efd_modesum_status(const void* workspace, void* stream) {
     if (!workspace) return fail(EFD_ERR_ARG, "efd_modesum_status: NULL workspace");
     Header h{};

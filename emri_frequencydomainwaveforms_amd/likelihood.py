@@ -293,6 +293,9 @@ class Likelihood:
     # tools/chain_timeline.py), and the groups' sums need no common stream (each writes its own
     # slice of out); the streams join once, before the copy out. False: round 3's sum stream.
     FUSED_SUM_OWN_STREAM = os.environ.get("EFD_SUM_STREAM", "0") != "1"
+    # a group's staging, upload, preparation and fused sum in one native call
+    # (BatchPreparer.flush_loglike, efd_fused_group); False: the Python steps of round 5
+    FUSED_NATIVE_GROUP = True
 
     def _get_ll_fused(self, tm, params, args, kwargs, out):
         """The pipelined path with the likelihood fused into the mode sum: per group of
@@ -353,6 +356,7 @@ class Likelihood:
         if pin is None or pin.numel() < n:
             pin = F["pin"] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
         own = self.FUSED_SUM_OWN_STREAM
+        native = self.FUSED_NATIVE_GROUP and hasattr(lib, "efd_fused_group")
         used = []
         try:
             batch = getattr(tm, "submit_batch", None)
@@ -363,6 +367,17 @@ class Likelihood:
                     for i in range(g0, min(n, g0 + G)):
                         tm.submit(B, None, *params[i], *args, order=False, prepare_only=True,
                                   **kwargs)
+                if own and native:
+                    # the group's staging, upload, preparation and fused sum in one native call
+                    # on the group's stream (efd_fused_group), the tile constants made on it
+                    # first (once per grid)
+                    p0 = B._pending[0]
+                    sst = B.groups[B._next]["stream"]
+                    tc = self._tile_constants({"freq": p0[1], "k0": p0[4]}, sst, F)
+                    m = len(B._pending)
+                    used.append(B.flush_loglike(self._d, self._w_templ, out[g0:g0 + m],
+                                                tile_const=tc))
+                    continue
                 gi, jobs = B.flush()
                 used.append(gi)
                 if own:

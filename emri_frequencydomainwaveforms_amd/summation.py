@@ -628,7 +628,7 @@ class BatchPreparer:
         self.lib = self.groups[0]["engines"][0].lib
         self._next = 0
         self._pending = []
-        self.last_jobs = []
+        self._jobs = []      # the last flush()'s (engine, job) pairs (last_jobs)
 
     # -- the WaveformPipeline surface the template chain uses ---------------------------------
     def next_slot(self):
@@ -679,14 +679,7 @@ class BatchPreparer:
             G["pin_done"].synchronize()     # the group's previous copy out of the pinned buffer
         n = len(pend)
         if "args" not in G:
-            A = G["args"] = (_lib.ModesumArgs * self.group)()
-            size = ctypes.sizeof(_lib.ModesumArgs)
-            base = ctypes.addressof(A)
-            G["pa"] = ctypes.cast((ctypes.c_void_p * self.group)(
-                *[base + i * size for i in range(self.group)]),
-                ctypes.POINTER(ctypes.POINTER(_lib.ModesumArgs)))
-            G["pw"] = (ctypes.c_void_p * self.group)()
-            G["pb"] = (ctypes.c_size_t * self.group)()
+            self.flush_setup(G)
         freq = pend[0][1]
         nf = int(freq.numel())
         for _, f, sym, _, k0, acc in pend:
@@ -789,8 +782,157 @@ class BatchPreparer:
             T["prepare_batch"] = T.get("prepare_batch", 0.0) + time.perf_counter() - t_4
         G["used"] = True
         G["n"] = n
-        self.last_jobs = jobs
+        self._jobs, self._last = jobs, None
         return gi, jobs
+
+    def flush_loglike(self, d, w, out, tile_const=None):
+        """flush() and sum_loglike() of the collected walkers in one native call
+        (efd_fused_group: staging, upload, the staged event, the preparation and the fused sum
+        on the next group's stream); returns the group index. The fused likelihood's per-group
+        host path (Likelihood._get_ll_fused): the same launches on the same stream as flush()
+        then sum_loglike(gi, ..., G's stream), bitwise the same logL, in one ctypes
+        transition instead of five. d, w: checked once per (d, w) pair."""
+        import ctypes
+        torch = _torch()
+        pend, self._pending = self._pending, []
+        if not pend:
+            raise ValueError("flush_loglike: nothing submitted")
+        gi = self._next
+        self._next = (gi + 1) % len(self.groups)
+        G = self.groups[gi]
+        st = G["stream"]
+        if G["busy"] is not None:
+            st.wait_event(G["busy"])        # the group's last sum has read its workspaces
+        if G["pin_done"] is None:
+            G["pin_done"] = torch.cuda.Event()
+            G["pin_done"].record(st)        # (the native call re-records its handle)
+        G["pin_done"].synchronize()         # the group's previous copy out of the pinned buffer
+        n = len(pend)
+        if "args" not in G:
+            self.flush_setup(G)
+        freq = pend[0][1]
+        nf = int(freq.numel())
+        for _, f, sym, _, k0, acc in pend:
+            if f is not freq and (int(f.numel()) != nf or f.data_ptr() != freq.data_ptr()):
+                raise ValueError("flush: the walkers of a group share one frequency grid")
+        _, _, sym, _, k0, acc = pend[0]
+        if any(p[2] != sym or p[4] != k0 or p[5] != acc for p in pend):
+            raise ValueError("flush: grid symmetry, k0 and accumulate must agree in a group")
+        key = (id(d), id(w), nf - k0)
+        if self._ll_checked != key:
+            _check_ll_io(torch, d, w, out, nf - k0, n)
+            self._ll_checked = key
+        elif out.dtype != torch.float64 or out.numel() < n or not out.is_contiguous():
+            raise ValueError(f"flush_loglike: out float64 [>= {n}], contiguous")
+        tmpl = _lib.ModesumArgs(freq=freq.data_ptr(), nf=nf, grid_symmetric=1 if sym else 0,
+                                caustic=CAUSTIC_MODES[self.caustic],
+                                accumulate=1 if acc else 0, k0=k0)
+        src, shape, scale, keep = self._sources(pend)
+        pw, pb, engines = G["pw"], G["pb"], G["engines"]
+        dev = freq.device
+        for i, (nt_i, K_i) in enumerate(shape.tolist()):
+            eng = engines[i]
+            nbytes = _WS_BYTES.get((nt_i, K_i, nf))
+            if nbytes is None or eng._ws is None or eng._ws_cap < nbytes or eng._ws_dev != dev:
+                eng._workspace(nt_i, K_i, nf, dev, stream=st)   # sized, or grown, here
+            pw[i] = eng._ws_ptr
+            pb[i] = eng._ws_cap
+            eng._last_args = G["A_i"][i]
+        total = ctypes.c_size_t(0)
+        dp, wp = torch.view_as_real(d).data_ptr(), w.data_ptr()
+        tcp = tile_const.data_ptr() if tile_const is not None else None
+        for attempt in range(2):
+            pin, dbuf = G["pin"], G["dbuf"]
+            rc = self.lib.efd_fused_group(
+                pin.data_ptr() if pin is not None else None, pin.numel() if pin is not None else 0,
+                dbuf.data_ptr() if dbuf is not None else None,
+                dbuf.numel() if dbuf is not None else 0, n, src.ctypes.data, shape.ctypes.data,
+                scale.ctypes.data, ctypes.byref(tmpl), G["args_ptr"], G["pw_ptr"], G["pb_ptr"],
+                dp, wp, tcp, out.data_ptr(), G["pin_done"].cuda_event, st.cuda_stream,
+                ctypes.byref(total))
+            if rc == _lib.EFD_OK:
+                break
+            if rc != _lib.EFD_ERR_WORKSPACE or attempt == 1:
+                raise _lib.EFDError(f"efd_fused_group: {_lib.last_error(self.lib)} ({rc})")
+            cap = max(2 * total.value, 1 << 20)
+            if pin is None or pin.numel() < total.value:
+                G["pin"] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            if dbuf is None or dbuf.numel() < total.value:
+                with torch.cuda.stream(st):
+                    G["dbuf"] = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        del keep
+        G["used"] = True
+        G["n"] = n
+        self._last = (gi, n, freq, k0, sym)
+        return gi
+
+    _ll_checked = None
+    _last = None
+
+    @property
+    def last_jobs(self):
+        """(engine, job) of the last flush()'s or flush_loglike()'s walkers (made on demand)."""
+        if self._last is None:
+            return self._jobs
+        gi, n, freq, k0, sym = self._last
+        G = self.groups[gi]
+        return [(G["engines"][i], {"freq": freq, "k0": k0, "grid_symmetric": sym,
+                                   "_args": G["A_i"][i]}) for i in range(n)]
+
+    def flush_setup(self, G):
+        """A group's argument array, its pointer table and the workspace pointer / size arrays
+        (made once per group)."""
+        import ctypes
+        A = G["args"] = (_lib.ModesumArgs * self.group)()
+        size = ctypes.sizeof(_lib.ModesumArgs)
+        base = ctypes.addressof(A)
+        G["pa"] = ctypes.cast((ctypes.c_void_p * self.group)(
+            *[base + i * size for i in range(self.group)]),
+            ctypes.POINTER(ctypes.POINTER(_lib.ModesumArgs)))
+        G["pw"] = (ctypes.c_void_p * self.group)()
+        G["pb"] = (ctypes.c_size_t * self.group)()
+        G["args_ptr"] = base
+        G["pw_ptr"] = ctypes.addressof(G["pw"])
+        G["pb_ptr"] = ctypes.addressof(G["pb"])
+        G["A_i"] = [A[i] for i in range(self.group)]
+
+    @staticmethod
+    def _sources(pend):
+        """(src, shape, scale, keep) of efd_stage_batch for the pending walkers: the native
+        upstream's packed addresses joined, or each walker's arrays converted (kept alive in
+        keep until the staging copy)."""
+        n = len(pend)
+        keep = []
+        fast = [p[0].get("_src") for p in pend]
+        scale = np.array([p[3] for p in pend], dtype=np.complex128).view(np.float64)
+        if None not in fast:
+            src = np.frombuffer(b"".join(fast), dtype=np.uint64)
+            shape = np.frombuffer(b"".join([p[0]["_shape"] for p in pend]),
+                                  dtype=np.int32).reshape(n, 2)
+            return src, shape, scale, keep
+        src = np.empty((n, 10), dtype=np.uint64)
+        shape = np.empty((n, 2), dtype=np.int32)
+        for i, (host, _, _, _, _, _) in enumerate(pend):
+            if fast[i] is not None:
+                src[i] = np.frombuffer(fast[i], dtype=np.uint64)
+                shape[i] = np.frombuffer(host["_shape"], dtype=np.int32)
+                continue
+            amps = np.ascontiguousarray(host["amp"], dtype=np.complex128)
+            nt, K = amps.shape
+            arrays = [np.ascontiguousarray(host[k], dtype=_F64)
+                      for k in ("t", "phi_phi", "phi_r", "f_phi", "f_r")]
+            arrays += [amps, np.ascontiguousarray(host["m"], dtype=_I32),
+                       np.ascontiguousarray(host["n"], dtype=_I32),
+                       np.ascontiguousarray(host["ylm_p"], dtype=np.complex128),
+                       np.ascontiguousarray(host["ylm_m"], dtype=np.complex128)]
+            if any(a.size != nt for a in arrays[:5]):
+                raise ValueError("trajectory arrays and amplitudes must share N_t")
+            if any(a.size != K for a in arrays[6:]):
+                raise ValueError("m, n, ylm_p, ylm_m must have K entries")
+            keep.append(arrays)
+            src[i] = [a.ctypes.data for a in arrays]
+            shape[i] = (nt, K)
+        return src, shape, scale, keep
 
     def sum_loglike(self, gi, d, w, out, stream, tile_const=None):
         """efd_modesum_sum_loglike(_ex) over group gi's last flush (its argument and workspace

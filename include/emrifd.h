@@ -469,6 +469,23 @@ int efd_stage_batch(void* pin, size_t pin_bytes, uint64_t dev_base, int32_t coun
                     const uint64_t* src, const int32_t* shape, const double* scale,
                     const efd_modesum_args* tmpl, efd_modesum_args* args, size_t* total);
 
+/*
+ * One walker group of the fused likelihood in one call: efd_stage_batch(pin, pin_bytes, dbuf,
+ * count, src, shape, scale, tmpl, args, total), the host-to-device copy of pin to dbuf on
+ * `stream`, staged_event (a hipEvent_t, or NULL) recorded after it, then
+ * efd_modesum_prepare_batch and efd_modesum_sum_loglike_ex(args, workspace, workspace_bytes,
+ * d, w, tile_const, out) in launches of EFD_BATCH_MAX walkers on `stream`. EFD_ERR_WORKSPACE
+ * with *total set and nothing queued when pin or dbuf is shorter than *total. Not part of the
+ * reference's interface: Likelihood.get_ll's per-group host steps (likelihood.py:246-274
+ * callers) in one native call.
+ */
+int efd_fused_group(void* pin, size_t pin_bytes, void* dbuf, size_t dbuf_bytes, int32_t count,
+                    const uint64_t* src, const int32_t* shape, const double* scale,
+                    const efd_modesum_args* tmpl, efd_modesum_args* args,
+                    void* const* workspace, const size_t* workspace_bytes, const double* d,
+                    const double* w, const double* tile_const, double* out, void* staged_event,
+                    void* stream, size_t* total);
+
 #ifdef __cplusplus
 }
 #endif

@@ -175,26 +175,30 @@ def test_fused_likelihood_many_walkers(setup):
         sum_batch_loglike(bad, like._d, like._w_templ, out)
     # a failure inside the second group's flush, after its upload and preparation are queued:
     # get_ll raises only once every group stream is idle, and the next call is unaffected
+    # (both host paths: one native call per group, flush_loglike, and the Python steps, flush)
     like.fused_likelihood = True
     Bp = like._fused["prep"]
-    orig, seen = Bp.flush, []
+    for native, name in ((True, "flush_loglike"), (False, "flush")):
+        like.FUSED_NATIVE_GROUP = native
+        orig, seen = getattr(Bp, name), []
 
-    def flaky():
-        r = orig()
-        seen.append(r[0])
-        if len(seen) == 2:
-            raise RuntimeError("injected flush failure")
-        return r
+        def flaky(*a, **k):
+            r = orig(*a, **k)
+            seen.append(r if native else r[0])
+            if len(seen) == 2:
+                raise RuntimeError("injected flush failure")
+            return r
 
-    Bp.flush = flaky
-    try:
-        with pytest.raises(RuntimeError, match="injected"):
-            like.get_ll(walkers, **kw)
-        assert len(seen) == 2 and seen[0] != seen[1]
-        assert all(g["stream"].query() for g in Bp.groups)
-    finally:
-        del Bp.flush
-    np.testing.assert_array_equal(like.get_ll(walkers, **kw), llf)
+        setattr(Bp, name, flaky)
+        try:
+            with pytest.raises(RuntimeError, match="injected"):
+                like.get_ll(walkers, **kw)
+            assert len(seen) == 2 and seen[0] != seen[1]
+            assert all(g["stream"].query() for g in Bp.groups)
+        finally:
+            delattr(Bp, name)
+            del like.FUSED_NATIVE_GROUP
+        np.testing.assert_array_equal(like.get_ll(walkers, **kw), llf)
 
 
 def test_fused_likelihood_large_group(setup):

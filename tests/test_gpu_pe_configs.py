@@ -104,6 +104,14 @@ def _run(s, name, half_steps=2):
     like.fused_likelihood = True
     llf = np.concatenate([like(b, **s.kwargs) for b in batches])
     assert np.array_equal(np.concatenate([like(b, **s.kwargs) for b in batches]), llf)
+    # the group's host steps in Python (round 5) against the one native call per group
+    # (efd_fused_group): the same launches on the same streams, bitwise the same logL
+    like.FUSED_NATIVE_GROUP = False
+    try:
+        llp = np.concatenate([like(b, **s.kwargs) for b in batches])
+    finally:
+        del like.FUSED_NATIVE_GROUP
+    assert np.array_equal(llp, llf)
     like.fused_likelihood = False
     llu = np.concatenate([like(b, **s.kwargs) for b in batches])
     like.fused_likelihood = True

@@ -41,6 +41,7 @@ sys.path.insert(0, ROOT)
 SUM_KW = dict(pad_output=True, output_type="fd", odd_len=True)
 NO_CPU = False       # --no-cpu-baseline
 HANN_PAIR = False    # --hann-pair: the windowed logL in its mirror-pair form (efd_hann_loglike)
+PY_GROUPS = False    # --python-groups: the fused groups' host steps in Python (round 5)
 CPU_SECONDS = 8.0    # --cpu-seconds: the host twin's time budget per configuration
 # injection angles of emri_pe.py:603-617 (qS, phiS, qK, phiK) and dist = 2.4539 Gpc (:612)
 ANGLES = dict(dist=2.4539, qS=0.2, phiS=0.2, qK=0.8, phiK=0.8)
@@ -271,6 +272,8 @@ def config_like(name, T, eps, downsample, nwalkers, reps, slots=4, fused=True, g
     like.fused_likelihood = fused
     if HANN_PAIR:
         like.HANN_LOCAL = False
+    if PY_GROUPS:
+        like.FUSED_NATIVE_GROUP = False
     if group:
         like.FUSED_GROUP = group
     if os.environ.get("FUSED_DEPTH"):
@@ -348,9 +351,13 @@ def main():
     ap.add_argument("--hann-pair", action="store_true", help="windowed config: the logL in "
                     "its mirror-pair form after the transforms (efd_hann_loglike) instead of "
                     "the per-bin form reduced inside them (efd_hann_loglike_local)")
+    ap.add_argument("--python-groups", action="store_true", help="configs 4, 5: each fused "
+                    "group's staging and launches as Python steps instead of one native call "
+                    "(efd_fused_group)")
     args = ap.parse_args()
-    global NO_CPU, CPU_SECONDS, HANN_PAIR
+    global NO_CPU, CPU_SECONDS, HANN_PAIR, PY_GROUPS
     NO_CPU, CPU_SECONDS, HANN_PAIR = args.no_cpu_baseline, args.cpu_seconds, args.hann_pair
+    PY_GROUPS = args.python_groups
     which = set(args.only.split(","))
     out = []
     if "1" in which:

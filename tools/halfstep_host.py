@@ -1,6 +1,8 @@
 """Host time of one fused-likelihood half-step by phase (config 4 / 5, memoised upstream).
 
-    python tools/halfstep_host.py config4|config5
+    python tools/halfstep_host.py config4|config5 [python]
+
+("python": the groups' host steps in Python, Likelihood.FUSED_NATIVE_GROUP = False)
 
 Runs bench.py's likelihood setup (pe.setup) with a copy of Likelihood._get_ll_fused that adds
 timers between its phases (grid check and prefetch, stream setup, submit_batch, flush,
@@ -14,6 +16,8 @@ import bench
 from emri_frequencydomainwaveforms_amd import pe, likelihood as L
 from emri_frequencydomainwaveforms_amd.summation import BatchPreparer
 cfg = bench.LIKE_CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "config5"]
+if "python" in sys.argv[2:]:
+    L.Likelihood.FUSED_NATIVE_GROUP = False
 s = pe.setup(**cfg)
 batches = s.half_steps()
 memo = pe.MemoizedUpstream(s.few.waveform_generator)
@@ -59,6 +63,15 @@ def fused(self, tm, params, args, kwargs, out):
         ta = pc()
         batch(B, params[g0:g0 + G], *args, **kwargs)
         tb = pc(); acc["submit_batch"] += tb - ta
+        if self.FUSED_NATIVE_GROUP:
+            # one native call per group (efd_fused_group), as Likelihood._get_ll_fused
+            p0 = B._pending[0]
+            sst = B.groups[B._next]["stream"]
+            tcon = self._tile_constants({"freq": p0[1], "k0": p0[4]}, sst, F)
+            used.append(B.flush_loglike(self._d, self._w_templ, out[g0:g0 + len(B._pending)],
+                                        tile_const=tcon))
+            acc["flush+sum (native)"] += pc() - tb
+            continue
         gi, jobs = B.flush()
         used.append(gi)
         tc = pc(); acc["flush"] += tc - tb
