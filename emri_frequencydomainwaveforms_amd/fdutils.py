@@ -332,8 +332,15 @@ class HannConvolution:
         layout): dl complex128 [n + 1] with d0 - i d1 at each kept bin k, conj(d0 + i d1) at its
         mirror n-1-k (at dl[n] when the mirror is k itself, kself = k), wl float64 [n] the
         weight at both; bins neither kept nor mirrored hold 0 (no term)."""
-        torch = require_gpu()
-        n, k0 = self.n, int(k0)
+        require_gpu()
+        return self.local_layout(self.n, d, w, k0)
+
+    @staticmethod
+    def local_layout(n, d, w, k0):
+        """local_data's arithmetic for a grid of n bins, on d's device (any torch device: the
+        CPU tests pin the layout and the recombination identity with it)."""
+        import torch
+        n, k0 = int(n), int(k0)
         dev = d.device
         dl = torch.zeros(n + 1, dtype=torch.complex128, device=dev)
         wl = torch.zeros(n, dtype=torch.float64, device=dev)
