@@ -823,6 +823,15 @@ __device__ __forceinline__ double4 group_amp_at(const double* __restrict__ amp,
     return group_amp_sum(amp, ylm_p, ylm_m, sc_re, sc_im, gm[g] != 0, gstart[g], gstart[g + 1],
                          [&](int p) { return gmem[p]; }, K, i);
 }
+// the grids of k_items and k_group_amp at K >= ITEMS_SPLIT_K: K / ITEMS_PER_THREAD_K threads per
+// interval or knot, a thread taking every (K / ITEMS_PER_THREAD_K)-th of the G <= K (m, n) groups
+// (config 2's 3,020 harmonics form 627 groups: K-sized grids were ~80% workgroups that exit at
+// once, and each held a slot of the sum beside which the next batch is prepared; 1 -> 8:
+// +2.2% waveforms/s, r06v, within noise on a slower box, r06w)
+#ifndef ITEMS_PER_THREAD_K
+#define ITEMS_PER_THREAD_K 8
+#endif
+constexpr int ITEMS_SPLIT_K = 1024;
 __device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
                                                    const double* __restrict__ ylm_p,
                                                    const double* __restrict__ ylm_m, double sc_re,
@@ -831,12 +840,16 @@ __device__ __forceinline__ void group_amp_body(const double* __restrict__ amp,
                                                    const int32_t* __restrict__ gmem, int nt, int K,
                                                    const Header* __restrict__ hdr,
                                                    double* __restrict__ gamp) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    // (the grid covers K / ITEMS_PER_THREAD_K groups at large K: a thread may take several)
     const int i = blockIdx.y;
-    if (g >= hdr->groups || i >= nt) return;
-    const double4 v = group_amp_at(amp, ylm_p, ylm_m, sc_re, sc_im, gm, gstart, gmem, K, i, g);
-    double* o = gamp + (size_t)i * 4 * K + 4 * g;
-    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    const int G = hdr->groups;
+    if (i >= nt) return;
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+        const double4 v = group_amp_at(amp, ylm_p, ylm_m, sc_re, sc_im, gm, gstart, gmem, K, i,
+                                       g);
+        double* o = gamp + (size_t)i * 4 * K + 4 * g;
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
 }
 __global__ __launch_bounds__(256) void k_group_amp(const double* __restrict__ amp,
                                                    const double* __restrict__ ylm_p,
@@ -1507,20 +1520,26 @@ __device__ __forceinline__ void items_body(const double* __restrict__ t, const d
                         Header* __restrict__ hdr, bool runs_mark, bool env) {
     const int ni = nt - 1;
     const int G = hdr->groups;
-    // the grid is sized for K >= G groups: whole blocks past the records leave at once
-    if ((int64_t)blockIdx.x * blockDim.x >= (int64_t)ni * G) return;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the grid is sized for K >= G groups (K / ITEMS_PER_THREAD_K threads per interval at large
+    // K): whole blocks past the records leave at once; a thread takes the records gid, gid +
+    // the grid's threads, ... (config 2: 627 groups over 377 threads an interval, one or two)
+    const int64_t total = (int64_t)ni * G;
+    if ((int64_t)blockIdx.x * blockDim.x >= total) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     __shared__ unsigned long long red[3][4];
     unsigned long long ev = 0, contrib = 0, eev = 0;
-    if (gid < (int64_t)ni * G) {
+    for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+         gid += stride) {
         const int g = (int)(gid % G), j = (int)(gid / G);
         // the PCR inverse splines' run-overflow marker (rr[3]) into the header's sticky flag
         if (runs_mark && j == 0 && runs[(size_t)g * 4 * MAXRUNS + 3] != 0)
             atomicOr(&hdr->runs_overflow, 1);
+        unsigned long long e1 = 0;
         const bool envr = build_item(t, f_phi, f_r, gm, gn, ni, K, coefA, coefT, runs, freq, nf,
-                                     paired, nl, nl1, items, ranges, g, j, ev, env);
-        contrib = ev * (unsigned long long)(gstart[g + 1] - gstart[g]);
-        eev = envr ? ev : 0;
+                                     paired, nl, nl1, items, ranges, g, j, e1, env);
+        ev += e1;
+        contrib += e1 * (unsigned long long)(gstart[g + 1] - gstart[g]);
+        eev += envr ? e1 : 0;
     }
     for (int o = 32; o > 0; o >>= 1) {
         ev += __shfl_xor(ev, o);
@@ -5615,7 +5634,10 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
         ntmax = std::max(ntmax, ai->nt);
         Kmax = std::max(Kmax, ai->K);
         nimax = std::max(nimax, ai->nt - 1);
-        items_max = std::max(items_max, (int64_t)(ai->nt - 1) * ai->K);
+        // (G <= K groups; at large K each thread may take several records: config 2's 3,020
+        // harmonics form 627 groups, so a K-sized grid was 79% workgroups that exit at once)
+        const int64_t per = ai->K >= ITEMS_SPLIT_K ? ITEMS_PER_THREAD_K : 1;
+        items_max = std::max(items_max, ((int64_t)(ai->nt - 1) * ai->K + per - 1) / per);
         if (i == 0) {
             B.paired = paired;
             B.nf = ai->nf;
@@ -5637,8 +5659,9 @@ static int prepare_batch_impl(const char* fn, const efd_modesum_args* const* a,
             HIP_TRY(hipGetLastError());
         }
         if (any_thomas) {
-            hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax + 255) / 256, ntmax, nz), dim3(256), 0,
-                               st, B);
+            const int gper = Kmax >= ITEMS_SPLIT_K ? ITEMS_PER_THREAD_K : 1;
+            hipLaunchKernelGGL(k_group_amp_b, dim3((Kmax / gper + 255) / 256, ntmax, nz),
+                               dim3(256), 0, st, B);
             HIP_TRY(hipGetLastError());
         }
     }

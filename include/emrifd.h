@@ -347,7 +347,9 @@ int efd_hann_convolve(const double* S, int64_t stride, int64_t nf, int32_t rows,
  * (R = m / C; kfp's layout above with 8192 replaced by C): 16384 at m = 2^24, else 8192. */
 int efd_hann_four_step_cols(int64_t m);
 /* The windowed logL with the correction reduced inside efd_hann_convolve's inverse column pass
- * (no correction array written or read back). With the same weight w on both channels the two
+ * (no correction array written or read back): the reference's per-channel window convolution
+ * (FDutils.py:95-96 under emri_pe.py:259-263) followed by Likelihood.get_ll's reduction
+ * (likelihood.py:257-274), for a walker group. With the same weight w on both channels the two
  * channels' terms of a kept bin k and of its mirror k' = nf-1-k recombine into one term per bin:
  *   sum_k |d0 - w h+|^2 + |d1 - w hx|^2 = (1/2) sum_j |dl[j] - wl[j] S_w[j]|^2,
  * dl[k] = d0[k] - i d1[k], dl[k'] = conj(d0[k] + i d1[k]), wl = w at both (complex128 [nf + 1]
