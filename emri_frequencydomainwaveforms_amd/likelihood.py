@@ -287,7 +287,7 @@ class Likelihood:
     # 43-tile grids) ran 54-60 k logL/s in 4 groups against 40-51 k in 8 (5 interleaved rounds);
     # config 4's 8 walkers are one group either way (groups of 4 or 3: -5 to -10%)
     FUSED_GROUP = min(max(1, int(os.environ.get("EFD_FUSED_GROUP", "16"))), 64)
-    FUSED_DEPTH = 2
+    FUSED_DEPTH = max(1, int(os.environ.get("EFD_FUSED_DEPTH", "2")))
     # each group's sum on the group's own stream, right behind its preparation: no
     # cross-stream wait between the two (~12 us of idle device per group on config 4's chain,
     # tools/chain_timeline.py), and the groups' sums need no common stream (each writes its own
@@ -374,9 +374,8 @@ class Likelihood:
                     p0 = B._pending[0]
                     sst = B.groups[B._next]["stream"]
                     tc = self._tile_constants({"freq": p0[1], "k0": p0[4]}, sst, F)
-                    m = len(B._pending)
-                    used.append(B.flush_loglike(self._d, self._w_templ, out[g0:g0 + m],
-                                                tile_const=tc))
+                    used.append(B.flush_loglike(self._d, self._w_templ, out, tile_const=tc,
+                                                out_off=g0))
                     continue
                 gi, jobs = B.flush()
                 used.append(gi)

@@ -785,13 +785,14 @@ class BatchPreparer:
         self._jobs, self._last = jobs, None
         return gi, jobs
 
-    def flush_loglike(self, d, w, out, tile_const=None):
+    def flush_loglike(self, d, w, out, tile_const=None, out_off=0):
         """flush() and sum_loglike() of the collected walkers in one native call
         (efd_fused_group: staging, upload, the staged event, the preparation and the fused sum
         on the next group's stream); returns the group index. The fused likelihood's per-group
         host path (Likelihood._get_ll_fused): the same launches on the same stream as flush()
         then sum_loglike(gi, ..., G's stream), bitwise the same logL, in one ctypes
-        transition instead of five. d, w: checked once per (d, w) pair."""
+        transition instead of five. d, w: checked once per pair of buffers. The logL go to
+        out[out_off : out_off + n]."""
         import ctypes
         torch = _torch()
         pend, self._pending = self._pending, []
@@ -818,29 +819,46 @@ class BatchPreparer:
         _, _, sym, _, k0, acc = pend[0]
         if any(p[2] != sym or p[4] != k0 or p[5] != acc for p in pend):
             raise ValueError("flush: grid symmetry, k0 and accumulate must agree in a group")
-        key = (id(d), id(w), nf - k0)
+        dp, wp = d.data_ptr(), w.data_ptr()
+        key = (dp, wp, nf - k0)
         if self._ll_checked != key:
             _check_ll_io(torch, d, w, out, nf - k0, n)
             self._ll_checked = key
-        elif out.dtype != torch.float64 or out.numel() < n or not out.is_contiguous():
-            raise ValueError(f"flush_loglike: out float64 [>= {n}], contiguous")
-        tmpl = _lib.ModesumArgs(freq=freq.data_ptr(), nf=nf, grid_symmetric=1 if sym else 0,
-                                caustic=CAUSTIC_MODES[self.caustic],
-                                accumulate=1 if acc else 0, k0=k0)
+        if out.dtype != torch.float64 or out.numel() < out_off + n or not out.is_contiguous():
+            raise ValueError(f"flush_loglike: out float64 [>= {out_off + n}], contiguous")
+        tkey = (freq.data_ptr(), nf, sym, acc, k0)
+        tmpl = G.get("tmpl")
+        if tmpl is None or tmpl[0] != tkey:
+            tmpl = G["tmpl"] = (tkey, _lib.ModesumArgs(
+                freq=freq.data_ptr(), nf=nf, grid_symmetric=1 if sym else 0,
+                caustic=CAUSTIC_MODES[self.caustic], accumulate=1 if acc else 0, k0=k0))
+        tmpl = tmpl[1]
         src, shape, scale, keep = self._sources(pend)
         pw, pb, engines = G["pw"], G["pb"], G["engines"]
         dev = freq.device
-        for i, (nt_i, K_i) in enumerate(shape.tolist()):
-            eng = engines[i]
-            nbytes = _WS_BYTES.get((nt_i, K_i, nf))
-            if nbytes is None or eng._ws is None or eng._ws_cap < nbytes or eng._ws_dev != dev:
-                eng._workspace(nt_i, K_i, nf, dev, stream=st)   # sized, or grown, here
-            pw[i] = eng._ws_ptr
-            pb[i] = eng._ws_cap
-            eng._last_args = G["A_i"][i]
+        # the workspaces: sized for the group's largest (N_t, K) (the layout grows with both),
+        # so once every engine holds that much the pointer and size arrays stand as they are
+        # and no per-walker step is needed
+        kb = (int(shape[:, 0].max()), int(shape[:, 1].max()), nf)
+        nbmax = _WS_BYTES.get(kb)
+        if nbmax is None:
+            nbmax = int(self.lib.efd_modesum_workspace_bytes(*kb))
+            if nbmax == 0:
+                raise _lib.EFDError("efd_modesum_workspace_bytes rejected the shape")
+            _WS_BYTES[kb] = nbmax
+        floor = G.get("ws_floor")
+        if floor is None or floor[0] != dev or floor[1] < nbmax or floor[2] < n:
+            for i in range(n):
+                eng = engines[i]
+                if eng._ws is None or eng._ws_cap < nbmax or eng._ws_dev != dev:
+                    eng._workspace(kb[0], kb[1], nf, dev, stream=st)   # sized, or grown
+                pw[i] = eng._ws_ptr
+                pb[i] = eng._ws_cap
+                eng._last_args = G["A_i"][i]
+            G["ws_floor"] = (dev, min(engines[i]._ws_cap for i in range(n)), n)
         total = ctypes.c_size_t(0)
-        dp, wp = torch.view_as_real(d).data_ptr(), w.data_ptr()
         tcp = tile_const.data_ptr() if tile_const is not None else None
+        op = out.data_ptr() + 8 * out_off
         for attempt in range(2):
             pin, dbuf = G["pin"], G["dbuf"]
             rc = self.lib.efd_fused_group(
@@ -848,7 +866,7 @@ class BatchPreparer:
                 dbuf.data_ptr() if dbuf is not None else None,
                 dbuf.numel() if dbuf is not None else 0, n, src.ctypes.data, shape.ctypes.data,
                 scale.ctypes.data, ctypes.byref(tmpl), G["args_ptr"], G["pw_ptr"], G["pb_ptr"],
-                dp, wp, tcp, out.data_ptr(), G["pin_done"].cuda_event, st.cuda_stream,
+                dp, wp, tcp, op, G["pin_done"].cuda_event, st.cuda_stream,
                 ctypes.byref(total))
             if rc == _lib.EFD_OK:
                 break

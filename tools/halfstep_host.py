@@ -68,8 +68,8 @@ def fused(self, tm, params, args, kwargs, out):
             p0 = B._pending[0]
             sst = B.groups[B._next]["stream"]
             tcon = self._tile_constants({"freq": p0[1], "k0": p0[4]}, sst, F)
-            used.append(B.flush_loglike(self._d, self._w_templ, out[g0:g0 + len(B._pending)],
-                                        tile_const=tcon))
+            used.append(B.flush_loglike(self._d, self._w_templ, out, tile_const=tcon,
+                                        out_off=g0))
             acc["flush+sum (native)"] += pc() - tb
             continue
         gi, jobs = B.flush()
