@@ -183,6 +183,8 @@ static_assert(offsetof(Item, dtj) == offsetof(Item, fd) + 24 &&
               offsetof(Item, fdd) == offsetof(Item, fd) + 32 &&
               offsetof(Item, jser) == offsetof(Item, fd) + 8 * (ENV_DEG + 1),
               "envelope coefficients: fd, dtj, fdd contiguous");
+// envelope records store A(w) times the sum's cosine constant (COS_A below; static_assert there)
+constexpr double ENV_AMP_SCALE = 1.000000000029531;
 __host__ __device__ __forceinline__ double* env_of(Item* it) {
     return reinterpret_cast<double*>(reinterpret_cast<char*>(it) + offsetof(Item, fd));
 }
@@ -1792,8 +1794,10 @@ __device__ bool build_item(
     if (env && (it.fdneg & 2) && ymin_rec >= ENV_MIN_Y && evals > 0) {
         EnvFit E;
         if (env_fit(it.fd, gq, it.dtj, (it.fdneg & 1) != 0, E)) {
+            // A's coefficients times the cosine polynomial's constant (sincos_tab_amp's cos r =
+            // COS_A - r^2/2 then costs one FMA on the scaled amplitude)
             double* e = env_of(&it);
-            for (int c = 0; c <= ENV_DEG; ++c) e[c] = E.a[c];
+            for (int c = 0; c <= ENV_DEG; ++c) e[c] = E.a[c] * ENV_AMP_SCALE;
             for (int c = 0; c < 4; ++c) it.ph[c] -= E.th[c];
             it.jser = 0;   // the sum's envelope class
             return true;
@@ -2287,6 +2291,7 @@ constexpr int SCTAB = 512;
 // fma(-v, v, COS_A) = COS_A rho to 2e-20).
 constexpr double COS_A = 1.000000000029531;
 constexpr double COS_B = -0.5;
+static_assert(COS_A == ENV_AMP_SCALE, "envelope amplitudes carry COS_A (k_items)");
 __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* __restrict__ tab,
                                            double& s, double& c, double extra = 0.0,
                                            bool use_extra = false, double extra_scale = 1.0,
@@ -2316,9 +2321,12 @@ __device__ __forceinline__ void sincos_tab(double x, int shift, const double2* _
 
 // amp (sin, cos)(x + shift pi/256) for the envelope records, in the tangent form: with the
 // table's (sin a, cos a), sin(a + r) = cos r (sin a + cos a tan r) and cos(a + r) =
-// cos r (cos a - sin a tan r), so the amplitude multiplies cos r once instead of both outputs
-// (12 FP64 operations against sincos_tab's 11 plus the two products). tan r = r + r^3/3
-// (dropped 2 r^5/15 <= 1.1e-12 at |r| <= pi/512), cos r as sincos_tab's minimax COS_A - z/2.
+// cos r (cos a - sin a tan r), so the amplitude multiplies cos r once instead of both outputs.
+// tan r = r + r^3/3 (dropped 2 r^5/15 <= 1.1e-12 at |r| <= pi/512); cos r as sincos_tab's minimax
+// COS_A - r^2/2, with COS_A already in the record's amplitude (k_items: amp = COS_A A) so that
+// amp cos r = amp (1 + h), h = -r^2/2 (the product's -1/2 from the output modifier, IEEE mode
+// off in k_modesum as for rsqrt_pos_sum; COS_A h against h: 6e-16 relative). 11 FP64 operations
+// against sincos_tab's 11 plus the two products.
 __device__ __forceinline__ void sincos_tab_amp(double x, int shift,
                                                const double2* __restrict__ tab, double amp,
                                                double& wr, double& wi) {
@@ -2331,9 +2339,10 @@ __device__ __forceinline__ void sincos_tab_amp(double x, int shift,
     const int qi = __double2loint(qs);
     const uint32_t off = ((uint32_t)qi * 16u + (uint32_t)shift * 16u) & (uint32_t)(16 * (SCTAB - 1));
     const double2 t = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
-    const double z = r * r;
-    const double tr = fma(r * z, 0.3333333333333333, r);
-    const double ac = amp * fma(z, COS_B, COS_A);
+    double h;
+    asm("v_mul_f64 %0, -%1, %2 div:2" : "=v"(h) : "v"(r), "v"(r));
+    const double tr = fma(r * h, -0.6666666666666666, r);
+    const double ac = fma(amp, h, amp);
     wi = ac * fma(t.y, tr, t.x);
     wr = ac * fma(-t.x, tr, t.y);
 }
@@ -2655,7 +2664,7 @@ __device__ __forceinline__ void spa_simple3(const Item* __restrict__ it, double 
 }
 // Envelope records (k_items, env_fit.inc; Item::jser = 0, always certified safe): the phase with
 // theta already in the record's phase cubic and the amplitude A(w) = rho / sqrt|F'| from its
-// degree-ENV_DEG polynomial, for the NB bins of the lane. 27 FP64 operations per bin instead of
+// degree-ENV_DEG polynomial, for the NB bins of the lane. 26 FP64 operations per bin instead of
 // spa_simple's 36 (the sin/cos in sincos_tab_amp's tangent form): no F', F'' quadratics, no 1/sqrt|F'| Newton step, no 1/|y| and no angle or rho
 // fold in the sin/cos.
 // MASK: the record covers the wave's chunk only partly; lanes outside am[i] get A = +0 (flushed).
